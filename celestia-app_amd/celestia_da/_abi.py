@@ -1,0 +1,109 @@
+"""ctypes binding of include/dagpu.h (libdagpu.so, built for gfx950).
+
+The product path: every compute call goes through the HIP library.  If the
+library is missing this module raises -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_PKG_ROOT, "libdagpu.so")
+
+SHARE_SIZE = 512
+NAMESPACE_SIZE = 29
+ROOT_SIZE = 90
+HASH_SIZE = 32
+
+OK = 0
+ERR_NOT_POW2 = -1
+ERR_NOT_SQUARE = -2
+ERR_SHARE_SIZE = -3
+ERR_PUSH_ORDER = -4
+ERR_TOO_FEW_SHARDS = -5
+ERR_UNREPAIRABLE = -6
+ERR_BYZANTINE = -7
+ERR_BAD_ROOTS = -8
+ERR_ARG = -9
+ERR_DEVICE = -10
+ERR_UNSUPPORTED = -11
+
+# Every symbol include/dagpu.h declares (checked by tests/test_abi_cpu.py).
+EXPORTS = (
+    "dagpu_version",
+    "dagpu_init",
+    "dagpu_destroy",
+    "dagpu_last_error",
+    "dagpu_extend_shares",
+    "dagpu_extend_batch",
+    "dagpu_workspace_size",
+    "dagpu_extend_batch_device",
+    "dagpu_extend_rs_device",
+    "dagpu_roots_device",
+    "dagpu_roots",
+    "dagpu_encode",
+    "dagpu_decode",
+    "dagpu_repair_batch_device",
+    "dagpu_repair",
+    "dagpu_profile_enable",
+    "dagpu_profile_read",
+    "dagpu_dah_hash",
+)
+
+PROFILE_KERNELS = ("rs_row", "rs_col", "nmt_leaves", "nmt_trees", "dah", "decode")
+
+_lib = None
+
+u8p = ctypes.POINTER(ctypes.c_uint8)
+u32p = ctypes.POINTER(ctypes.c_uint32)
+i32p = ctypes.POINTER(ctypes.c_int32)
+vp = ctypes.c_void_p
+sz = ctypes.c_size_t
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"HIP extension not built: {LIB_PATH} missing (run __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        L.dagpu_version.restype = ctypes.c_int
+        L.dagpu_init.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+        L.dagpu_destroy.argtypes = [vp]
+        L.dagpu_destroy.restype = None
+        L.dagpu_last_error.argtypes = [vp]
+        L.dagpu_last_error.restype = ctypes.c_char_p
+        L.dagpu_extend_shares.argtypes = [vp, vp, sz, sz, vp, vp, vp, vp]
+        L.dagpu_extend_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
+        L.dagpu_workspace_size.argtypes = [ctypes.c_uint32, sz]
+        L.dagpu_workspace_size.restype = sz
+        L.dagpu_extend_batch_device.argtypes = [vp, ctypes.c_uint32, sz, vp, vp, vp, vp, vp, vp,
+                                                vp, vp]
+        L.dagpu_extend_rs_device.argtypes = [vp, ctypes.c_uint32, sz, vp, vp, vp]
+        L.dagpu_roots_device.argtypes = [vp, ctypes.c_uint32, sz, vp, vp, vp, vp, vp, vp, vp]
+        L.dagpu_roots.argtypes = [vp, ctypes.c_uint32, vp, vp, vp, vp]
+        L.dagpu_encode.argtypes = [vp, ctypes.c_uint32, sz, sz, vp, vp]
+        L.dagpu_decode.argtypes = [vp, ctypes.c_uint32, sz, sz, vp, vp]
+        L.dagpu_repair_batch_device.argtypes = [vp, ctypes.c_uint32, sz, vp, vp, vp, vp, vp, vp,
+                                                vp, vp]
+        L.dagpu_repair.argtypes = [vp, ctypes.c_uint32, vp, vp, vp, vp]
+        L.dagpu_dah_hash.argtypes = [vp, vp, sz, vp]
+        L.dagpu_profile_enable.argtypes = [vp, ctypes.c_int]
+        L.dagpu_profile_read.argtypes = [vp, vp, vp, ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+def addr(buf) -> int:
+    """Address of a numpy array / bytearray / torch tensor (device or host)."""
+    if buf is None:
+        return 0
+    if hasattr(buf, "data_ptr"):
+        return buf.data_ptr()
+    if hasattr(buf, "ctypes"):
+        return buf.ctypes.data
+    if isinstance(buf, bytearray):
+        return ctypes.addressof((ctypes.c_char * len(buf)).from_buffer(buf))
+    raise TypeError(f"unsupported buffer type {type(buf)}")

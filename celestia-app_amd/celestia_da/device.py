@@ -1,0 +1,67 @@
+"""Device-resident batched pipeline (block replay / sync batches).
+
+PyTorch is used only as the device allocator and stream provider; the work is
+the HIP kernels behind dagpu_extend_batch_device (include/dagpu.h).  Inputs are
+already resident in HBM and only the roots/DAH (or nothing) come back.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _abi
+from .da import Context, DAError, default_context
+
+ROOT = _abi.ROOT_SIZE
+
+
+def _stream_handle(stream: Optional[torch.cuda.Stream]) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+class DeviceSquares:
+    """n squares of width k resident on one GPU.
+
+    ods:  (n, k*k*512) uint8   eds: (n, 4k^2*512) uint8
+    row_roots/col_roots: (n, 2k, 90)   dah: (n, 32)   status: (n,) int32
+    """
+
+    def __init__(self, k: int, n: int, device: int = 0, ctx: Optional[Context] = None,
+                 with_ods: bool = True):
+        self.k, self.n = int(k), int(n)
+        self.ctx = ctx or default_context()
+        dev = torch.device("cuda", device)
+        w = 2 * self.k
+        self.ods = torch.empty((n, self.k * self.k * 512), dtype=torch.uint8, device=dev) if with_ods else None
+        self.eds = torch.empty((n, w * w * 512), dtype=torch.uint8, device=dev)
+        self.row_roots = torch.empty((n, w, ROOT), dtype=torch.uint8, device=dev)
+        self.col_roots = torch.empty((n, w, ROOT), dtype=torch.uint8, device=dev)
+        self.dah = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+        self.status = torch.zeros((n,), dtype=torch.int32, device=dev)
+        ws = self.ctx._L.dagpu_workspace_size(self.k, self.n)
+        self.workspace = torch.empty((ws,), dtype=torch.uint8, device=dev)
+
+    def _ck(self, rc: int) -> None:
+        if rc != 0:
+            raise DAError(rc, self.ctx.last_error())
+
+    def extend(self, stream: Optional[torch.cuda.Stream] = None) -> None:
+        """ODS -> EDS -> roots -> DAH, enqueued on `stream` (no sync)."""
+        L = self.ctx._L
+        self._ck(L.dagpu_extend_batch_device(
+            self.ctx.handle, self.k, self.n, _abi.addr(self.ods), _abi.addr(self.eds),
+            _abi.addr(self.row_roots), _abi.addr(self.col_roots), _abi.addr(self.dah),
+            _abi.addr(self.status), _abi.addr(self.workspace), _stream_handle(stream)))
+
+    def extend_rs(self, stream: Optional[torch.cuda.Stream] = None) -> None:
+        self._ck(self.ctx._L.dagpu_extend_rs_device(
+            self.ctx.handle, self.k, self.n, _abi.addr(self.ods), _abi.addr(self.eds),
+            _stream_handle(stream)))
+
+    def roots(self, stream: Optional[torch.cuda.Stream] = None) -> None:
+        self._ck(self.ctx._L.dagpu_roots_device(
+            self.ctx.handle, self.k, self.n, _abi.addr(self.eds), _abi.addr(self.row_roots),
+            _abi.addr(self.col_roots), _abi.addr(self.dah), _abi.addr(self.status),
+            _abi.addr(self.workspace), _stream_handle(stream)))

@@ -1,0 +1,50 @@
+"""Synthetic inputs of the shape the reference benchmarks/tests use.
+
+random_blob_square: "random-namespace blob shares" as produced by
+test/util/testfactory/common.go:36-46 (GenerateRandNamespacedRawData): 512
+random bytes per share, bytes [0:29] overwritten by a random blob namespace
+(version 0, 18 zero bytes, 10 random bytes, not reserved --
+pkg/namespace/random_blob.go:22-30), then all shares sorted bytewise.
+The PRNG is numpy PCG64 with the given seed (the reference uses tmrand).
+
+constant_square: pkg/da/data_availability_header_test.go:247-263 generateShares
+(namespace MustNewV0([1]*10) followed by 0xFF*483, all shares identical).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+SHARE = 512
+
+
+def random_blob_square(k: int, seed: int) -> np.ndarray:
+    """(k*k, 512) uint8, sorted bytewise (so every Q0 row/column is NMT-ordered)."""
+    rng = np.random.default_rng(seed)
+    n = k * k
+    s = rng.integers(0, 256, size=(n, SHARE), dtype=np.uint8)
+    s[:, 0] = 0          # namespace version 0
+    s[:, 1:19] = 0       # NamespaceVersionZeroPrefix (18 zero bytes)
+    # reserved iff ID <= 0x00..00FF: the first 9 of the 10 random bytes all zero
+    reserved = ~s[:, 19:28].any(axis=1)
+    s[reserved, 19] = 1
+    return sort_shares(s)
+
+
+def sort_shares(s: np.ndarray) -> np.ndarray:
+    """Bytewise lexicographic sort of rows (bytes.Compare order)."""
+    # big-endian 64-bit words compare like the bytes they hold
+    words = s.view(">u8")
+    order = np.lexsort(words.T[::-1])
+    return np.ascontiguousarray(s[order])
+
+
+def constant_square(k: int) -> np.ndarray:
+    ns = bytes([0]) + bytes(18) + bytes([1] * 10)
+    share = ns + b"\xff" * (SHARE - len(ns))
+    return np.tile(np.frombuffer(share, np.uint8), (k * k, 1))
+
+
+def tail_padding_square(k: int) -> np.ndarray:
+    ns = b"\xff" * 28 + b"\xfe"
+    share = ns + b"\x01" + b"\x00" * 4 + b"\x00" * (SHARE - 34)
+    return np.tile(np.frombuffer(share, np.uint8), (k * k, 1))

@@ -1,0 +1,516 @@
+// dagpu.cpp -- C-ABI host runtime for the MI355X DA hot path (include/dagpu.h).
+//
+// Mirrors the reference entry points:
+//   da.ExtendShares            pkg/da/data_availability_header.go:65-75
+//   da.NewDataAvailabilityHeader / Hash   :44-63, :92-108
+//   rsmt2d.ComputeExtendedDataSquare (3k Encode calls) via the Leopard codec
+//   appconsts.DefaultCodec     pkg/appconsts/global_consts.go:92
+// The pipeline per batch of same-k squares (all on one HIP stream):
+//   row encode Q0 -> Q1 (+ Q0 placement)  |  column encode [Q0|Q1] -> [Q2|Q3]
+//   leaf digests (each cell once)  |  row+col NMT trees  |  DAH
+// The EDS never leaves HBM unless the caller asks for it.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <cmath>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/dagpu.h"
+#include "host_sha256.hpp"
+#include "kernels.hpp"
+
+using namespace dagpu;
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= n) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipSuccess) n = bytes;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+struct ProfRec {
+  int id;
+  hipEvent_t a, b;
+};
+
+struct dagpu_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  std::string err;
+  DevBuf ods, eds, rr, cr, dah, status, ws;
+  // profiling
+  bool prof = false;
+  std::mutex prof_mu;
+  std::vector<ProfRec> pending;
+  std::vector<hipEvent_t> pool;
+  double prof_ms[DAGPU_PROFILE_KERNELS] = {};
+  uint64_t prof_n[DAGPU_PROFILE_KERNELS] = {};
+};
+
+namespace {
+
+constexpr size_t kSS = kShareSize;
+
+bool is_pow2(uint64_t v) { return v != 0 && (v & (v - 1)) == 0; }
+
+int set_err(dagpu_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+int hip_fail(dagpu_ctx* c, hipError_t e, const char* what) {
+  char buf[256];
+  snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+  return set_err(c, DAGPU_ERR_DEVICE, buf);
+}
+
+#define HIP_TRY(ctx, expr)                                   \
+  do {                                                       \
+    hipError_t e_ = (expr);                                  \
+    if (e_ != hipSuccess) return hip_fail((ctx), e_, #expr); \
+  } while (0)
+
+hipEvent_t pool_get(dagpu_ctx* c) {
+  if (!c->pool.empty()) {
+    hipEvent_t e = c->pool.back();
+    c->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+// RAII bracket: records events around one kernel launch when profiling is on.
+struct ProfScope {
+  dagpu_ctx* c;
+  int id;
+  hipStream_t s;
+  hipEvent_t a = nullptr, b = nullptr;
+  ProfScope(dagpu_ctx* c_, int id_, hipStream_t s_) : c(c_), id(id_), s(s_) {
+    if (!c->prof) return;
+    std::lock_guard<std::mutex> g(c->prof_mu);
+    a = pool_get(c);
+    b = pool_get(c);
+    (void)hipEventRecord(a, s);
+  }
+  ~ProfScope() {
+    if (!a) return;
+    (void)hipEventRecord(b, s);
+    std::lock_guard<std::mutex> g(c->prof_mu);
+    c->pending.push_back({id, a, b});
+  }
+};
+
+size_t eds_bytes(uint64_t k) { return 4ull * k * k * kSS; }
+size_t ods_bytes(uint64_t k) { return 1ull * k * k * kSS; }
+
+// RS extension of n squares (uniform k), device pointers.
+int enqueue_rs(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_ods, uint8_t* d_eds,
+               hipStream_t s) {
+  const long w = 2L * k;
+  const long esq = (long)eds_bytes(k);
+  EncodeArgs ra{};
+  // Row pass: vector r = row r of Q0 -> Q1 (and copy Q0 into place).
+  if (d_ods) {
+    ra.in = d_ods;
+    ra.in_sq_stride = (long)ods_bytes(k);
+    ra.in_vec_stride = (long)k * kSS;
+    ra.in_shard_stride = kSS;
+    ra.copy = d_eds;
+    ra.copy_sq_stride = esq;
+    ra.copy_vec_stride = w * kSS;
+    ra.copy_shard_stride = kSS;
+  } else {
+    ra.in = d_eds;
+    ra.in_sq_stride = esq;
+    ra.in_vec_stride = w * kSS;
+    ra.in_shard_stride = kSS;
+    ra.copy = nullptr;
+  }
+  ra.out = d_eds + (long)k * kSS;
+  ra.out_sq_stride = esq;
+  ra.out_vec_stride = w * kSS;
+  ra.out_shard_stride = kSS;
+  ra.nsq = (long)n;
+  ra.nvec = k;
+  ra.nchunk = 1;
+  ra.shard_bytes = kSS;
+  {
+    ProfScope p(ctx, 0, s);
+    HIP_TRY(ctx, launch_leo8_encode((int)k, ra, s));
+  }
+  // Column pass: vector c = column c of [Q0|Q1] -> [Q2|Q3].
+  EncodeArgs ca{};
+  ca.in = d_eds;
+  ca.in_sq_stride = esq;
+  ca.in_vec_stride = kSS;
+  ca.in_shard_stride = w * kSS;
+  ca.out = d_eds + (long)k * w * kSS;
+  ca.out_sq_stride = esq;
+  ca.out_vec_stride = kSS;
+  ca.out_shard_stride = w * kSS;
+  ca.copy = nullptr;
+  ca.nsq = (long)n;
+  ca.nvec = w;
+  ca.nchunk = 1;
+  ca.shard_bytes = kSS;
+  {
+    ProfScope p(ctx, 1, s);
+    HIP_TRY(ctx, launch_leo8_encode((int)k, ca, s));
+  }
+  return DAGPU_OK;
+}
+
+int enqueue_roots(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_eds, uint8_t* d_rr,
+                  uint8_t* d_cr, uint8_t* d_dah, int32_t* d_status, void* d_ws, hipStream_t s) {
+  SquareArgs sa{};
+  sa.eds = d_eds;
+  sa.eds_sq_stride = (long)eds_bytes(k);
+  sa.digests = (uint8_t*)d_ws;
+  sa.row_roots = d_rr;
+  sa.col_roots = d_cr;
+  sa.dah = d_dah;
+  sa.status = d_status;
+  sa.k = (int)k;
+  sa.nsq = (long)n;
+  HIP_TRY(ctx, hipMemsetAsync(d_status, 0, n * sizeof(int32_t), s));
+  {
+    ProfScope p(ctx, 2, s);
+    HIP_TRY(ctx, launch_nmt_leaves(sa, s));
+  }
+  {
+    ProfScope p(ctx, 3, s);
+    HIP_TRY(ctx, launch_nmt_trees(sa, s));
+  }
+  {
+    ProfScope p(ctx, 4, s);
+    HIP_TRY(ctx, launch_dah(sa, s));
+  }
+  return DAGPU_OK;
+}
+
+int check_k(dagpu_ctx* ctx, uint64_t k) {
+  if (!is_pow2(k)) return set_err(ctx, DAGPU_ERR_ARG, "square width must be a power of two");
+  if (k > 128) {
+    return set_err(ctx, DAGPU_ERR_UNSUPPORTED,
+                   "k > 128 (GF(2^16) Leopard) is not implemented in this build");
+  }
+  return DAGPU_OK;
+}
+
+// Runs one uniform-k group from host memory.  Caller holds ctx->mu.
+int run_group_host(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* ods, uint8_t* eds_out,
+                   uint8_t* rr, uint8_t* cr, uint8_t* dah, int32_t* status) {
+  int rc = check_k(ctx, k);
+  if (rc) return rc;
+  const size_t w = 2 * (size_t)k;
+  hipStream_t s = ctx->stream;
+  HIP_TRY(ctx, ctx->ods.ensure(ods_bytes(k) * n));
+  HIP_TRY(ctx, ctx->eds.ensure(eds_bytes(k) * n));
+  HIP_TRY(ctx, ctx->rr.ensure(w * kNodeSize * n));
+  HIP_TRY(ctx, ctx->cr.ensure(w * kNodeSize * n));
+  HIP_TRY(ctx, ctx->dah.ensure(32 * n));
+  HIP_TRY(ctx, ctx->status.ensure(sizeof(int32_t) * n));
+  HIP_TRY(ctx, ctx->ws.ensure(dagpu_workspace_size(k, n)));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->ods.p, ods, ods_bytes(k) * n, hipMemcpyHostToDevice, s));
+  rc = enqueue_rs(ctx, k, n, (const uint8_t*)ctx->ods.p, (uint8_t*)ctx->eds.p, s);
+  if (rc) return rc;
+  rc = enqueue_roots(ctx, k, n, (const uint8_t*)ctx->eds.p, (uint8_t*)ctx->rr.p,
+                     (uint8_t*)ctx->cr.p, (uint8_t*)ctx->dah.p, (int32_t*)ctx->status.p,
+                     ctx->ws.p, s);
+  if (rc) return rc;
+  if (eds_out)
+    HIP_TRY(ctx, hipMemcpyAsync(eds_out, ctx->eds.p, eds_bytes(k) * n, hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipMemcpyAsync(rr, ctx->rr.p, w * kNodeSize * n, hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipMemcpyAsync(cr, ctx->cr.p, w * kNodeSize * n, hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipMemcpyAsync(dah, ctx->dah.p, 32 * n, hipMemcpyDeviceToHost, s));
+  std::vector<int32_t> st(n);
+  HIP_TRY(ctx, hipMemcpyAsync(st.data(), ctx->status.p, sizeof(int32_t) * n,
+                              hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipStreamSynchronize(s));
+  int first = DAGPU_OK;
+  for (size_t i = 0; i < n; i++) {
+    int v = (st[i] & kStatusPushOrder) ? DAGPU_ERR_PUSH_ORDER : DAGPU_OK;
+    if (status) status[i] = v;
+    if (v && !first) first = v;
+  }
+  if (first) set_err(ctx, first, "invalid push order: namespaces of original data square are not sorted");
+  return first;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dagpu_version(void) { return 100; }
+
+int dagpu_init(int device, dagpu_ctx** out) {
+  if (!out) return DAGPU_ERR_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return DAGPU_ERR_DEVICE;
+  if (device < 0 || device >= ndev) return DAGPU_ERR_ARG;
+  if (hipSetDevice(device) != hipSuccess) return DAGPU_ERR_DEVICE;
+  dagpu_ctx* c = new dagpu_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return DAGPU_ERR_DEVICE;
+  }
+  *out = c;
+  return DAGPU_OK;
+}
+
+void dagpu_destroy(dagpu_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  c->ods.release(); c->eds.release(); c->rr.release(); c->cr.release();
+  c->dah.release(); c->status.release(); c->ws.release();
+  for (auto& r : c->pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+  for (auto e : c->pool) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* dagpu_last_error(dagpu_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+size_t dagpu_workspace_size(uint32_t k, size_t n) {
+  return (size_t)4 * k * k * kDigest * n + 256;
+}
+
+int dagpu_extend_shares(dagpu_ctx* ctx, const uint8_t* shares, size_t n_shares,
+                        size_t share_size, uint8_t* eds_out, uint8_t* row_roots,
+                        uint8_t* col_roots, uint8_t* dah) {
+  if (!ctx || !row_roots || !col_roots || !dah) return DAGPU_ERR_ARG;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  (void)hipSetDevice(ctx->device);
+  // pkg/da/data_availability_header.go:67-69
+  if (!is_pow2(n_shares)) {
+    return set_err(ctx, DAGPU_ERR_NOT_POW2,
+                   "number of shares is not a power of 2: got " + std::to_string(n_shares));
+  }
+  // SquareSize (:205-207) then rsmt2d newDataSquare's square check
+  const uint64_t k = (uint64_t)std::llround(std::ceil(std::sqrt((double)n_shares)));
+  if (k * k != n_shares) return set_err(ctx, DAGPU_ERR_NOT_SQUARE, "number of chunks must be a square number");
+  if (share_size != kSS) {
+    return set_err(ctx, DAGPU_ERR_SHARE_SIZE,
+                   "share size must be " + std::to_string(kSS) + " bytes (appconsts.ShareSize)");
+  }
+  if (!shares) return DAGPU_ERR_ARG;
+  int32_t st = 0;
+  return run_group_host(ctx, (uint32_t)k, 1, shares, eds_out, row_roots, col_roots, dah, &st);
+}
+
+int dagpu_extend_batch(dagpu_ctx* ctx, const uint8_t* ods, const uint32_t* k, size_t n,
+                       uint8_t* eds_or_null, uint8_t* row_roots, uint8_t* col_roots,
+                       uint8_t* dah, int32_t* status) {
+  if (!ctx || (n && (!ods || !k || !row_roots || !col_roots || !dah))) return DAGPU_ERR_ARG;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  (void)hipSetDevice(ctx->device);
+  // per-square offsets in the packed arrays
+  std::vector<size_t> o_ods(n), o_eds(n), o_root(n);
+  size_t a = 0, b = 0, c = 0;
+  for (size_t i = 0; i < n; i++) {
+    int rc = check_k(ctx, k[i]);
+    if (rc) {
+      if (status) status[i] = rc;
+      return rc;
+    }
+    o_ods[i] = a; o_eds[i] = b; o_root[i] = c;
+    a += ods_bytes(k[i]); b += eds_bytes(k[i]); c += 2ull * k[i] * kNodeSize;
+  }
+  // group consecutive runs of equal k (block replay batches are mostly uniform)
+  int first = DAGPU_OK;
+  size_t i = 0;
+  std::vector<int32_t> st;
+  while (i < n) {
+    size_t j = i;
+    while (j < n && k[j] == k[i]) j++;
+    st.assign(j - i, 0);
+    int rc = run_group_host(ctx, k[i], j - i, ods + o_ods[i],
+                            eds_or_null ? eds_or_null + o_eds[i] : nullptr,
+                            row_roots + o_root[i], col_roots + o_root[i], dah + 32 * i, st.data());
+    if (rc && rc != DAGPU_ERR_PUSH_ORDER) return rc;
+    for (size_t t = i; t < j; t++) {
+      if (status) status[t] = st[t - i];
+      if (st[t - i] && !first) first = st[t - i];
+    }
+    i = j;
+  }
+  return first;
+}
+
+int dagpu_extend_rs_device(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_ods,
+                           uint8_t* d_eds, void* stream) {
+  if (!ctx || !d_eds) return DAGPU_ERR_ARG;
+  int rc = check_k(ctx, k);
+  if (rc) return rc;
+  return enqueue_rs(ctx, k, n, d_ods, d_eds, (hipStream_t)stream);
+}
+
+int dagpu_roots_device(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_eds,
+                       uint8_t* d_row_roots, uint8_t* d_col_roots, uint8_t* d_dah,
+                       int32_t* d_status, void* d_workspace, void* stream) {
+  if (!ctx || !d_eds || !d_row_roots || !d_col_roots || !d_dah || !d_status || !d_workspace)
+    return DAGPU_ERR_ARG;
+  int rc = check_k(ctx, k);
+  if (rc) return rc;
+  return enqueue_roots(ctx, k, n, d_eds, d_row_roots, d_col_roots, d_dah, d_status, d_workspace,
+                       (hipStream_t)stream);
+}
+
+int dagpu_extend_batch_device(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_ods,
+                              uint8_t* d_eds, uint8_t* d_row_roots, uint8_t* d_col_roots,
+                              uint8_t* d_dah, int32_t* d_status, void* d_workspace,
+                              void* stream) {
+  int rc = dagpu_extend_rs_device(ctx, k, n, d_ods, d_eds, stream);
+  if (rc) return rc;
+  return dagpu_roots_device(ctx, k, n, d_eds, d_row_roots, d_col_roots, d_dah, d_status,
+                            d_workspace, stream);
+}
+
+int dagpu_roots(dagpu_ctx* ctx, uint32_t k, const uint8_t* eds, uint8_t* row_roots,
+                uint8_t* col_roots, uint8_t* dah) {
+  if (!ctx || !eds || !row_roots || !col_roots || !dah) return DAGPU_ERR_ARG;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  (void)hipSetDevice(ctx->device);
+  int rc = check_k(ctx, k);
+  if (rc) return rc;
+  const size_t w = 2 * (size_t)k;
+  hipStream_t s = ctx->stream;
+  HIP_TRY(ctx, ctx->eds.ensure(eds_bytes(k)));
+  HIP_TRY(ctx, ctx->rr.ensure(w * kNodeSize));
+  HIP_TRY(ctx, ctx->cr.ensure(w * kNodeSize));
+  HIP_TRY(ctx, ctx->dah.ensure(32));
+  HIP_TRY(ctx, ctx->status.ensure(sizeof(int32_t)));
+  HIP_TRY(ctx, ctx->ws.ensure(dagpu_workspace_size(k, 1)));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->eds.p, eds, eds_bytes(k), hipMemcpyHostToDevice, s));
+  rc = enqueue_roots(ctx, k, 1, (const uint8_t*)ctx->eds.p, (uint8_t*)ctx->rr.p,
+                     (uint8_t*)ctx->cr.p, (uint8_t*)ctx->dah.p, (int32_t*)ctx->status.p, ctx->ws.p, s);
+  if (rc) return rc;
+  int32_t st = 0;
+  HIP_TRY(ctx, hipMemcpyAsync(row_roots, ctx->rr.p, w * kNodeSize, hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipMemcpyAsync(col_roots, ctx->cr.p, w * kNodeSize, hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipMemcpyAsync(dah, ctx->dah.p, 32, hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipMemcpyAsync(&st, ctx->status.p, sizeof st, hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipStreamSynchronize(s));
+  if (st & kStatusPushOrder)
+    return set_err(ctx, DAGPU_ERR_PUSH_ORDER, "invalid push order: namespaces of original data square are not sorted");
+  return DAGPU_OK;
+}
+
+int dagpu_encode(dagpu_ctx* ctx, uint32_t k, size_t nvec, size_t shard_size,
+                 const uint8_t* data, uint8_t* parity) {
+  if (!ctx || (nvec && (!data || !parity))) return DAGPU_ERR_ARG;
+  if (shard_size == 0 || shard_size % 64)
+    return set_err(ctx, DAGPU_ERR_SHARE_SIZE, "shard size must be a multiple of 64");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  (void)hipSetDevice(ctx->device);
+  int rc = check_k(ctx, k);
+  if (rc) return rc;
+  if (nvec == 0) return DAGPU_OK;
+  const size_t bytes = (size_t)k * shard_size * nvec;
+  hipStream_t s = ctx->stream;
+  HIP_TRY(ctx, ctx->ods.ensure(bytes));
+  HIP_TRY(ctx, ctx->eds.ensure(bytes));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->ods.p, data, bytes, hipMemcpyHostToDevice, s));
+  EncodeArgs ea{};
+  ea.in = (const uint8_t*)ctx->ods.p;
+  ea.out = (uint8_t*)ctx->eds.p;
+  ea.copy = nullptr;
+  ea.in_sq_stride = 0;
+  ea.out_sq_stride = 0;
+  ea.in_vec_stride = (long)k * (long)shard_size;
+  ea.out_vec_stride = (long)k * (long)shard_size;
+  ea.in_shard_stride = (long)shard_size;
+  ea.out_shard_stride = (long)shard_size;
+  ea.nsq = 1;
+  ea.nvec = (long)nvec;
+  ea.nchunk = (long)((shard_size + 511) / 512);
+  ea.shard_bytes = (long)shard_size;
+  HIP_TRY(ctx, launch_leo8_encode((int)k, ea, s));
+  HIP_TRY(ctx, hipMemcpyAsync(parity, ctx->eds.p, bytes, hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipStreamSynchronize(s));
+  return DAGPU_OK;
+}
+
+int dagpu_decode(dagpu_ctx* ctx, uint32_t k, size_t nvec, size_t shard_size, uint8_t* shards,
+                 const uint8_t* present) {
+  (void)k; (void)nvec; (void)shard_size; (void)shards; (void)present;
+  return set_err(ctx, DAGPU_ERR_UNSUPPORTED, "decode not implemented yet");
+}
+
+int dagpu_repair(dagpu_ctx* ctx, uint32_t k, uint8_t* eds, uint8_t* present,
+                 const uint8_t* row_roots, const uint8_t* col_roots) {
+  (void)k; (void)eds; (void)present; (void)row_roots; (void)col_roots;
+  return set_err(ctx, DAGPU_ERR_UNSUPPORTED, "repair not implemented yet");
+}
+
+int dagpu_repair_batch_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds,
+                              uint8_t* d_present, const uint8_t* d_row_roots,
+                              const uint8_t* d_col_roots, int32_t* d_status, void* d_workspace,
+                              void* stream) {
+  (void)k; (void)n; (void)d_eds; (void)d_present; (void)d_row_roots; (void)d_col_roots;
+  (void)d_status; (void)d_workspace; (void)stream;
+  return set_err(ctx, DAGPU_ERR_UNSUPPORTED, "repair not implemented yet");
+}
+
+int dagpu_profile_enable(dagpu_ctx* ctx, int on) {
+  if (!ctx) return DAGPU_ERR_ARG;
+  ctx->prof = on != 0;
+  return DAGPU_OK;
+}
+
+int dagpu_profile_read(dagpu_ctx* ctx, double* total_ms, uint64_t* launches, int reset) {
+  if (!ctx) return DAGPU_ERR_ARG;
+  std::lock_guard<std::mutex> g(ctx->prof_mu);
+  for (auto& r : ctx->pending) {
+    HIP_TRY(ctx, hipEventSynchronize(r.b));
+    float ms = 0;
+    HIP_TRY(ctx, hipEventElapsedTime(&ms, r.a, r.b));
+    ctx->prof_ms[r.id] += ms;
+    ctx->prof_n[r.id] += 1;
+    ctx->pool.push_back(r.a);
+    ctx->pool.push_back(r.b);
+  }
+  ctx->pending.clear();
+  for (int i = 0; i < DAGPU_PROFILE_KERNELS; i++) {
+    if (total_ms) total_ms[i] = ctx->prof_ms[i];
+    if (launches) launches[i] = ctx->prof_n[i];
+    if (reset) { ctx->prof_ms[i] = 0; ctx->prof_n[i] = 0; }
+  }
+  return DAGPU_OK;
+}
+
+int dagpu_dah_hash(const uint8_t* row_roots, const uint8_t* col_roots, size_t w,
+                   uint8_t* out32) {
+  if (!out32 || (w && (!row_roots || !col_roots))) return DAGPU_ERR_ARG;
+  std::vector<const uint8_t*> items;
+  items.reserve(2 * w);
+  for (size_t i = 0; i < w; i++) items.push_back(row_roots + i * kNodeSize);
+  for (size_t i = 0; i < w; i++) items.push_back(col_roots + i * kNodeSize);
+  host::rfc6962_root(items, kNodeSize, out32);
+  return DAGPU_OK;
+}
+
+}  // extern "C"

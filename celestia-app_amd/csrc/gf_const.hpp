@@ -1,0 +1,99 @@
+// gf_const.hpp -- compile-time Leopard GF(2^8) constants for the gfx950 kernels.
+//
+// Restates klauspost/reedsolomon v1.11.8 leopard8.go (initLUTs8, initFFTSkew8,
+// mul8LUTs), the field the reference's default codec uses
+// (pkg/appconsts/global_consts.go:92 DefaultCodec = rsmt2d.NewLeoRSCodec ->
+// reedsolomon.New(k, k, WithLeopardGF(true)), GF(2^8) while 2k <= 256).
+//
+// Everything here is constexpr: the encode kernels are fully unrolled per k,
+// so every skew value and every multiply table folds to an immediate.
+//
+// Multiply-by-constant on four packed bytes uses v_perm_b32 as a byte-table
+// lookup.  Multiplication by a fixed field element is GF(2)-linear in the bit
+// representation, so  c*x = T0[x&3] ^ T1[(x>>2)&3] ^ T2[(x>>4)&3] ^ T3[x>>6]
+// with four 4-entry byte tables.  Each table is ONE dword, so every v_perm_b32
+// reads a single SGPR (gfx950 VOP3 reads at most one scalar operand); 8-entry
+// tables would need a second constant in a VGPR, which the compiler hoists and
+// keeps live (256 VGPRs at k=128).
+#pragma once
+#include <stdint.h>
+
+namespace dagpu {
+
+constexpr int kGf8Bits = 8;
+constexpr int kGf8Order = 256;
+constexpr int kGf8Mod = 255;
+
+struct Gf8Const {
+  uint8_t log[256];
+  uint8_t exp[256];
+  uint8_t skew[255];
+  // perm tables per log_m: t[g][lm] = bytes c*(v << 2g), v = 0..3
+  uint32_t t[4][256];
+};
+
+constexpr uint8_t gf8_add_mod(unsigned a, unsigned b) {
+  unsigned s = a + b;
+  return (uint8_t)(s + (s >> 8));
+}
+
+constexpr Gf8Const make_gf8_const() {
+  Gf8Const g{};
+  const uint8_t cantor[8] = {1, 214, 152, 146, 86, 200, 88, 230};
+  unsigned state = 1;
+  for (unsigned i = 0; i < 255; i++) {
+    g.exp[state] = (uint8_t)i;
+    state <<= 1;
+    if (state >= 256) state ^= 0x11D;
+  }
+  g.exp[0] = 255;
+  g.log[0] = 0;
+  for (int i = 0; i < 8; i++) {
+    int width = 1 << i;
+    for (int j = 0; j < width; j++) g.log[j + width] = (uint8_t)(g.log[j] ^ cantor[i]);
+  }
+  for (int i = 0; i < 256; i++) g.log[i] = g.exp[g.log[i]];
+  for (int i = 0; i < 256; i++) g.exp[g.log[i]] = (uint8_t)i;
+  g.exp[255] = g.exp[0];
+
+  auto mullog = [&](uint8_t a, uint8_t lb) -> uint8_t {
+    if (a == 0) return 0;
+    return g.exp[gf8_add_mod(g.log[a], lb)];
+  };
+
+  uint8_t temp[7] = {};
+  for (int i = 1; i < 8; i++) temp[i - 1] = (uint8_t)(1 << i);
+  for (int i = 0; i < 255; i++) g.skew[i] = 0;
+  for (int m = 0; m < 7; m++) {
+    int step = 1 << (m + 1);
+    g.skew[(1 << m) - 1] = 0;
+    for (int i = m; i < 7; i++) {
+      int s = 1 << (i + 1);
+      for (int j = (1 << m) - 1; j < s; j += step) g.skew[j + s] = (uint8_t)(g.skew[j] ^ temp[i]);
+    }
+    temp[m] = (uint8_t)(255 - g.log[mullog(temp[m], g.log[temp[m] ^ 1])]);
+    for (int i = m + 1; i < 7; i++) {
+      uint8_t sum = gf8_add_mod(g.log[temp[i] ^ 1], temp[m]);
+      temp[i] = mullog(temp[i], sum);
+    }
+  }
+  for (int i = 0; i < 255; i++) g.skew[i] = g.log[g.skew[i]];
+
+  for (int lm = 0; lm < 256; lm++) {
+    for (int grp = 0; grp < 4; grp++) {
+      uint32_t v = 0;
+      for (int x = 0; x < 4; x++) v |= (uint32_t)mullog((uint8_t)(x << (2 * grp)), (uint8_t)lm) << (8 * x);
+      g.t[grp][lm] = v;
+    }
+  }
+  return g;
+}
+
+inline constexpr Gf8Const kGf8 = make_gf8_const();
+
+// Sanity: first skew entries quoted in SURVEY.md Appendix A.1.
+static_assert(kGf8.skew[0] == 255 && kGf8.skew[2] == 85 && kGf8.skew[4] == 17 &&
+                  kGf8.skew[8] == 153 && kGf8.skew[14] == 187,
+              "Leopard GF(2^8) FFT skew mismatch");
+
+}  // namespace dagpu

@@ -1,0 +1,156 @@
+/*
+ * dagpu.h -- C ABI of the MI355X-native celestia-app data-availability hot path.
+ *
+ * Library: celestia-app_amd/libdagpu.so (hipcc --offload-arch=gfx950).
+ * Plain pointers and sizes only; the caller owns every buffer and nothing is
+ * retained after a call returns.  Each entry point names the reference
+ * interface it replaces (paths relative to the reference repo root).  The Go
+ * (cgo) binding a maintainer would add on the reference side is in
+ * INTEGRATION.md.
+ *
+ * Layouts
+ *   share      512 bytes (appconsts.ShareSize, pkg/appconsts/global_consts.go:29)
+ *   ODS        k*k shares, row-major                     (k*k*512 B)
+ *   EDS        (2k)*(2k) shares, row-major, Q0|Q1 / Q2|Q3 ((2k)^2*512 B)
+ *   root       90 bytes = minNs(29) | maxNs(29) | sha256(32)
+ *   row_roots  2k roots, col_roots 2k roots, dah 32 bytes
+ *   batches    squares packed back to back in each array (mixed-k batches:
+ *              square i starts after the bytes of squares 0..i-1)
+ *
+ * Errors: functions return 0 or a negative dagpu_status; batch calls also
+ * fill a per-square status array.  dagpu_last_error() gives the message of the
+ * last failure on that context (same wording as the reference where one
+ * exists).  A context is thread-safe: host-memory calls are serialised on it.
+ */
+#ifndef DAGPU_H
+#define DAGPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DAGPU_SHARE_SIZE 512
+#define DAGPU_NAMESPACE_SIZE 29
+#define DAGPU_ROOT_SIZE 90
+#define DAGPU_HASH_SIZE 32
+
+typedef enum dagpu_status {
+  DAGPU_OK = 0,
+  DAGPU_ERR_NOT_POW2 = -1,       /* pkg/da/data_availability_header.go:67-69 */
+  DAGPU_ERR_NOT_SQUARE = -2,     /* rsmt2d newDataSquare: "number of chunks must be a square number" */
+  DAGPU_ERR_SHARE_SIZE = -3,     /* shares not all 512 B / shard not a multiple of 64 */
+  DAGPU_ERR_PUSH_ORDER = -4,     /* nmt ErrInvalidPushOrder (Q0 namespaces unsorted) */
+  DAGPU_ERR_TOO_FEW_SHARDS = -5, /* reedsolomon ErrTooFewShards */
+  DAGPU_ERR_UNREPAIRABLE = -6,   /* rsmt2d ErrUnrepairableDataSquare */
+  DAGPU_ERR_BYZANTINE = -7,      /* rsmt2d ErrByzantineData */
+  DAGPU_ERR_BAD_ROOTS = -8,      /* rsmt2d "bad root input" */
+  DAGPU_ERR_ARG = -9,
+  DAGPU_ERR_DEVICE = -10,        /* HIP runtime failure */
+  DAGPU_ERR_UNSUPPORTED = -11    /* e.g. k above what this build implements */
+} dagpu_status;
+
+typedef struct dagpu_ctx dagpu_ctx;
+
+/* Library version (major*10000 + minor*100 + patch). */
+int dagpu_version(void);
+
+/* Open a context on HIP device `device` (one context per GPU per process). */
+int dagpu_init(int device, dagpu_ctx** out);
+void dagpu_destroy(dagpu_ctx* ctx);
+const char* dagpu_last_error(dagpu_ctx* ctx);
+
+/* Replaces da.ExtendShares + da.NewDataAvailabilityHeader + dah.Hash()
+ * (pkg/da/data_availability_header.go:65-75, :44-63, :92-108) for one square.
+ * shares: n_shares * share_size bytes (host).  eds_out may be NULL (roots/DAH
+ * only, the device-resident default).  Errors as ExtendShares: n_shares not a
+ * power of two -> DAGPU_ERR_NOT_POW2; not a square -> DAGPU_ERR_NOT_SQUARE;
+ * unsorted Q0 namespaces -> DAGPU_ERR_PUSH_ORDER (NewDataAvailabilityHeader). */
+int dagpu_extend_shares(dagpu_ctx* ctx, const uint8_t* shares, size_t n_shares,
+                        size_t share_size, uint8_t* eds_out, uint8_t* row_roots,
+                        uint8_t* col_roots, uint8_t* dah);
+
+/* Batched host-memory form (app/extend_block.go:14-22 block replay; mixed k).
+ * k[i] = original square width of square i.  status[i] gets a dagpu_status.
+ * Returns DAGPU_OK if every square succeeded, else the first failing status. */
+int dagpu_extend_batch(dagpu_ctx* ctx, const uint8_t* ods, const uint32_t* k, size_t n,
+                       uint8_t* eds_or_null, uint8_t* row_roots, uint8_t* col_roots,
+                       uint8_t* dah, int32_t* status);
+
+/* Device-resident batch, one k for all n squares; every pointer is device
+ * memory; work is enqueued on `stream` (hipStream_t, NULL = default stream) and
+ * the call returns without synchronising.  d_ods may be NULL when Q0 is already
+ * in place inside d_eds.  d_status: n int32 bitmasks (0 = OK, 1 = push order).
+ * d_workspace: dagpu_workspace_size(k, n) bytes. */
+size_t dagpu_workspace_size(uint32_t k, size_t n);
+int dagpu_extend_batch_device(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_ods,
+                              uint8_t* d_eds, uint8_t* d_row_roots, uint8_t* d_col_roots,
+                              uint8_t* d_dah, int32_t* d_status, void* d_workspace,
+                              void* stream);
+
+/* Device-resident stages (for profiling and for callers that already hold an
+ * EDS on the device): RS extension only, and NMT roots + DAH only. */
+int dagpu_extend_rs_device(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_ods,
+                           uint8_t* d_eds, void* stream);
+int dagpu_roots_device(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_eds,
+                       uint8_t* d_row_roots, uint8_t* d_col_roots, uint8_t* d_dah,
+                       int32_t* d_status, void* d_workspace, void* stream);
+
+/* Replaces NewDataAvailabilityHeader(eds) for an EDS already in host memory
+ * (rsmt2d RowRoots/ColRoots + Hash). */
+int dagpu_roots(dagpu_ctx* ctx, uint32_t k, const uint8_t* eds, uint8_t* row_roots,
+                uint8_t* col_roots, uint8_t* dah);
+
+/* rsmt2d.Codec (LeoRSCodec, pkg/appconsts/global_consts.go:92) Encode over many
+ * vectors: data = nvec * k shards of shard_size bytes (contiguous per vector),
+ * parity = nvec * k shards.  shard_size must be a multiple of 64. */
+int dagpu_encode(dagpu_ctx* ctx, uint32_t k, size_t nvec, size_t shard_size,
+                 const uint8_t* data, uint8_t* parity);
+
+/* rsmt2d.Codec Decode (klauspost Reconstruct via Leopard GF(2^8)): shards =
+ * nvec * 2k shards of shard_size bytes, present = nvec * 2k flags (non-zero =
+ * shard present).  Missing shards are rebuilt in place.  Needs >= k present
+ * per vector (DAGPU_ERR_TOO_FEW_SHARDS otherwise). */
+int dagpu_decode(dagpu_ctx* ctx, uint32_t k, size_t nvec, size_t shard_size,
+                 uint8_t* shards, const uint8_t* present);
+
+/* rsmt2d ExtendedDataSquare.Repair for one square in host memory: eds is
+ * (2k)^2 * 512 bytes with present[(2k)^2] flags; missing cells are filled in
+ * place and every row/column root is re-verified against row_roots/col_roots
+ * (DAGPU_ERR_BYZANTINE on mismatch, DAGPU_ERR_UNREPAIRABLE if the crossword
+ * cannot be solved, DAGPU_ERR_BAD_ROOTS if a complete axis disagrees up front). */
+int dagpu_repair(dagpu_ctx* ctx, uint32_t k, uint8_t* eds, uint8_t* present,
+                 const uint8_t* row_roots, const uint8_t* col_roots);
+
+/* Device-resident batched Repair: n squares of width k (device pointers),
+ * d_present = n * (2k)^2 flags (updated), expected roots as produced by
+ * dagpu_extend_batch_device.  d_status gets one dagpu_status per square.
+ * d_workspace: dagpu_workspace_size(k, n) bytes + n*(2k)^2*... see
+ * dagpu_repair_workspace_size. */
+int dagpu_repair_batch_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds,
+                              uint8_t* d_present, const uint8_t* d_row_roots,
+                              const uint8_t* d_col_roots, int32_t* d_status,
+                              void* d_workspace, void* stream);
+
+/* Per-kernel timing with HIP events recorded on the launch stream around each
+ * kernel the pipeline enqueues (for bench.py's roofline; off by default).
+ * Kernel ids: 0 RS row pass, 1 RS column pass, 2 NMT leaves, 3 NMT trees,
+ * 4 DAH, 5 decode.  dagpu_profile_read synchronises the recorded events and
+ * returns, per kernel id, the summed milliseconds and launch count since the
+ * last reset (arrays of DAGPU_PROFILE_KERNELS entries). */
+#define DAGPU_PROFILE_KERNELS 6
+int dagpu_profile_enable(dagpu_ctx* ctx, int on);
+int dagpu_profile_read(dagpu_ctx* ctx, double* total_ms, uint64_t* launches, int reset);
+
+/* RFC-6962 root of rowRoots || colRoots (DataAvailabilityHeader.Hash,
+ * pkg/da/data_availability_header.go:92-108), computed on the host side of the
+ * boundary for small inputs (w = number of row roots; w == 0 gives the
+ * empty-tree hash SHA256("")). */
+int dagpu_dah_hash(const uint8_t* row_roots, const uint8_t* col_roots, size_t w,
+                   uint8_t* out32);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
