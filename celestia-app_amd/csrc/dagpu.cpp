@@ -185,7 +185,9 @@ int enqueue_roots(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_eds, ui
   SquareArgs sa{};
   sa.eds = d_eds;
   sa.eds_sq_stride = (long)eds_bytes(k);
-  sa.digests = (uint8_t*)d_ws;
+  sa.k = (int)k;
+  sa.nsq = (long)n;
+  nmt_workspace_carve(sa, d_ws);
   sa.row_roots = d_rr;
   sa.col_roots = d_cr;
   sa.dah = d_dah;
@@ -295,7 +297,8 @@ void dagpu_destroy(dagpu_ctx* c) {
 const char* dagpu_last_error(dagpu_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 size_t dagpu_workspace_size(uint32_t k, size_t n) {
-  return (size_t)4 * k * k * kDigest * n + 256;
+  if (k == 0 || n == 0) return 256;
+  return nmt_workspace_bytes((int)k, (long)n) + 256;
 }
 
 int dagpu_extend_shares(dagpu_ctx* ctx, const uint8_t* shares, size_t n_shares,

@@ -33,6 +33,9 @@ struct SquareArgs {
   const uint8_t* eds;   // nsq squares, each (2k)^2 * 512 B, row-major
   long eds_sq_stride;
   uint8_t* digests;     // leaf digests: nsq * (2k)^2 * 32 B
+  uint8_t* ns_table;    // Q0 namespaces: nsq * k^2 * 32 B
+  uint8_t* rec_a;       // tree node records (48 B): nsq * 2w * w/2
+  uint8_t* rec_b;       // nsq * 2w * w/4
   uint8_t* row_roots;   // nsq * 2k * 90 B
   uint8_t* col_roots;   // nsq * 2k * 90 B
   uint8_t* dah;         // nsq * 32 B
@@ -42,6 +45,9 @@ struct SquareArgs {
 };
 
 hipError_t launch_nmt_leaves(const SquareArgs& a, hipStream_t s);
+// workspace layout for SquareArgs (digests | ns_table | rec_a | rec_b)
+size_t nmt_workspace_bytes(int k, long nsq);
+void nmt_workspace_carve(SquareArgs& a, void* ws);
 hipError_t launch_nmt_trees(const SquareArgs& a, hipStream_t s);
 hipError_t launch_dah(const SquareArgs& a, hipStream_t s);
 

@@ -17,10 +17,14 @@
 // Kernel 1 (leaves): one lane per cell; 542-B message 0x00|ns|share = 9 SHA
 //   blocks; the share is streamed with 16-B loads and re-aligned into big-endian
 //   message words with one v_perm_b32 per word.
-// Kernel 2 (trees): one workgroup builds 512/w trees (w = 2k): level 1 reads
-//   leaf digests + namespaces, levels >= 2 run in LDS.  Node namespace ranges
-//   follow HashNode with ignoreMaxNamespace=true; push-order (ErrInvalidPushOrder)
-//   is checked on Q0 leaves.
+// Kernel 2 (tree levels): one launch per tree level over ALL 4k trees of ALL
+//   squares in the batch (thread = node), so every level runs at full lane
+//   occupancy (a per-tree workgroup would idle most lanes in the last levels).
+//   A node record is 48 B: digest(32) | minRef | maxRef (cell index of the Q0
+//   leaf whose namespace it carries, or PARITY).  Namespace bytes are read from
+//   a dense Q0 namespace table written by kernel 1.  Node ranges follow
+//   HashNode with ignoreMaxNamespace=true; push order (ErrInvalidPushOrder) is
+//   checked on Q0 leaves at level 1.
 // Kernel 3 (DAH): one workgroup per square, RFC-6962 over 4k roots.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -71,6 +75,11 @@ __global__ __launch_bounds__(256) void nmt_leaf_kernel(SquareArgs a) {
       m[7] = 0xFFFF0000u;
     }
     m[7] |= __builtin_amdgcn_perm(d[0], d[0], (PZ << 24) | (PZ << 16) | 0x0001u);
+    if (q0) {  // dense Q0 namespace table (29 B, zero padded to 32)
+      uint4* nsp = (uint4*)(a.ns_table + (sq * k * k + r * k + c) * 32);
+      nsp[0] = make_uint4(d[0], d[1], d[2], d[3]);
+      nsp[1] = make_uint4(d[4], d[5], d[6], d[7] & 0xFFu);
+    }
 #pragma unroll
     for (int j = 8; j < 16; j++) m[j] = __builtin_amdgcn_perm(d[j - 8], d[j - 7], 0x06070001u);
     sha256_compress(st, m);
@@ -209,125 +218,146 @@ __device__ __forceinline__ void load_digest(const uint8_t* p, uint32_t (&d)[8]) 
 }
 
 // ---------------------------------------------------------------------------
-// Kernel 2: trees.  Tree id t in [0, nsq*2w): sq = t / 2w, axis = (t/w)&1,
-// idx = t % w.  tpw = 512/w trees per 256-thread workgroup (w <= 512), so every
-// level has at most one node per thread.  Nodes live in LDS as 24 dwords:
-// [0..7] minNs, [8..15] maxNs, [16..23] digest (memory byte order).
+// Kernel 2: one tree level.  Tree id t in [0, nsq*2w): sq = t / 2w,
+// axis = (t / w) & 1, idx = t % w.  Level L has w >> L nodes per tree.
 // ---------------------------------------------------------------------------
-constexpr int kTreeThreads = 256;
+constexpr uint32_t kParityRef = 0xFFFFFFFFu;
 
-__global__ __launch_bounds__(kTreeThreads) void nmt_tree_kernel(SquareArgs a, int tpw) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+__device__ __forceinline__ void ns_by_ref(const uint8_t* ns_sq, uint32_t ref, uint32_t (&ns)[8]) {
+  if (ref == kParityRef) {
+#pragma unroll
+    for (int i = 0; i < 7; i++) ns[i] = 0xFFFFFFFFu;
+    ns[7] = 0xFFu;
+  } else {
+    const uint4* p = (const uint4*)(ns_sq + (long)ref * 32);
+    const uint4 v0 = p[0], v1 = p[1];
+    ns[0] = v0.x; ns[1] = v0.y; ns[2] = v0.z; ns[3] = v0.w;
+    ns[4] = v1.x; ns[5] = v1.y; ns[6] = v1.z; ns[7] = v1.w;
+  }
+}
+
+__device__ __forceinline__ void write_root(uint8_t* dst, const uint32_t (&mn)[8], const uint32_t (&mx)[8],
+                                           const uint32_t (&dg)[8]) {
+  // 90 B at a 2-byte aligned address: 45 halfword stores
+  uint16_t* d16 = (uint16_t*)dst;
+#pragma unroll
+  for (int h = 0; h < 45; h++) {
+    uint32_t lo, hi;
+    const int b0 = 2 * h, b1 = 2 * h + 1;
+    auto byte_at = [&](int b) -> uint32_t {
+      if (b < 29) return (mn[b >> 2] >> (8 * (b & 3))) & 0xFFu;
+      if (b < 58) { const int q = b - 29; return (mx[q >> 2] >> (8 * (q & 3))) & 0xFFu; }
+      const int q = b - 58;
+      return (dg[q >> 2] >> (8 * (q & 3))) & 0xFFu;
+    };
+    lo = byte_at(b0);
+    hi = byte_at(b1);
+    d16[h] = (uint16_t)(lo | (hi << 8));
+  }
+}
+
+// Level 1: pairs of leaves.  Leaf node = ns | ns | digest; a Q0 leaf whose
+// namespace equals the parity namespace gets kParityRef (same bytes).
+__global__ __launch_bounds__(256) void nmt_level1_kernel(SquareArgs a, uint8_t* out_rec, int final_level) {
   const int k = a.k;
   const int w = 2 * k;
-  const long tree0 = (long)blockIdx.x * tpw;
-  const long ntrees = a.nsq * 2L * w;
-  const int half = w / 2;  // level-1 nodes per tree
-  const int g = threadIdx.x;
-
-  // ---- level 1: hash pairs of leaves (leaf node = ns | ns | digest) ----
-  {
-    const int tl = g / half, p = g - tl * half;
-    const long t = tree0 + tl;
-    uint32_t out[24];
-    if (tl < tpw && t < ntrees) {
-      const long sq = t / (2L * w);
-      const int axis = (int)((t / w) & 1);
-      const int idx = (int)(t % w);
-      const uint8_t* eds = a.eds + sq * a.eds_sq_stride;
-      const uint8_t* dig = a.digests + sq * (long)w * w * kDigest;
-      const int j0 = 2 * p, j1 = 2 * p + 1;
-      const long cell0 = axis == 0 ? (long)idx * w + j0 : (long)j0 * w + idx;
-      const long cell1 = axis == 0 ? (long)idx * w + j1 : (long)j1 * w + idx;
-      const bool q00 = (idx < k) && (j0 < k), q01 = (idx < k) && (j1 < k);
-      uint32_t nl[8], nr[8], dl[8], dr[8];
-      load_ns(eds + cell0 * kShareSize, q00, nl);
-      load_ns(eds + cell1 * kShareSize, q01, nr);
-      load_digest(dig + cell0 * kDigest, dl);
-      load_digest(dig + cell1 * kDigest, dr);
-      // nmt Push order: ns(j0) <= ns(j1) <= ns(j1+1); only Q0 leaves can violate
-      if (q01) {
-        bool bad = ns_less(nr, nl);
-        if (j1 + 1 < k) {
-          const long cell2 = axis == 0 ? (long)idx * w + j1 + 1 : (long)(j1 + 1) * w + idx;
-          uint32_t n2[8];
-          load_ns(eds + cell2 * kShareSize, true, n2);
-          bad |= ns_less(n2, nr);
-        }
-        if (bad) atomicOr(&a.status[sq], kStatusPushOrder);
-      }
-      uint32_t st[8];
-      auto get = [&](int P, int i) -> uint32_t {
-        return P == 0 || P == 1 ? nl[i] : P == 2 ? dl[i] : P == 3 || P == 4 ? nr[i] : dr[i];
-      };
-      sha_node_msg(get, st);
-      const bool rpar = ns_is_parity(nr);
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        out[i] = nl[i];
-        out[8 + i] = rpar ? nl[i] : nr[i];
-        out[16 + i] = bswap32(st[i]);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 24; i++) out[i] = 0;
+  const int half = w / 2;
+  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+  const long total = a.nsq * 2L * w * half;
+  if (gid >= total) return;
+  const long t = gid / half;
+  const int p = (int)(gid - t * half);
+  const long sq = t / (2L * w);
+  const int axis = (int)((t / w) & 1);
+  const int idx = (int)(t % w);
+  const uint8_t* dig = a.digests + sq * (long)w * w * kDigest;
+  const uint8_t* ns_sq = a.ns_table + sq * (long)k * k * 32;
+  const int j0 = 2 * p, j1 = 2 * p + 1;
+  const long cell0 = axis == 0 ? (long)idx * w + j0 : (long)j0 * w + idx;
+  const long cell1 = axis == 0 ? (long)idx * w + j1 : (long)j1 * w + idx;
+  const bool q00 = (idx < k) && (j0 < k), q01 = (idx < k) && (j1 < k);
+  // Q0 ref = r*k + c
+  const uint32_t ref0 = q00 ? (axis == 0 ? (uint32_t)(idx * k + j0) : (uint32_t)(j0 * k + idx)) : kParityRef;
+  const uint32_t ref1 = q01 ? (axis == 0 ? (uint32_t)(idx * k + j1) : (uint32_t)(j1 * k + idx)) : kParityRef;
+  uint32_t nl[8], nr[8], dl[8], dr[8];
+  ns_by_ref(ns_sq, ref0, nl);
+  ns_by_ref(ns_sq, ref1, nr);
+  load_digest(dig + cell0 * kDigest, dl);
+  load_digest(dig + cell1 * kDigest, dr);
+  if (q01) {  // nmt Push order: ns(j0) <= ns(j1) <= ns(j1+1)
+    bool bad = ns_less(nr, nl);
+    if (j1 + 1 < k) {
+      const uint32_t ref2 = axis == 0 ? (uint32_t)(idx * k + j1 + 1) : (uint32_t)((j1 + 1) * k + idx);
+      uint32_t n2[8];
+      ns_by_ref(ns_sq, ref2, n2);
+      bad |= ns_less(n2, nr);
     }
-    uint4* slot = (uint4*)(lds + g * 24);
-#pragma unroll
-    for (int i = 0; i < 6; i++) slot[i] = make_uint4(out[4 * i], out[4 * i + 1], out[4 * i + 2], out[4 * i + 3]);
+    if (bad) atomicOr(&a.status[sq], kStatusPushOrder);
   }
-  __syncthreads();
-
-  // ---- levels >= 2 in LDS: node q of tree tl reads slots 2q, 2q+1 ----
-  for (int per_tree = half; per_tree > 1; per_tree >>= 1) {
-    const int next = per_tree >> 1;
-    const int total = tpw * next;
-    uint32_t out[24];
-    const bool active = g < total;
-    int tl = 0, q = 0;
-    if (active) {
-      tl = g / next;
-      q = g - tl * next;
-      const uint32_t* sl = lds + ((long)tl * half + 2 * q) * 24;
-      const uint32_t* sr = sl + 24;
-      uint32_t st[8];
-      auto get = [&](int P, int i) -> uint32_t { return P < 3 ? sl[8 * P + i] : sr[8 * (P - 3) + i]; };
-      sha_node_msg(get, st);
-      uint32_t rmn[8];
+  uint32_t st[8];
+  auto get = [&](int P, int i) -> uint32_t {
+    return P == 0 || P == 1 ? nl[i] : P == 2 ? dl[i] : P == 3 || P == 4 ? nr[i] : dr[i];
+  };
+  sha_node_msg(get, st);
+  const bool lpar = ns_is_parity(nl), rpar = ns_is_parity(nr);
+  uint32_t dg[8];
 #pragma unroll
-      for (int i = 0; i < 8; i++) rmn[i] = sr[i];
-      const bool rpar = ns_is_parity(rmn);
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        out[i] = sl[i];
-        out[8 + i] = rpar ? sl[8 + i] : sr[8 + i];
-        out[16 + i] = bswap32(st[i]);
-      }
-    }
-    __syncthreads();
-    if (active) {
-      uint4* slot = (uint4*)(lds + ((long)tl * half + q) * 24);
-#pragma unroll
-      for (int i = 0; i < 6; i++) slot[i] = make_uint4(out[4 * i], out[4 * i + 1], out[4 * i + 2], out[4 * i + 3]);
-    }
-    __syncthreads();
+  for (int i = 0; i < 8; i++) dg[i] = bswap32(st[i]);
+  if (final_level) {
+    uint8_t* dst = (axis == 0 ? a.row_roots : a.col_roots) + (sq * w + idx) * kNodeSize;
+    write_root(dst, nl, rpar ? nl : nr, dg);
+  } else {
+    const uint32_t lref = lpar ? kParityRef : ref0;
+    const uint32_t rref = rpar ? kParityRef : ref1;
+    uint4* o = (uint4*)(out_rec + gid * 48);
+    o[0] = make_uint4(dg[0], dg[1], dg[2], dg[3]);
+    o[1] = make_uint4(dg[4], dg[5], dg[6], dg[7]);
+    o[2] = make_uint4(lref, rref == kParityRef ? lref : rref, 0u, 0u);
   }
+}
 
-  // ---- write roots (90 B each) ----
-  for (int e = g; e < tpw * kNodeSize; e += kTreeThreads) {
-    const int tl = e / kNodeSize, b = e - tl * kNodeSize;
-    const long t = tree0 + tl;
-    if (t >= ntrees) continue;
-    const long sq = t / (2L * w);
+// Levels >= 2: node q of tree t from records 2q, 2q+1 of the previous level.
+__global__ __launch_bounds__(256) void nmt_level_kernel(SquareArgs a, const uint8_t* in_rec, uint8_t* out_rec,
+                                                        int level, int final_level) {
+  const int k = a.k;
+  const int w = 2 * k;
+  const int per = w >> level;  // nodes per tree at this level
+  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+  const long total = a.nsq * 2L * w * per;
+  if (gid >= total) return;
+  const long t = gid / per;
+  const long sq = t / (2L * w);
+  const uint8_t* ns_sq = a.ns_table + sq * (long)k * k * 32;
+  const uint4* li = (const uint4*)(in_rec + (2 * gid) * 48);
+  const uint4* ri = li + 3;
+  const uint4 l0 = li[0], l1 = li[1], l2 = li[2], r0 = ri[0], r1 = ri[1], r2 = ri[2];
+  const uint32_t dl[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+  const uint32_t dr[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+  uint32_t lmn[8], lmx[8], rmn[8], rmx[8];
+  ns_by_ref(ns_sq, l2.x, lmn);
+  ns_by_ref(ns_sq, l2.y, lmx);
+  ns_by_ref(ns_sq, r2.x, rmn);
+  ns_by_ref(ns_sq, r2.y, rmx);
+  uint32_t st[8];
+  auto get = [&](int P, int i) -> uint32_t {
+    return P == 0 ? lmn[i] : P == 1 ? lmx[i] : P == 2 ? dl[i] : P == 3 ? rmn[i] : P == 4 ? rmx[i] : dr[i];
+  };
+  sha_node_msg(get, st);
+  uint32_t dg[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) dg[i] = bswap32(st[i]);
+  const bool rpar = r2.x == kParityRef;
+  if (final_level) {
     const int axis = (int)((t / w) & 1);
     const int idx = (int)(t % w);
-    const uint32_t* slot = lds + (long)tl * half * 24;
-    int word, byte;
-    if (b < 29) { word = b >> 2; byte = b & 3; }
-    else if (b < 58) { word = 8 + ((b - 29) >> 2); byte = (b - 29) & 3; }
-    else { word = 16 + ((b - 58) >> 2); byte = (b - 58) & 3; }
     uint8_t* dst = (axis == 0 ? a.row_roots : a.col_roots) + (sq * w + idx) * kNodeSize;
-    dst[b] = (uint8_t)(slot[word] >> (8 * byte));
+    if (rpar) write_root(dst, lmn, lmx, dg);
+    else write_root(dst, lmn, rmx, dg);
+  } else {
+    uint4* o = (uint4*)(out_rec + gid * 48);
+    o[0] = make_uint4(dg[0], dg[1], dg[2], dg[3]);
+    o[1] = make_uint4(dg[4], dg[5], dg[6], dg[7]);
+    o[2] = make_uint4(l2.x, rpar ? l2.y : r2.y, 0u, 0u);
   }
 }
 
@@ -426,13 +456,48 @@ hipError_t launch_nmt_leaves(const SquareArgs& a, hipStream_t s) {
 
 hipError_t launch_nmt_trees(const SquareArgs& a, hipStream_t s) {
   const int w = 2 * a.k;
-  if (w > 512) return hipErrorInvalidValue;
-  const int tpw = 512 / w;
-  const long ntrees = a.nsq * 2L * w;
-  const long blocks = (ntrees + tpw - 1) / tpw;
-  const size_t lds = (size_t)kTreeThreads * 24 * sizeof(uint32_t);
-  hipLaunchKernelGGL(nmt_tree_kernel, dim3((unsigned)blocks), dim3(kTreeThreads), lds, s, a, tpw);
-  return hipGetLastError();
+  int levels = 0;
+  while ((1 << levels) < w) levels++;
+  // ping-pong node buffers: level 1 -> recA, 2 -> recB, 3 -> recA, ...
+  uint8_t* bufs[2] = {a.rec_a, a.rec_b};
+  {
+    const long total = a.nsq * 2L * w * (w / 2);
+    hipLaunchKernelGGL(nmt_level1_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a,
+                       bufs[0], (int)(levels == 1));
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  for (int L = 2; L <= levels; L++) {
+    const long total = a.nsq * 2L * w * (w >> L);
+    hipLaunchKernelGGL(nmt_level_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a,
+                       (const uint8_t*)bufs[(L - 2) & 1], bufs[(L - 1) & 1], L, (int)(L == levels));
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+size_t nmt_workspace_bytes(int k, long nsq) {
+  const size_t w = 2 * (size_t)k;
+  const size_t dig = align256(w * w * kDigest * nsq);
+  const size_t ns = align256((size_t)k * k * 32 * nsq);
+  const size_t ra = align256(nsq * 2 * w * (w / 2) * 48);
+  const size_t rb = align256(nsq * 2 * w * (w / 4 > 0 ? w / 4 : 1) * 48);
+  return dig + ns + ra + rb;
+}
+
+void nmt_workspace_carve(SquareArgs& a, void* ws) {
+  const size_t w = 2 * (size_t)a.k;
+  uint8_t* p = (uint8_t*)ws;
+  a.digests = p;
+  p += align256(w * w * kDigest * a.nsq);
+  a.ns_table = p;
+  p += align256((size_t)a.k * a.k * 32 * a.nsq);
+  a.rec_a = p;
+  p += align256(a.nsq * 2 * w * (w / 2) * 48);
+  a.rec_b = p;
 }
 
 hipError_t launch_dah(const SquareArgs& a, hipStream_t s) {
