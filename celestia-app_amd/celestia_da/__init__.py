@@ -11,6 +11,7 @@ from .da import (  # noqa: F401
     DataAvailabilityHeader,
     ErrByzantineData,
     ErrInvalidPushOrder,
+    ErrTooFewShards,
     ErrUnrepairableDataSquare,
     ExtendedDataSquare,
     LeoRSCodec,
@@ -21,6 +22,7 @@ from .da import (  # noqa: F401
     min_data_availability_header,
     min_shares,
     new_data_availability_header,
+    repair,
     nil_dah_hash,
     round_up_power_of_two,
     square_size,

@@ -44,6 +44,7 @@ EXPORTS = (
     "dagpu_roots",
     "dagpu_encode",
     "dagpu_decode",
+    "dagpu_repair_workspace_size",
     "dagpu_repair_batch_device",
     "dagpu_repair",
     "dagpu_profile_enable",
@@ -87,7 +88,9 @@ def lib() -> ctypes.CDLL:
         L.dagpu_encode.argtypes = [vp, ctypes.c_uint32, sz, sz, vp, vp]
         L.dagpu_decode.argtypes = [vp, ctypes.c_uint32, sz, sz, vp, vp]
         L.dagpu_repair_batch_device.argtypes = [vp, ctypes.c_uint32, sz, vp, vp, vp, vp, vp, vp,
-                                                vp, vp]
+                                                vp]
+        L.dagpu_repair_workspace_size.argtypes = [ctypes.c_uint32, sz]
+        L.dagpu_repair_workspace_size.restype = sz
         L.dagpu_repair.argtypes = [vp, ctypes.c_uint32, vp, vp, vp, vp]
         L.dagpu_dah_hash.argtypes = [vp, vp, sz, vp]
         L.dagpu_profile_enable.argtypes = [vp, ctypes.c_int]

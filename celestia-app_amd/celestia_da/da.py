@@ -53,7 +53,12 @@ class ErrUnrepairableDataSquare(DAError):
     pass
 
 
+class ErrTooFewShards(DAError):
+    pass
+
+
 _ERR_CLASS = {
+    _abi.ERR_TOO_FEW_SHARDS: ErrTooFewShards,
     _abi.ERR_PUSH_ORDER: ErrInvalidPushOrder,
     _abi.ERR_BYZANTINE: ErrByzantineData,
     _abi.ERR_UNREPAIRABLE: ErrUnrepairableDataSquare,
@@ -325,6 +330,24 @@ class LeoRSCodec:
         self.ctx.check(self.ctx._L.dagpu_decode(self.ctx.handle, n // 2, 1, size, _abi.addr(buf),
                                                 _abi.addr(present)))
         return [buf[i].tobytes() for i in range(n)]
+
+
+def repair(eds: np.ndarray, present: np.ndarray, row_roots, col_roots,
+           ctx: Optional[Context] = None):
+    """rsmt2d ExtendedDataSquare.Repair(rowRoots, colRoots) on the GPU.
+
+    eds: (2k, 2k, 512) uint8 with arbitrary bytes in missing cells; present:
+    (2k, 2k) bool.  Returns (repaired eds, present after repair).  Raises
+    ErrByzantineData, ErrUnrepairableDataSquare or DAError("bad root input")."""
+    ctx = ctx or default_context()
+    e = np.ascontiguousarray(eds, dtype=np.uint8).copy()
+    w = e.shape[0]
+    p = np.ascontiguousarray(present, dtype=np.uint8).reshape(w, w).copy()
+    rr = np.ascontiguousarray(np.frombuffer(b"".join(bytes(r) for r in row_roots), np.uint8))
+    cr = np.ascontiguousarray(np.frombuffer(b"".join(bytes(c) for c in col_roots), np.uint8))
+    rc = ctx._L.dagpu_repair(ctx.handle, w // 2, _abi.addr(e), _abi.addr(p), _abi.addr(rr), _abi.addr(cr))
+    ctx.check(rc)
+    return e, p.astype(bool)
 
 
 def extend_batch(ods: np.ndarray, ks: Sequence[int], ctx: Optional[Context] = None,

@@ -60,6 +60,19 @@ class DeviceSquares:
             self.ctx.handle, self.k, self.n, _abi.addr(self.ods), _abi.addr(self.eds),
             _stream_handle(stream)))
 
+    def repair(self, present: torch.Tensor, status: torch.Tensor, workspace: torch.Tensor,
+               stream: Optional[torch.cuda.Stream] = None) -> None:
+        """Device-resident rsmt2d Repair of self.eds against self.row/col_roots.
+        present: (n, (2k)^2) uint8, updated in place; status: (n,) int32."""
+        self._ck(self.ctx._L.dagpu_repair_batch_device(
+            self.ctx.handle, self.k, self.n, _abi.addr(self.eds), _abi.addr(present),
+            _abi.addr(self.row_roots), _abi.addr(self.col_roots), _abi.addr(status),
+            _abi.addr(workspace), _stream_handle(stream)))
+
+    def repair_workspace(self) -> torch.Tensor:
+        ws = self.ctx._L.dagpu_repair_workspace_size(self.k, self.n)
+        return torch.empty((ws,), dtype=torch.uint8, device=self.eds.device)
+
     def roots(self, stream: Optional[torch.cuda.Stream] = None) -> None:
         self._ck(self.ctx._L.dagpu_roots_device(
             self.ctx.handle, self.k, self.n, _abi.addr(self.eds), _abi.addr(self.row_roots),

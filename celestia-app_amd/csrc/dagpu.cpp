@@ -459,23 +459,241 @@ int dagpu_encode(dagpu_ctx* ctx, uint32_t k, size_t nvec, size_t shard_size,
 
 int dagpu_decode(dagpu_ctx* ctx, uint32_t k, size_t nvec, size_t shard_size, uint8_t* shards,
                  const uint8_t* present) {
-  (void)k; (void)nvec; (void)shard_size; (void)shards; (void)present;
-  return set_err(ctx, DAGPU_ERR_UNSUPPORTED, "decode not implemented yet");
+  if (!ctx || (nvec && (!shards || !present))) return DAGPU_ERR_ARG;
+  if (shard_size == 0 || shard_size % 64)
+    return set_err(ctx, DAGPU_ERR_SHARE_SIZE, "shard size must be a multiple of 64");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  (void)hipSetDevice(ctx->device);
+  int rc = check_k(ctx, k);
+  if (rc) return rc;
+  if (nvec == 0) return DAGPU_OK;
+  const size_t n = 2 * (size_t)k;
+  const size_t bytes = n * shard_size * nvec;
+  hipStream_t s = ctx->stream;
+  HIP_TRY(ctx, ctx->eds.ensure(bytes));
+  HIP_TRY(ctx, ctx->ods.ensure(n * nvec));
+  HIP_TRY(ctx, ctx->ws.ensure(nvec * 256 + nvec * sizeof(int32_t) + 256));
+  HIP_TRY(ctx, ctx->status.ensure(sizeof(int32_t)));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->eds.p, shards, bytes, hipMemcpyHostToDevice, s));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->ods.p, present, n * nvec, hipMemcpyHostToDevice, s));
+  HIP_TRY(ctx, hipMemsetAsync(ctx->status.p, 0, sizeof(int32_t), s));
+  DecodeArgs da{};
+  da.data = (uint8_t*)ctx->eds.p;
+  da.sq_stride = 0;
+  da.vec_stride = (long)(n * shard_size);
+  da.shard_stride = (long)shard_size;
+  da.present = (uint8_t*)ctx->ods.p;
+  da.p_sq_stride = 0;
+  da.p_vec_stride = (long)n;
+  da.p_shard_stride = 1;
+  da.err = (uint8_t*)ctx->ws.p;
+  da.flags = (int32_t*)((uint8_t*)ctx->ws.p + nvec * 256);
+  da.too_few = (int32_t*)ctx->status.p;
+  da.nsq = 1;
+  da.nvec = (long)nvec;
+  da.nchunk = (long)((shard_size + 511) / 512);
+  da.shard_bytes = (long)shard_size;
+  da.k = (int)k;
+  {
+    ProfScope p(ctx, 5, s);
+    HIP_TRY(ctx, launch_leo8_decode(da, s, false));
+  }
+  int32_t too_few = 0;
+  HIP_TRY(ctx, hipMemcpyAsync(&too_few, ctx->status.p, sizeof too_few, hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipMemcpyAsync(shards, ctx->eds.p, bytes, hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipStreamSynchronize(s));
+  if (too_few) return set_err(ctx, DAGPU_ERR_TOO_FEW_SHARDS, "too few shards given");
+  return DAGPU_OK;
 }
 
-int dagpu_repair(dagpu_ctx* ctx, uint32_t k, uint8_t* eds, uint8_t* present,
-                 const uint8_t* row_roots, const uint8_t* col_roots) {
-  (void)k; (void)eds; (void)present; (void)row_roots; (void)col_roots;
-  return set_err(ctx, DAGPU_ERR_UNSUPPORTED, "repair not implemented yet");
+namespace {
+
+struct RepairWs {
+  SquareArgs sa;        // NMT verification (roots of the repaired square)
+  uint8_t* p0;          // presence before repair
+  int32_t* complete_before;
+  int32_t* complete_now;
+  uint8_t* err_rows;
+  uint8_t* err_cols;
+  int32_t* flags_rows;
+  int32_t* flags_cols;
+  int32_t* bits;
+  int32_t* counters;    // [0] decodable rows, [1] decodable cols
+};
+
+size_t a256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+size_t repair_ws_bytes(uint32_t k, size_t n) {
+  const size_t w = 2 * (size_t)k;
+  size_t t = a256(nmt_workspace_bytes((int)k, (long)n));
+  t += 2 * a256(n * w * kNodeSize) + a256(n * 32) + a256(n * 4);  // got roots, dah, nmt status
+  t += a256(n * w * w);                                           // p0
+  t += 2 * a256(n * 2 * w * 4);                                   // complete before/now
+  t += 2 * a256(n * w * 256) + 2 * a256(n * w * 4);               // err, flags
+  t += a256(n * 4) + 256;                                         // bits, counters
+  return t;
+}
+
+RepairWs carve_repair(uint32_t k, size_t n, void* base) {
+  const size_t w = 2 * (size_t)k;
+  uint8_t* p = (uint8_t*)base;
+  RepairWs r{};
+  r.sa.k = (int)k;
+  r.sa.nsq = (long)n;
+  nmt_workspace_carve(r.sa, p);
+  p += a256(nmt_workspace_bytes((int)k, (long)n));
+  r.sa.row_roots = p; p += a256(n * w * kNodeSize);
+  r.sa.col_roots = p; p += a256(n * w * kNodeSize);
+  r.sa.dah = p; p += a256(n * 32);
+  r.sa.status = (int32_t*)p; p += a256(n * 4);
+  r.p0 = p; p += a256(n * w * w);
+  r.complete_before = (int32_t*)p; p += a256(n * 2 * w * 4);
+  r.complete_now = (int32_t*)p; p += a256(n * 2 * w * 4);
+  r.err_rows = p; p += a256(n * w * 256);
+  r.err_cols = p; p += a256(n * w * 256);
+  r.flags_rows = (int32_t*)p; p += a256(n * w * 4);
+  r.flags_cols = (int32_t*)p; p += a256(n * w * 4);
+  r.bits = (int32_t*)p; p += a256(n * 4);
+  r.counters = (int32_t*)p;
+  return r;
+}
+
+DecodeArgs axis_decode_args(uint32_t k, size_t n, uint8_t* eds, uint8_t* present, int axis,
+                            const RepairWs& r) {
+  const long w = 2L * k;
+  DecodeArgs d{};
+  d.data = eds;
+  d.sq_stride = (long)eds_bytes(k);
+  d.present = present;
+  d.p_sq_stride = w * w;
+  if (axis == 0) {
+    d.vec_stride = w * (long)kSS; d.shard_stride = kSS;
+    d.p_vec_stride = w; d.p_shard_stride = 1;
+    d.err = r.err_rows; d.flags = r.flags_rows; d.ndecodable = r.counters + 0;
+  } else {
+    d.vec_stride = kSS; d.shard_stride = w * (long)kSS;
+    d.p_vec_stride = 1; d.p_shard_stride = w;
+    d.err = r.err_cols; d.flags = r.flags_cols; d.ndecodable = r.counters + 1;
+  }
+  d.nsq = (long)n;
+  d.nvec = w;
+  d.nchunk = 1;
+  d.shard_bytes = kSS;
+  d.k = (int)k;
+  return d;
+}
+
+// rsmt2d Repair for n same-k squares resident on the device (see repair.hip).
+int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t* d_present,
+                  const uint8_t* d_rr, const uint8_t* d_cr, int32_t* d_status, void* d_ws,
+                  hipStream_t s) {
+  const long w = 2L * k;
+  RepairWs r = carve_repair(k, n, d_ws);
+  HIP_TRY(ctx, hipMemcpyAsync(r.p0, d_present, n * w * w, hipMemcpyDeviceToDevice, s));
+  HIP_TRY(ctx, hipMemsetAsync(r.bits, 0, n * sizeof(int32_t), s));
+  HIP_TRY(ctx, launch_axis_complete(d_present, (int)k, (long)n, r.complete_before, s));
+  // prerepairSanityCheck: complete axes must satisfy parity == Encode(data)
+  for (int axis = 0; axis < 2; axis++) {
+    EncodeArgs e{};
+    e.in = d_eds;
+    e.in_sq_stride = (long)eds_bytes(k);
+    e.out_sq_stride = (long)eds_bytes(k);
+    if (axis == 0) {
+      e.in_vec_stride = w * kSS; e.in_shard_stride = kSS;
+      e.out = d_eds + (long)k * kSS; e.out_vec_stride = w * kSS; e.out_shard_stride = kSS;
+    } else {
+      e.in_vec_stride = kSS; e.in_shard_stride = w * kSS;
+      e.out = d_eds + (long)k * w * kSS; e.out_vec_stride = kSS; e.out_shard_stride = w * kSS;
+    }
+    e.nsq = (long)n; e.nvec = w; e.nchunk = 1; e.shard_bytes = kSS;
+    e.vec_flags = r.complete_before + (long)axis * n * w;
+    e.mismatch = r.bits;
+    e.mismatch_bit = kRepPreByz;
+    HIP_TRY(ctx, launch_leo8_encode((int)k, e, s));
+  }
+  // solveCrossword: each round rebuilds every decodable row or every decodable
+  // column (whichever set is larger) until no axis can make progress.
+  const int max_rounds = 4 * (int)w + 4;
+  for (int round = 0; round < max_rounds; round++) {
+    DecodeArgs dr = axis_decode_args(k, n, d_eds, d_present, 0, r);
+    DecodeArgs dc = axis_decode_args(k, n, d_eds, d_present, 1, r);
+    HIP_TRY(ctx, hipMemsetAsync(r.counters, 0, 2 * sizeof(int32_t), s));
+    HIP_TRY(ctx, launch_leo8_errlocs(dr, s));
+    HIP_TRY(ctx, launch_leo8_errlocs(dc, s));
+    int32_t cnt[2] = {0, 0};
+    HIP_TRY(ctx, hipMemcpyAsync(cnt, r.counters, sizeof cnt, hipMemcpyDeviceToHost, s));
+    HIP_TRY(ctx, hipStreamSynchronize(s));
+    if (cnt[0] == 0 && cnt[1] == 0) break;
+    ProfScope p(ctx, 5, s);
+    HIP_TRY(ctx, launch_leo8_decode_only(cnt[0] >= cnt[1] ? dr : dc, s, true));
+  }
+  // verify every complete axis against the given roots
+  HIP_TRY(ctx, launch_axis_complete(d_present, (int)k, (long)n, r.complete_now, s));
+  r.sa.eds = d_eds;
+  r.sa.eds_sq_stride = (long)eds_bytes(k);
+  int rc = enqueue_roots(ctx, k, n, d_eds, r.sa.row_roots, r.sa.col_roots, r.sa.dah, r.sa.status,
+                         r.sa.digests, s);
+  if (rc) return rc;
+  HIP_TRY(ctx, launch_verify_roots(d_rr, d_cr, r.sa.row_roots, r.sa.col_roots, r.complete_now,
+                                   r.complete_before, (int)k, (long)n, r.bits, s));
+  HIP_TRY(ctx, launch_finalize_repair(r.bits, (long)n, d_status, s));
+  return DAGPU_OK;
+}
+
+}  // namespace
+
+size_t dagpu_repair_workspace_size(uint32_t k, size_t n) {
+  if (k == 0 || n == 0) return 256;
+  return repair_ws_bytes(k, n) + 256;
 }
 
 int dagpu_repair_batch_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds,
                               uint8_t* d_present, const uint8_t* d_row_roots,
                               const uint8_t* d_col_roots, int32_t* d_status, void* d_workspace,
                               void* stream) {
-  (void)k; (void)n; (void)d_eds; (void)d_present; (void)d_row_roots; (void)d_col_roots;
-  (void)d_status; (void)d_workspace; (void)stream;
-  return set_err(ctx, DAGPU_ERR_UNSUPPORTED, "repair not implemented yet");
+  if (!ctx || !d_eds || !d_present || !d_row_roots || !d_col_roots || !d_status || !d_workspace)
+    return DAGPU_ERR_ARG;
+  int rc = check_k(ctx, k);
+  if (rc) return rc;
+  if (n == 0) return DAGPU_OK;
+  return repair_device(ctx, k, n, d_eds, d_present, d_row_roots, d_col_roots, d_status, d_workspace,
+                       (hipStream_t)stream);
+}
+
+int dagpu_repair(dagpu_ctx* ctx, uint32_t k, uint8_t* eds, uint8_t* present,
+                 const uint8_t* row_roots, const uint8_t* col_roots) {
+  if (!ctx || !eds || !present || !row_roots || !col_roots) return DAGPU_ERR_ARG;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  (void)hipSetDevice(ctx->device);
+  int rc = check_k(ctx, k);
+  if (rc) return rc;
+  const size_t w = 2 * (size_t)k;
+  hipStream_t s = ctx->stream;
+  HIP_TRY(ctx, ctx->eds.ensure(eds_bytes(k)));
+  HIP_TRY(ctx, ctx->ods.ensure(w * w));
+  HIP_TRY(ctx, ctx->rr.ensure(w * kNodeSize));
+  HIP_TRY(ctx, ctx->cr.ensure(w * kNodeSize));
+  HIP_TRY(ctx, ctx->status.ensure(sizeof(int32_t)));
+  HIP_TRY(ctx, ctx->ws.ensure(dagpu_repair_workspace_size(k, 1)));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->eds.p, eds, eds_bytes(k), hipMemcpyHostToDevice, s));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->ods.p, present, w * w, hipMemcpyHostToDevice, s));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->rr.p, row_roots, w * kNodeSize, hipMemcpyHostToDevice, s));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->cr.p, col_roots, w * kNodeSize, hipMemcpyHostToDevice, s));
+  rc = repair_device(ctx, k, 1, (uint8_t*)ctx->eds.p, (uint8_t*)ctx->ods.p, (const uint8_t*)ctx->rr.p,
+                     (const uint8_t*)ctx->cr.p, (int32_t*)ctx->status.p, ctx->ws.p, s);
+  if (rc) return rc;
+  int32_t st = 0;
+  HIP_TRY(ctx, hipMemcpyAsync(&st, ctx->status.p, sizeof st, hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipMemcpyAsync(eds, ctx->eds.p, eds_bytes(k), hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipMemcpyAsync(present, ctx->ods.p, w * w, hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipStreamSynchronize(s));
+  switch (st) {
+    case DAGPU_OK: return DAGPU_OK;
+    case DAGPU_ERR_BAD_ROOTS: return set_err(ctx, st, "bad root input");
+    case DAGPU_ERR_BYZANTINE: return set_err(ctx, st, "byzantine data");
+    case DAGPU_ERR_UNREPAIRABLE: return set_err(ctx, st, "failed to solve data square");
+    default: return set_err(ctx, st, "repair failed");
+  }
 }
 
 int dagpu_profile_enable(dagpu_ctx* ctx, int on) {

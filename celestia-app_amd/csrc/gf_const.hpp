@@ -28,6 +28,7 @@ struct Gf8Const {
   uint8_t log[256];
   uint8_t exp[256];
   uint8_t skew[255];
+  uint8_t walsh[256];  // logWalsh8 = FWHT(log with [0] = 0), decode only
   // perm tables per log_m: t[g][lm] = bytes c*(v << 2g), v = 0..3
   uint32_t t[4][256];
 };
@@ -78,6 +79,24 @@ constexpr Gf8Const make_gf8_const() {
     }
   }
   for (int i = 0; i < 255; i++) g.skew[i] = g.log[g.skew[i]];
+
+  // logWalsh8: fwht8(log with [0] = 0, m = mtrunc = 256)
+  {
+    for (int i = 0; i < 256; i++) g.walsh[i] = g.log[i];
+    g.walsh[0] = 0;
+    auto addm = [](unsigned a, unsigned b) -> uint8_t { unsigned s = a + b; return (uint8_t)(s + (s >> 8)); };
+    auto subm = [](unsigned a, unsigned b) -> uint8_t { unsigned d = a - b; return (uint8_t)(d + (d >> 8)); };
+    for (int dist = 1, dist4 = 4; dist4 <= 256; dist = dist4, dist4 <<= 2) {
+      for (int r = 0; r < 256; r += dist4) {
+        for (int i = r; i < r + dist; i++) {
+          uint8_t t0 = g.walsh[i], t1 = g.walsh[i + dist], t2 = g.walsh[i + 2 * dist], t3 = g.walsh[i + 3 * dist];
+          uint8_t a0 = addm(t0, t1), a1 = subm(t0, t1), a2 = addm(t2, t3), a3 = subm(t2, t3);
+          g.walsh[i] = addm(a0, a2); g.walsh[i + 2 * dist] = subm(a0, a2);
+          g.walsh[i + dist] = addm(a1, a3); g.walsh[i + 3 * dist] = subm(a1, a3);
+        }
+      }
+    }
+  }
 
   for (int lm = 0; lm < 256; lm++) {
     for (int grp = 0; grp < 4; grp++) {

@@ -25,9 +25,50 @@ struct EncodeArgs {
   long copy_sq_stride, copy_vec_stride, copy_shard_stride;
   long nsq, nvec, nchunk;  // nchunk = ceil(shard_bytes / 512)
   long shard_bytes;
+  // Compare mode (rsmt2d prerepairSanityCheck): when `mismatch` is set the
+  // kernel compares the computed parity with the bytes already at `out` and
+  // ORs `mismatch_bit` into mismatch[square] on any difference; vectors whose
+  // vec_flags entry is 0 are skipped.
+  const int32_t* vec_flags;
+  int32_t* mismatch;
+  int mismatch_bit;
 };
 
 hipError_t launch_leo8_encode(int k, const EncodeArgs& a, hipStream_t s);
+
+// Decode addressing: shard i of vector (s, v) at
+//   data + s*sq_stride + v*vec_stride + i*shard_stride   (2k shards)
+// and its presence flag at present + s*p_sq_stride + v*p_vec_stride + i*p_shard_stride.
+struct DecodeArgs {
+  uint8_t* data;
+  long sq_stride, vec_stride, shard_stride;
+  uint8_t* present;
+  long p_sq_stride, p_vec_stride, p_shard_stride;
+  uint8_t* err;        // workspace: nsq*nvec*256 error locators
+  int32_t* flags;      // workspace: nsq*nvec (1 = vector decoded this pass)
+  int32_t* too_few;    // optional: set to 1 if any vector has < k shards
+  int32_t* progress;   // optional: += number of vectors rebuilt (mark pass)
+  int32_t* ndecodable; // optional: += number of decodable vectors (errlocs pass)
+  long nsq, nvec, nchunk, shard_bytes;
+  int k;
+};
+
+hipError_t launch_leo8_decode(const DecodeArgs& a, hipStream_t s, bool mark_present);
+hipError_t launch_leo8_errlocs(const DecodeArgs& a, hipStream_t s);
+hipError_t launch_leo8_decode_only(const DecodeArgs& a, hipStream_t s, bool mark_present);
+
+// Repair helpers (repair.hip).  Status bits per square:
+constexpr int kRepPreByz = 1;      // complete axis whose parity != Encode(data)
+constexpr int kRepBadRoots = 2;    // axis complete before repair, root mismatch
+constexpr int kRepByz = 4;         // rebuilt axis, root mismatch
+constexpr int kRepIncomplete = 8;  // crossword could not finish
+// complete[sq*2w + axis*w + idx] = axis fully present
+hipError_t launch_axis_complete(const uint8_t* present, int k, long nsq, int32_t* complete, hipStream_t s);
+hipError_t launch_verify_roots(const uint8_t* exp_rr, const uint8_t* exp_cr, const uint8_t* got_rr,
+                               const uint8_t* got_cr, const int32_t* complete_now,
+                               const int32_t* complete_before, int k, long nsq, int32_t* bits,
+                               hipStream_t s);
+hipError_t launch_finalize_repair(const int32_t* bits, long nsq, int32_t* status, hipStream_t s);
 
 struct SquareArgs {
   const uint8_t* eds;   // nsq squares, each (2k)^2 * 512 B, row-major

@@ -1,0 +1,55 @@
+// leo8.hpp -- Leopard GF(2^8) butterflies and multiplies shared by the encode
+// (rs_gf8.hip) and decode (rs_decode.hip) kernels.  Restates the element-wise
+// operations of klauspost/reedsolomon v1.11.8 leopard8.go (mulAdd8/refMulAdd8,
+// ifftDIT28, fftDIT28, mulgf8) on 4 packed bytes per lane.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gf_const.hpp"
+
+namespace dagpu {
+
+// x ^= y * exp(log_m)    (leopard8.go mulAdd8 / refMulAdd8): 7 index ops,
+// 4 v_perm_b32 (one SGPR table each), 2 v_bitop3 xor3.
+__device__ __forceinline__ void gf8_muladd(uint32_t& x, uint32_t y, const int lm) {
+  const uint32_t p0 = __builtin_amdgcn_perm(kGf8.t[0][lm], kGf8.t[0][lm], y & 0x03030303u);
+  const uint32_t p1 = __builtin_amdgcn_perm(kGf8.t[1][lm], kGf8.t[1][lm], (y >> 2) & 0x03030303u);
+  const uint32_t p2 = __builtin_amdgcn_perm(kGf8.t[2][lm], kGf8.t[2][lm], (y >> 4) & 0x03030303u);
+  const uint32_t p3 = __builtin_amdgcn_perm(kGf8.t[3][lm], kGf8.t[3][lm], (y >> 6) & 0x03030303u);
+  x = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(x, p0, p1, 0x96), p2, p3, 0x96);
+}
+
+// Raw buffer resource over [base, base + 2^31): all offsets used by one block
+// (k shards at stride <= 2k*512 B) stay far below that.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
+  const uint64_t p = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+  void* bp = (void*)(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(bp, (short)0, 0x7FFFFFFF, 0x00020000);
+}
+
+// ifftDIT28: y ^= x; x ^= y*log_m (multiply skipped when log_m == 255)
+__device__ __forceinline__ void ifft2(uint32_t& x, uint32_t& y, const int lm) {
+  y ^= x;
+  if (lm != kGf8Mod) gf8_muladd(x, y, lm);
+}
+// fftDIT28: x ^= y*log_m; y ^= x
+__device__ __forceinline__ void fft2(uint32_t& x, uint32_t& y, const int lm) {
+  if (lm != kGf8Mod) gf8_muladd(x, y, lm);
+  y ^= x;
+}
+
+// x = y * exp(log_m) with a RUNTIME log_m (decode multipliers): the four
+// table dwords come from constant memory (wave-uniform index -> scalar loads).
+__device__ __forceinline__ uint32_t gf8_mul_rt(uint32_t y, uint32_t lm) {
+  const uint32_t t0 = kGf8.t[0][lm], t1 = kGf8.t[1][lm], t2 = kGf8.t[2][lm], t3 = kGf8.t[3][lm];
+  const uint32_t p0 = __builtin_amdgcn_perm(t0, t0, y & 0x03030303u);
+  const uint32_t p1 = __builtin_amdgcn_perm(t1, t1, (y >> 2) & 0x03030303u);
+  const uint32_t p2 = __builtin_amdgcn_perm(t2, t2, (y >> 4) & 0x03030303u);
+  const uint32_t p3 = __builtin_amdgcn_perm(t3, t3, (y >> 6) & 0x03030303u);
+  return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(p0, p1, p2, 0x96), p3, 0u, 0x96);
+}
+
+}  // namespace dagpu

@@ -1,0 +1,353 @@
+// rs_decode.hip -- Leopard GF(2^8) reconstruct (decode) on gfx950.
+//
+// Replaces klauspost/reedsolomon v1.11.8 leopardFF8.reconstruct, reached from
+// rsmt2d v0.11.0 LeoRSCodec.Decode inside ExtendedDataSquare.Repair
+// (solveCrosswordRow/Col -> rebuildShares), SURVEY.md §3.5 and §8a row A11.
+//
+// Per vector of n = 2k shards with >= k present:
+//   1. error locator (kernel 1, one wave per vector):
+//        errLocs[i] = 1 for each missing position (work layout: [parity k][data k]),
+//        FWHT(errLocs, mtrunc = n); errLocs[i] = errLocs[i]*logWalsh[i] mod 255;
+//        FWHT(errLocs, 256)
+//   2. decode (kernel 2, one thread per dword column of the vector):
+//        work[i] = present ? shard*errLocs[i] : 0
+//        IFFT_n (decoder skew: fftSkew[iend-1]) ; formal derivative ; FFT_n
+//        missing shard = work[pos] * (255 - errLocs[pos])
+// The transform runs register-resident exactly like the encoder.  For k = 128
+// (n = 256 elements per dword column) one workgroup splits the column over two
+// halves of 128 elements each (waves 0-1 / waves 2-3): only the last IFFT
+// layer, the derivative's middle step and the first FFT layer cross halves, and
+// those exchange values through LDS in 32-element chunks.
+// MDS codes have a unique decoding, so any correct decoder is bit-exact; this
+// one is also step-for-step the reference algorithm.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.hpp"
+#include "leo8.hpp"
+
+namespace dagpu {
+
+// ---------------------------------------------------------------------------
+// Kernel 1: error locators.  One 64-thread block per vector.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t add_mod8(uint32_t a, uint32_t b) {
+  const uint32_t s = a + b;
+  return (s + (s >> 8)) & 0xFFu;
+}
+__device__ __forceinline__ uint32_t sub_mod8(uint32_t a, uint32_t b) {
+  const uint32_t d = a - b;
+  return (d + (d >> 8)) & 0xFFu;
+}
+
+// fwht8(data, m = 256, mtrunc): 4 radix-4 passes, 64 groups of 4 each.
+__device__ __forceinline__ void fwht256_lds(uint32_t* e, int mtrunc) {
+  const int g = threadIdx.x;  // 0..63
+#pragma unroll
+  for (int dist = 1; dist <= 64; dist *= 4) {
+    const int dist4 = dist * 4;
+    const int r = (g / dist) * dist4;
+    const int i = r + (g % dist);
+    if (r < mtrunc) {
+      const uint32_t t0 = e[i], t1 = e[i + dist], t2 = e[i + 2 * dist], t3 = e[i + 3 * dist];
+      const uint32_t a0 = add_mod8(t0, t1), a1 = sub_mod8(t0, t1);
+      const uint32_t a2 = add_mod8(t2, t3), a3 = sub_mod8(t2, t3);
+      e[i] = add_mod8(a0, a2);
+      e[i + 2 * dist] = sub_mod8(a0, a2);
+      e[i + dist] = add_mod8(a1, a3);
+      e[i + 3 * dist] = sub_mod8(a1, a3);
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(64) void leo8_errlocs_kernel(DecodeArgs a) {
+  __shared__ uint32_t e[256];
+  const long v = blockIdx.x;  // flattened (square, vector)
+  const long sq = v / a.nvec, vec = v % a.nvec;
+  const int k = a.k, n = 2 * k;
+  const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
+  int cnt = 0;
+  for (int i = threadIdx.x; i < 256; i += 64) {
+    uint32_t x = 0;
+    if (i < k) x = pres[(long)(k + i) * a.p_shard_stride] ? 0u : 1u;          // parity k+i -> work i
+    else if (i < n) x = pres[(long)(i - k) * a.p_shard_stride] ? 0u : 1u;     // data i-k -> work i
+    e[i] = x;
+    if (i < n) cnt += (x == 0);
+  }
+  // wave-wide count of present shards
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+  __syncthreads();
+  const bool decode = cnt >= k && cnt < n;
+  if (threadIdx.x == 0) {
+    a.flags[v] = decode ? 1 : 0;
+    if (cnt < k && a.too_few) atomicOr(a.too_few, 1);
+    if (decode && a.ndecodable) atomicAdd(a.ndecodable, 1);
+  }
+  if (!decode) return;  // uniform
+  fwht256_lds(e, n);
+  for (int i = threadIdx.x; i < 256; i += 64) e[i] = (e[i] * kGf8.walsh[i]) % 255u;
+  __syncthreads();
+  fwht256_lds(e, 256);
+  uint8_t* out = a.err + v * 256;
+  for (int i = threadIdx.x; i < n; i += 64) out[i] = (uint8_t)e[i];
+}
+
+// ---------------------------------------------------------------------------
+// Kernel 2: decode.  N = 2K work elements; thread half h holds [h*E, (h+1)*E).
+// ---------------------------------------------------------------------------
+// ifftDITDecoder8 radix-4 layers entirely inside this half (dist4 <= E).
+template <int N, int E, int BASE, int DIST>
+__device__ __forceinline__ void ifft_dec_local(uint32_t (&w)[E]) {
+  if constexpr (DIST * 4 <= E) {
+#pragma unroll
+    for (int r = 0; r < E; r += DIST * 4) {
+      const int iend = BASE + r + DIST;  // global index
+      const int l01 = kGf8.skew[iend - 1];
+      const int l02 = kGf8.skew[iend + DIST - 1];
+      const int l23 = kGf8.skew[iend + 2 * DIST - 1];
+#pragma unroll
+      for (int i = r; i < r + DIST; i++) {
+        ifft2(w[i], w[i + DIST], l01);
+        ifft2(w[i + 2 * DIST], w[i + 3 * DIST], l23);
+        ifft2(w[i], w[i + 2 * DIST], l02);
+        ifft2(w[i + DIST], w[i + 3 * DIST], l02);
+      }
+    }
+    ifft_dec_local<N, E, BASE, DIST * 4>(w);
+  } else if constexpr (E == N && DIST < N) {
+    // one layer left (N = 2 * 4^j), only when the whole vector is local
+    const int lm = kGf8.skew[DIST - 1];
+#pragma unroll
+    for (int i = 0; i < DIST; i++) ifft2(w[i], w[i + DIST], lm);
+  }
+}
+
+// fftDIT8 radix-4 layers with dist4 <= E (inside this half), then the final
+// radix-2 layer when it exists.
+template <int N, int E, int BASE, int DIST4>
+__device__ __forceinline__ void fft_dec_local(uint32_t (&w)[E]) {
+  constexpr int DIST = DIST4 >> 2;
+  if constexpr (DIST != 0) {
+#pragma unroll
+    for (int r = 0; r < E; r += DIST4) {
+      const int iend = BASE + r + DIST;
+      const int l01 = kGf8.skew[iend - 1];
+      const int l02 = kGf8.skew[iend + DIST - 1];
+      const int l23 = kGf8.skew[iend + 2 * DIST - 1];
+#pragma unroll
+      for (int i = r; i < r + DIST; i++) {
+        fft2(w[i], w[i + 2 * DIST], l02);
+        fft2(w[i + DIST], w[i + 3 * DIST], l02);
+        fft2(w[i], w[i + DIST], l01);
+        fft2(w[i + 2 * DIST], w[i + 3 * DIST], l23);
+      }
+    }
+    fft_dec_local<N, E, BASE, DIST>(w);
+  } else if constexpr (DIST4 == 2) {
+#pragma unroll
+    for (int r = 0; r < E; r += 2) fft2(w[r], w[r + 1], kGf8.skew[BASE + r]);
+  }
+}
+
+// formal derivative steps i in (0, E) of a half: work[i-width, i) ^= work[i, i+width)
+template <int E>
+__device__ __forceinline__ void derivative_local(uint32_t (&w)[E]) {
+#pragma unroll
+  for (int i = 1; i < E; i++) {
+    const int width = ((i ^ (i - 1)) + 1) >> 1;
+#pragma unroll
+    for (int j = 0; j < width; j++) w[i - width + j] ^= w[i + j];
+  }
+}
+
+template <int K>
+struct DecOcc { static constexpr int waves = K >= 64 ? 2 : (K >= 32 ? 4 : 8); };
+
+// Whole decode of one dword column for half HH (compile-time) of H halves.
+// With H == 2 the two halves live in the same workgroup (waves 0-1: HH = 0,
+// waves 2-3: HH = 1) and meet at the same sequence of barriers.
+template <int K, int H, int HH>
+__device__ __forceinline__ void decode_half(const DecodeArgs& a, long v, int t, uint32_t col, bool active,
+                                            uint32_t (*xch)[32][128]) {
+  constexpr int N = 2 * K;
+  constexpr int E = N / H;
+  const long sq = v / a.nvec, vec = v % a.nvec;
+  uint8_t* base = a.data + sq * a.sq_stride + vec * a.vec_stride;
+  const auto rsrc = make_rsrc(base);
+  const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
+  const uint8_t* err = a.err + v * 256;
+  const uint32_t ss = (uint32_t)a.shard_stride;
+
+  // 1. work[i] = present ? shard * errLocs[i] : 0   ([parity K][data K])
+  uint32_t w[E];
+#pragma unroll
+  for (int j = 0; j < E; j++) {
+    const int i = HH * E + j;
+    const int s = i < K ? K + i : i - K;
+    const bool p = pres[(long)s * a.p_shard_stride] != 0;
+    uint32_t x = 0;
+    if (p && active) x = __builtin_amdgcn_raw_buffer_load_b32(rsrc, col, (uint32_t)s * ss, 0);
+    w[j] = p ? gf8_mul_rt(x, err[i]) : 0u;
+  }
+
+  if constexpr (H == 1) {
+    ifft_dec_local<N, N, 0, 1>(w);
+    derivative_local<N>(w);
+    fft_dec_local<N, N, 0, N>(w);
+  } else {
+    static_assert(N == 256, "split decode is specialised for n = 256");
+    constexpr int D = N / 4;  // 64: last IFFT / first FFT radix-4 distance
+    constexpr int l01 = kGf8.skew[D - 1], l02 = kGf8.skew[2 * D - 1], l23 = kGf8.skew[3 * D - 1];
+    // ---- IFFT: local radix-4 layers (dist 1, 4, 16) ----
+    ifft_dec_local<N, E, HH * E, 1>(w);
+    // ---- last layer (dist = 64, one group): sub-layer 1 local ----
+#pragma unroll
+    for (int i = 0; i < D; i++) ifft2(w[i], w[i + D], HH == 0 ? l01 : l23);
+    // sub-layer 2 crosses halves: lower j <-> upper j
+#pragma unroll
+    for (int c = 0; c < E / 32; c++) {
+#pragma unroll
+      for (int q = 0; q < 32; q++) xch[HH][q][t] = w[32 * c + q];
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < 32; q++) {
+        const uint32_t o = xch[1 - HH][q][t];
+        if constexpr (HH == 0) {  // x = mine, y = o: y' = y ^ x; x ^= y' * L
+          const uint32_t y2 = o ^ w[32 * c + q];
+          if (l02 != kGf8Mod) gf8_muladd(w[32 * c + q], y2, l02);
+        } else {                  // y = mine, x = o: y' = y ^ x
+          w[32 * c + q] ^= o;
+        }
+      }
+      __syncthreads();
+    }
+    // ---- formal derivative: lower local steps, lower ^= upper(pre-local), upper local ----
+    if constexpr (HH == 0) derivative_local<E>(w);
+#pragma unroll
+    for (int c = 0; c < E / 32; c++) {
+      if constexpr (HH == 1) {
+#pragma unroll
+        for (int q = 0; q < 32; q++) xch[1][q][t] = w[32 * c + q];
+      }
+      __syncthreads();
+      if constexpr (HH == 0) {
+#pragma unroll
+        for (int q = 0; q < 32; q++) w[32 * c + q] ^= xch[1][q][t];
+      }
+      __syncthreads();
+    }
+    if constexpr (HH == 1) derivative_local<E>(w);
+    // ---- FFT first layer (dist4 = 256, dist = 64): sub-layer 1 crosses ----
+#pragma unroll
+    for (int c = 0; c < E / 32; c++) {
+#pragma unroll
+      for (int q = 0; q < 32; q++) xch[HH][q][t] = w[32 * c + q];
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < 32; q++) {
+        const uint32_t o = xch[1 - HH][q][t];
+        // x = lower, y = upper: x' = x ^ y*L; y' = y ^ x'  (both halves compute x')
+        uint32_t xx = HH == 0 ? w[32 * c + q] : o;
+        const uint32_t yy = HH == 0 ? o : w[32 * c + q];
+        if (l02 != kGf8Mod) gf8_muladd(xx, yy, l02);
+        w[32 * c + q] = HH == 0 ? xx : (yy ^ xx);
+      }
+      __syncthreads();
+    }
+    // sub-layer 2: (i, i+D) lower with l01, (i+2D, i+3D) upper with l23
+#pragma unroll
+    for (int i = 0; i < D; i++) fft2(w[i], w[i + D], HH == 0 ? l01 : l23);
+    // ---- remaining FFT layers (dist4 = 64, 16, 4) local ----
+    fft_dec_local<N, E, HH * E, E / 2>(w);
+  }
+
+  // 5. missing shard s: work[pos] * (255 - errLocs[pos]), pos = s >= K ? s-K : s+K
+  if (!active) return;
+#pragma unroll
+  for (int j = 0; j < E; j++) {
+    const int pos = HH * E + j;
+    const int s = pos < K ? pos + K : pos - K;
+    if (pres[(long)s * a.p_shard_stride] == 0) {
+      const uint32_t y = gf8_mul_rt(w[j], 255u - err[pos]);
+      __builtin_amdgcn_raw_buffer_store_b32(y, rsrc, col, (uint32_t)s * ss, 0);
+    }
+  }
+}
+
+template <int K, int H>
+__global__ __launch_bounds__(128 * H)
+__attribute__((amdgpu_waves_per_eu(DecOcc<K>::waves, 8))) void leo8_decode_kernel(DecodeArgs a) {
+  const long blk = blockIdx.x;
+  const int chunk = (int)(blk % a.nchunk);
+  const long v = blk / a.nchunk;  // flattened (square, vector)
+  if (a.flags[v] == 0) return;   // uniform: nothing to decode for this vector
+  const int t = threadIdx.x & 127;
+  const uint32_t col = (uint32_t)chunk * 512u + (uint32_t)t * 4u;
+  const bool active = col < (uint32_t)a.shard_bytes;
+  if constexpr (H == 1) {
+    decode_half<K, 1, 0>(a, v, t, col, active, nullptr);
+  } else {
+    __shared__ uint32_t xch[2][32][128];
+    const int h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 7);  // wave-uniform
+    if (h == 0) decode_half<K, H, 0>(a, v, t, col, active, xch);
+    else decode_half<K, H, 1>(a, v, t, col, active, xch);
+  }
+}
+
+// Marks rebuilt shards present (separate launch so decode kernels of the same
+// pass read a stable presence map).
+__global__ __launch_bounds__(256) void mark_present_kernel(DecodeArgs a) {
+  const long v = blockIdx.x;
+  if (a.flags[v] == 0) return;
+  const long sq = v / a.nvec, vec = v % a.nvec;
+  uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
+  for (int i = threadIdx.x; i < 2 * a.k; i += 256) pres[(long)i * a.p_shard_stride] = 1;
+  if (threadIdx.x == 0 && a.progress) atomicAdd(a.progress, 1);
+}
+
+template <int K, int H>
+static hipError_t launch_dec(const DecodeArgs& a, hipStream_t s) {
+  const long blocks = a.nsq * a.nvec * a.nchunk;
+  hipLaunchKernelGGL((leo8_decode_kernel<K, H>), dim3((unsigned)blocks), dim3(128 * H), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_leo8_errlocs(const DecodeArgs& a, hipStream_t s) {
+  const long nv = a.nsq * a.nvec;
+  if (nv <= 0) return hipSuccess;
+  hipLaunchKernelGGL(leo8_errlocs_kernel, dim3((unsigned)nv), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_leo8_decode_only(const DecodeArgs& a, hipStream_t s, bool mark_present) {
+  const long nv = a.nsq * a.nvec;
+  if (nv <= 0) return hipSuccess;
+  hipError_t e = hipSuccess;
+  switch (a.k) {
+    case 1: e = launch_dec<1, 1>(a, s); break;
+    case 2: e = launch_dec<2, 1>(a, s); break;
+    case 4: e = launch_dec<4, 1>(a, s); break;
+    case 8: e = launch_dec<8, 1>(a, s); break;
+    case 16: e = launch_dec<16, 1>(a, s); break;
+    case 32: e = launch_dec<32, 1>(a, s); break;
+    case 64: e = launch_dec<64, 1>(a, s); break;
+    case 128: e = launch_dec<128, 2>(a, s); break;
+    default: return hipErrorInvalidValue;
+  }
+  if (e != hipSuccess) return e;
+  if (mark_present) {
+    hipLaunchKernelGGL(mark_present_kernel, dim3((unsigned)nv), dim3(256), 0, s, a);
+    e = hipGetLastError();
+  }
+  return e;
+}
+
+hipError_t launch_leo8_decode(const DecodeArgs& a, hipStream_t s, bool mark_present) {
+  hipError_t e = launch_leo8_errlocs(a, s);
+  if (e != hipSuccess) return e;
+  return launch_leo8_decode_only(a, s, mark_present);
+}
+
+}  // namespace dagpu

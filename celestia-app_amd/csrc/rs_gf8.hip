@@ -16,41 +16,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "gf_const.hpp"
 #include "kernels.hpp"
+#include "leo8.hpp"
 
 namespace dagpu {
-
-// x ^= y * exp(log_m)    (leopard8.go mulAdd8 / refMulAdd8): 7 index ops,
-// 4 v_perm_b32 (one SGPR table each), 2 v_bitop3 xor3.
-__device__ __forceinline__ void gf8_muladd(uint32_t& x, uint32_t y, const int lm) {
-  const uint32_t p0 = __builtin_amdgcn_perm(kGf8.t[0][lm], kGf8.t[0][lm], y & 0x03030303u);
-  const uint32_t p1 = __builtin_amdgcn_perm(kGf8.t[1][lm], kGf8.t[1][lm], (y >> 2) & 0x03030303u);
-  const uint32_t p2 = __builtin_amdgcn_perm(kGf8.t[2][lm], kGf8.t[2][lm], (y >> 4) & 0x03030303u);
-  const uint32_t p3 = __builtin_amdgcn_perm(kGf8.t[3][lm], kGf8.t[3][lm], (y >> 6) & 0x03030303u);
-  x = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(x, p0, p1, 0x96), p2, p3, 0x96);
-}
-
-// Raw buffer resource over [base, base + 2^31): all offsets used by one block
-// (k shards at stride <= 2k*512 B) stay far below that.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
-  const uint64_t p = (uint64_t)base;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
-  void* bp = (void*)(((uint64_t)hi << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(bp, (short)0, 0x7FFFFFFF, 0x00020000);
-}
-
-// ifftDIT28: y ^= x; x ^= y*log_m (multiply skipped when log_m == 255)
-__device__ __forceinline__ void ifft2(uint32_t& x, uint32_t& y, const int lm) {
-  y ^= x;
-  if (lm != kGf8Mod) gf8_muladd(x, y, lm);
-}
-// fftDIT28: x ^= y*log_m; y ^= x
-__device__ __forceinline__ void fft2(uint32_t& x, uint32_t& y, const int lm) {
-  if (lm != kGf8Mod) gf8_muladd(x, y, lm);
-  y ^= x;
-}
 
 // ifftDITEncoder8 with m = mtrunc = K, skewLUT = fftSkew8[m-1:]
 template <int K, int DIST>
@@ -120,12 +89,10 @@ __attribute__((amdgpu_waves_per_eu(EncOcc<K>::waves, 8))) void leo8_encode_kerne
   const long sv = blk / a.nchunk;
   const long vec = sv % a.nvec;
   const long sq = sv / a.nvec;
+  if (a.vec_flags && a.vec_flags[sv] == 0) return;  // uniform
   const uint32_t col = (uint32_t)chunk * 512u + threadIdx.x * 4u;  // byte offset inside shard
   if (col >= (uint32_t)a.shard_bytes) return;
 
-  // Buffer descriptors built from wave-uniform values (guide T8/T20): each
-  // shard access is buffer_load/store with voffset = col (shared by all k
-  // shards) and soffset = i*stride (SGPR), so no per-shard VGPR address.
   const auto in_rsrc = make_rsrc(a.in + sq * a.in_sq_stride + vec * a.in_vec_stride);
   const uint32_t in_stride = (uint32_t)a.in_shard_stride;
   uint32_t w[K];
@@ -145,6 +112,13 @@ __attribute__((amdgpu_waves_per_eu(EncOcc<K>::waves, 8))) void leo8_encode_kerne
 
   const auto out_rsrc = make_rsrc(a.out + sq * a.out_sq_stride + vec * a.out_vec_stride);
   const uint32_t out_stride = (uint32_t)a.out_shard_stride;
+  if (a.mismatch) {  // prerepairSanityCheck: parity must equal Encode(data)
+    uint32_t diff = 0;
+#pragma unroll
+    for (int i = 0; i < K; i++) diff |= w[i] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, col, i * out_stride, 0);
+    if (diff) atomicOr(&a.mismatch[sq], a.mismatch_bit);
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < K; i++) __builtin_amdgcn_raw_buffer_store_b32(w[i], out_rsrc, col, i * out_stride, 0);
 }

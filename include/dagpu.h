@@ -124,10 +124,11 @@ int dagpu_repair(dagpu_ctx* ctx, uint32_t k, uint8_t* eds, uint8_t* present,
                  const uint8_t* row_roots, const uint8_t* col_roots);
 
 /* Device-resident batched Repair: n squares of width k (device pointers),
- * d_present = n * (2k)^2 flags (updated), expected roots as produced by
+ * d_present = n * (2k)^2 flags (updated in place), expected roots as produced by
  * dagpu_extend_batch_device.  d_status gets one dagpu_status per square.
- * d_workspace: dagpu_workspace_size(k, n) bytes + n*(2k)^2*... see
- * dagpu_repair_workspace_size. */
+ * d_workspace: dagpu_repair_workspace_size(k, n) bytes.  Enqueued on `stream`;
+ * the call synchronises once per crossword round to read two counters. */
+size_t dagpu_repair_workspace_size(uint32_t k, size_t n);
 int dagpu_repair_batch_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds,
                               uint8_t* d_present, const uint8_t* d_row_roots,
                               const uint8_t* d_col_roots, int32_t* d_status,

@@ -193,3 +193,130 @@ def test_device_batch_full_size(ctx):
     ds.extend()
     torch.cuda.synchronize()
     assert (ds.dah.cpu().numpy() == dah).all()
+
+
+# --- decode / Repair (rsmt2d Repair, klauspost Reconstruct) -------------------
+
+@pytest.mark.parametrize("k", [1, 2, 4, 8, 16, 32, 64, 128])
+@pytest.mark.parametrize("shard", [64, 512, 1536])
+def test_codec_decode_matches_oracle(ctx, k, shard):
+    rng = np.random.default_rng(k * 7 + shard)
+    codec = da.LeoRSCodec(ctx)
+    data = rng.integers(0, 256, (k, shard), dtype=np.uint8)
+    full = np.concatenate([data, oracle.encode(data)])
+    for trial in range(3):
+        keep = rng.choice(2 * k, k + trial * (k // 4), replace=False)
+        shards = [full[i].tobytes() if i in set(keep.tolist()) else None for i in range(2 * k)]
+        out = codec.decode(shards)
+        assert b"".join(out) == full.tobytes()
+
+
+def test_codec_decode_too_few(ctx):
+    k = 8
+    codec = da.LeoRSCodec(ctx)
+    shards = [bytes(64)] * (k - 1) + [None] * (k + 1)
+    with pytest.raises(da.ErrTooFewShards):
+        codec.decode(shards)
+
+
+def _subgrid(k, seed):
+    rng = np.random.default_rng(seed)
+    w = 2 * k
+    present = np.zeros((w, w), bool)
+    present[np.ix_(rng.choice(w, k, replace=False), rng.choice(w, k, replace=False))] = True
+    return present
+
+
+@pytest.mark.parametrize("k", [1, 2, 8, 32, 128])
+def test_repair_max_erasure(ctx, k):
+    """C4: keep a k x k sub-grid (3k^2 erased), repair, every root re-verified."""
+    ods = synth.random_blob_square(k, 40 + k)
+    eds, rr, cr, _ = oracle.extend_and_dah(ods, k, nthreads=8)
+    present = _subgrid(k, k)
+    damaged = eds * present[:, :, None]
+    fixed, pres = da.repair(damaged, present, rr, cr, ctx)
+    assert pres.all()
+    assert (fixed == eds).all()
+
+
+@pytest.mark.parametrize("k", [4, 16])
+def test_repair_random_patterns_match_oracle(ctx, k):
+    rng = np.random.default_rng(k)
+    ods = synth.random_blob_square(k, 60 + k)
+    eds, rr, cr, _ = oracle.extend_and_dah(ods, k)
+    w = 2 * k
+    for frac in (0.3, 0.45, 0.6, 0.9):
+        present = rng.random((w, w)) < frac
+        damaged = eds * present[:, :, None]
+        orc, ofixed = oracle.repair(damaged, present, k, rr, cr)
+        try:
+            fixed, _ = da.repair(damaged, present, rr, cr, ctx)
+            code = 0
+        except da.DAError as e:
+            code, fixed = e.code, None
+        assert code == orc, frac
+        if code == 0:
+            assert (fixed == ofixed).all() and (fixed == eds).all()
+
+
+def test_repair_byzantine_and_errors(ctx):
+    k = 8
+    w = 2 * k
+    ods = synth.random_blob_square(k, 99)
+    eds, rr, cr, _ = oracle.extend_and_dah(ods, k)
+    present = _subgrid(k, 1)
+    damaged = eds * present[:, :, None]
+    # corrupt one present share: the rebuilt axes no longer match the roots
+    r, c = np.argwhere(present)[0]
+    bad = damaged.copy()
+    bad[r, c, 200] ^= 0x40
+    with pytest.raises(da.ErrByzantineData):
+        da.repair(bad, present, rr, cr, ctx)
+    # too few shares everywhere -> unrepairable
+    few = present.copy()
+    few[r, :] = False
+    few[:, c] = False
+    with pytest.raises(da.ErrUnrepairableDataSquare):
+        da.repair(eds * few[:, :, None], few, rr, cr, ctx)
+    # complete square whose parity is inconsistent but roots commit to it:
+    # prerepairSanityCheck -> ErrByzantineData
+    inc = eds.copy()
+    inc[0, w - 1, 7] ^= 1
+    irr, icr = oracle.compute_roots(inc, k)
+    full = np.ones((w, w), bool)
+    full[w - 1, w - 1] = False
+    with pytest.raises(da.ErrByzantineData):
+        da.repair(inc, full, irr, icr, ctx)
+    # complete axis with a wrong root -> "bad root input"
+    wrong = rr.copy()
+    wrong[0, 70] ^= 1
+    with pytest.raises(da.DAError, match="bad root input"):
+        da.repair(eds, full, wrong, cr, ctx)
+    # nothing missing and consistent -> no-op
+    fixed, _ = da.repair(eds, np.ones((w, w), bool), rr, cr, ctx)
+    assert (fixed == eds).all()
+
+
+def test_repair_device_batch(ctx):
+    """C4 on the device-resident batch API: 8 squares at k=128."""
+    import torch
+    from celestia_da.device import DeviceSquares
+
+    k, n = 128, 8
+    ds = DeviceSquares(k, n, ctx=ctx)
+    host = np.stack([synth.random_blob_square(k, 8100 + i).reshape(-1) for i in range(n)])
+    ds.ods.copy_(torch.from_numpy(host))
+    ds.extend()
+    eds_ref = ds.eds.clone()
+    w = 2 * k
+    pres = np.stack([_subgrid(k, 500 + i).reshape(-1) for i in range(n)]).astype(np.uint8)
+    present = torch.from_numpy(pres).cuda()
+    mask = present.view(n, w * w, 1).to(torch.uint8)
+    ds.eds.copy_((ds.eds.view(n, w * w, 512) * mask).view(n, -1))
+    status = torch.full((n,), -99, dtype=torch.int32, device="cuda")
+    ws = ds.repair_workspace()
+    ds.repair(present, status, ws)
+    torch.cuda.synchronize()
+    assert (status.cpu().numpy() == 0).all()
+    assert bool((present == 1).all())
+    assert torch.equal(ds.eds, eds_ref)
