@@ -156,7 +156,7 @@ int enqueue_rs(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_ods, uint8
   ra.shard_bytes = kSS;
   {
     ProfScope p(ctx, 0, s);
-    HIP_TRY(ctx, launch_leo8_encode((int)k, ra, s));
+    HIP_TRY(ctx, launch_rs_encode((int)k, ra, s));
   }
   // Column pass: vector c = column c of [Q0|Q1] -> [Q2|Q3].
   EncodeArgs ca{};
@@ -175,7 +175,7 @@ int enqueue_rs(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_ods, uint8
   ca.shard_bytes = kSS;
   {
     ProfScope p(ctx, 1, s);
-    HIP_TRY(ctx, launch_leo8_encode((int)k, ca, s));
+    HIP_TRY(ctx, launch_rs_encode((int)k, ca, s));
   }
   return DAGPU_OK;
 }
@@ -212,9 +212,9 @@ int enqueue_roots(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_eds, ui
 
 int check_k(dagpu_ctx* ctx, uint64_t k) {
   if (!is_pow2(k)) return set_err(ctx, DAGPU_ERR_ARG, "square width must be a power of two");
-  if (k > 128) {
+  if (k > (uint64_t)kMaxK) {
     return set_err(ctx, DAGPU_ERR_UNSUPPORTED,
-                   "k > 128 (GF(2^16) Leopard) is not implemented in this build");
+                   "square width k > " + std::to_string(kMaxK) + " is not supported");
   }
   return DAGPU_OK;
 }
@@ -451,7 +451,7 @@ int dagpu_encode(dagpu_ctx* ctx, uint32_t k, size_t nvec, size_t shard_size,
   ea.nvec = (long)nvec;
   ea.nchunk = (long)((shard_size + 511) / 512);
   ea.shard_bytes = (long)shard_size;
-  HIP_TRY(ctx, launch_leo8_encode((int)k, ea, s));
+  HIP_TRY(ctx, launch_rs_encode((int)k, ea, s));
   HIP_TRY(ctx, hipMemcpyAsync(parity, ctx->eds.p, bytes, hipMemcpyDeviceToHost, s));
   HIP_TRY(ctx, hipStreamSynchronize(s));
   return DAGPU_OK;
@@ -472,7 +472,8 @@ int dagpu_decode(dagpu_ctx* ctx, uint32_t k, size_t nvec, size_t shard_size, uin
   hipStream_t s = ctx->stream;
   HIP_TRY(ctx, ctx->eds.ensure(bytes));
   HIP_TRY(ctx, ctx->ods.ensure(n * nvec));
-  HIP_TRY(ctx, ctx->ws.ensure(nvec * 256 + nvec * sizeof(int32_t) + 256));
+  const size_t errb = (size_t)rs_err_bytes((int)k) * nvec;
+  HIP_TRY(ctx, ctx->ws.ensure(errb + nvec * sizeof(int32_t) + 256));
   HIP_TRY(ctx, ctx->status.ensure(sizeof(int32_t)));
   HIP_TRY(ctx, hipMemcpyAsync(ctx->eds.p, shards, bytes, hipMemcpyHostToDevice, s));
   HIP_TRY(ctx, hipMemcpyAsync(ctx->ods.p, present, n * nvec, hipMemcpyHostToDevice, s));
@@ -487,7 +488,7 @@ int dagpu_decode(dagpu_ctx* ctx, uint32_t k, size_t nvec, size_t shard_size, uin
   da.p_vec_stride = (long)n;
   da.p_shard_stride = 1;
   da.err = (uint8_t*)ctx->ws.p;
-  da.flags = (int32_t*)((uint8_t*)ctx->ws.p + nvec * 256);
+  da.flags = (int32_t*)((uint8_t*)ctx->ws.p + errb);
   da.too_few = (int32_t*)ctx->status.p;
   da.nsq = 1;
   da.nvec = (long)nvec;
@@ -496,7 +497,7 @@ int dagpu_decode(dagpu_ctx* ctx, uint32_t k, size_t nvec, size_t shard_size, uin
   da.k = (int)k;
   {
     ProfScope p(ctx, 5, s);
-    HIP_TRY(ctx, launch_leo8_decode(da, s, false));
+    HIP_TRY(ctx, launch_rs_decode(da, s, false));
   }
   int32_t too_few = 0;
   HIP_TRY(ctx, hipMemcpyAsync(&too_few, ctx->status.p, sizeof too_few, hipMemcpyDeviceToHost, s));
@@ -529,7 +530,7 @@ size_t repair_ws_bytes(uint32_t k, size_t n) {
   t += 2 * a256(n * w * kNodeSize) + a256(n * 32) + a256(n * 4);  // got roots, dah, nmt status
   t += a256(n * w * w);                                           // p0
   t += 2 * a256(n * 2 * w * 4);                                   // complete before/now
-  t += 2 * a256(n * w * 256) + 2 * a256(n * w * 4);               // err, flags
+  t += 2 * a256(n * w * rs_err_bytes((int)k)) + 2 * a256(n * w * 4);  // err, flags
   t += a256(n * 4) + 256;                                         // bits, counters
   return t;
 }
@@ -549,8 +550,8 @@ RepairWs carve_repair(uint32_t k, size_t n, void* base) {
   r.p0 = p; p += a256(n * w * w);
   r.complete_before = (int32_t*)p; p += a256(n * 2 * w * 4);
   r.complete_now = (int32_t*)p; p += a256(n * 2 * w * 4);
-  r.err_rows = p; p += a256(n * w * 256);
-  r.err_cols = p; p += a256(n * w * 256);
+  r.err_rows = p; p += a256(n * w * rs_err_bytes((int)k));
+  r.err_cols = p; p += a256(n * w * rs_err_bytes((int)k));
   r.flags_rows = (int32_t*)p; p += a256(n * w * 4);
   r.flags_cols = (int32_t*)p; p += a256(n * w * 4);
   r.bits = (int32_t*)p; p += a256(n * 4);
@@ -609,7 +610,7 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
     e.vec_flags = r.complete_before + (long)axis * n * w;
     e.mismatch = r.bits;
     e.mismatch_bit = kRepPreByz;
-    HIP_TRY(ctx, launch_leo8_encode((int)k, e, s));
+    HIP_TRY(ctx, launch_rs_encode((int)k, e, s));
   }
   // solveCrossword: each round rebuilds every decodable row or every decodable
   // column (whichever set is larger) until no axis can make progress.
@@ -618,14 +619,14 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
     DecodeArgs dr = axis_decode_args(k, n, d_eds, d_present, 0, r);
     DecodeArgs dc = axis_decode_args(k, n, d_eds, d_present, 1, r);
     HIP_TRY(ctx, hipMemsetAsync(r.counters, 0, 2 * sizeof(int32_t), s));
-    HIP_TRY(ctx, launch_leo8_errlocs(dr, s));
-    HIP_TRY(ctx, launch_leo8_errlocs(dc, s));
+    HIP_TRY(ctx, launch_rs_errlocs(dr, s));
+    HIP_TRY(ctx, launch_rs_errlocs(dc, s));
     int32_t cnt[2] = {0, 0};
     HIP_TRY(ctx, hipMemcpyAsync(cnt, r.counters, sizeof cnt, hipMemcpyDeviceToHost, s));
     HIP_TRY(ctx, hipStreamSynchronize(s));
     if (cnt[0] == 0 && cnt[1] == 0) break;
     ProfScope p(ctx, 5, s);
-    HIP_TRY(ctx, launch_leo8_decode_only(cnt[0] >= cnt[1] ? dr : dc, s, true));
+    HIP_TRY(ctx, launch_rs_decode_only(cnt[0] >= cnt[1] ? dr : dc, s, true));
   }
   // verify every complete axis against the given roots
   HIP_TRY(ctx, launch_axis_complete(d_present, (int)k, (long)n, r.complete_now, s));

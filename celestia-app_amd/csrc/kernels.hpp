@@ -9,6 +9,10 @@ constexpr int kShareSize = 512;
 constexpr int kNsSize = 29;
 constexpr int kNodeSize = 90;  // minNs(29) | maxNs(29) | sha256(32)
 constexpr int kDigest = 32;
+constexpr int kMaxK = 512;     // appconsts.SquareSizeUpperBound; GF(2^16) above k = 128
+
+// Bytes of error-locator workspace per decoded vector.
+constexpr long rs_err_bytes(int k) { return k <= 128 ? 256 : 4L * k; }
 
 // Per-square status bits written by the kernels (0 = OK).
 constexpr int kStatusPushOrder = 1;
@@ -44,7 +48,7 @@ struct DecodeArgs {
   long sq_stride, vec_stride, shard_stride;
   uint8_t* present;
   long p_sq_stride, p_vec_stride, p_shard_stride;
-  uint8_t* err;        // workspace: nsq*nvec*256 error locators
+  uint8_t* err;        // workspace: nsq*nvec*rs_err_bytes(k) error locators
   int32_t* flags;      // workspace: nsq*nvec (1 = vector decoded this pass)
   int32_t* too_few;    // optional: set to 1 if any vector has < k shards
   int32_t* progress;   // optional: += number of vectors rebuilt (mark pass)
@@ -56,6 +60,17 @@ struct DecodeArgs {
 hipError_t launch_leo8_decode(const DecodeArgs& a, hipStream_t s, bool mark_present);
 hipError_t launch_leo8_errlocs(const DecodeArgs& a, hipStream_t s);
 hipError_t launch_leo8_decode_only(const DecodeArgs& a, hipStream_t s, bool mark_present);
+
+// GF(2^16) (rs_gf16.hip) and the field dispatch the host runtime uses:
+// GF(2^8) for k <= 128, GF(2^16) for 256 <= k <= kMaxK.  DecodeArgs.err then
+// holds rs_err_bytes(k) bytes per vector.
+hipError_t launch_leo16_encode(int k, const EncodeArgs& a, hipStream_t s);
+hipError_t launch_leo16_errlocs(const DecodeArgs& a, hipStream_t s);
+hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mark_present);
+hipError_t launch_rs_encode(int k, const EncodeArgs& a, hipStream_t s);
+hipError_t launch_rs_errlocs(const DecodeArgs& a, hipStream_t s);
+hipError_t launch_rs_decode_only(const DecodeArgs& a, hipStream_t s, bool mark_present);
+hipError_t launch_rs_decode(const DecodeArgs& a, hipStream_t s, bool mark_present);
 
 // Repair helpers (repair.hip).  Status bits per square:
 constexpr int kRepPreByz = 1;      // complete axis whose parity != Encode(data)

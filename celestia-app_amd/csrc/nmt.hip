@@ -368,7 +368,7 @@ __global__ __launch_bounds__(256) void nmt_level_kernel(SquareArgs a, const uint
 constexpr int kDahThreads = 256;
 
 __global__ __launch_bounds__(kDahThreads) void dah_kernel(SquareArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];  // n * 8 dwords
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];  // (n + n/2) * 8 dwords
   const long sq = blockIdx.x;
   const int w = 2 * a.k;
   const int n = 2 * w;
@@ -402,18 +402,19 @@ __global__ __launch_bounds__(kDahThreads) void dah_kernel(SquareArgs a) {
     for (int j = 0; j < 8; j++) lds[i * 8 + j] = bswap32(st[j]);
   }
   __syncthreads();
+  // inner levels ping-pong between lds[0, n) and lds[n, n + n/2) (digest slots)
+  uint32_t* src = lds;
+  uint32_t* dst = lds + n * 8;
   int cur = n;
   while (cur > 1) {
     const int next = cur / 2;
-    uint32_t keep[2][8];
-    int cnt = 0;
-    for (int i = threadIdx.x; i < next; i += kDahThreads, cnt++) {
+    for (int i = threadIdx.x; i < next; i += kDahThreads) {
       uint32_t m[32];
 #pragma unroll
       for (int j = 0; j < 32; j++) m[j] = 0;
       uint32_t lft[8], rgt[8];
 #pragma unroll
-      for (int j = 0; j < 8; j++) { lft[j] = lds[(2 * i) * 8 + j]; rgt[j] = lds[(2 * i + 1) * 8 + j]; }
+      for (int j = 0; j < 8; j++) { lft[j] = src[(2 * i) * 8 + j]; rgt[j] = src[(2 * i + 1) * 8 + j]; }
       m[0] = 0x01u;
       put_bytes<1>(m, lft);
       put_bytes<33>(m, rgt);
@@ -429,20 +430,17 @@ __global__ __launch_bounds__(kDahThreads) void dah_kernel(SquareArgs a) {
         sha256_compress(st, wv);
       }
 #pragma unroll
-      for (int j = 0; j < 8; j++) keep[cnt & 1][j] = bswap32(st[j]);
+      for (int j = 0; j < 8; j++) dst[i * 8 + j] = bswap32(st[j]);
     }
     __syncthreads();
-    cnt = 0;
-    for (int i = threadIdx.x; i < next; i += kDahThreads, cnt++) {
-#pragma unroll
-      for (int j = 0; j < 8; j++) lds[i * 8 + j] = keep[cnt & 1][j];
-    }
-    __syncthreads();
+    uint32_t* t = src;
+    src = dst;
+    dst = t;
     cur = next;
   }
   if (threadIdx.x < 8) {
-    uint32_t* dst = (uint32_t*)(a.dah + sq * 32);
-    dst[threadIdx.x] = lds[threadIdx.x];
+    uint32_t* out = (uint32_t*)(a.dah + sq * 32);
+    out[threadIdx.x] = src[threadIdx.x];
   }
 }
 
@@ -502,8 +500,13 @@ void nmt_workspace_carve(SquareArgs& a, void* ws) {
 
 hipError_t launch_dah(const SquareArgs& a, hipStream_t s) {
   const int n = 4 * a.k;
-  if (n > 2 * kDahThreads * 2) return hipErrorInvalidValue;  // keep[2] per thread
-  const size_t lds = (size_t)n * 8 * sizeof(uint32_t);
+  if (a.k > kMaxK) return hipErrorInvalidValue;
+  const size_t lds = (size_t)(n + n / 2) * 8 * sizeof(uint32_t);  // <= 96 KiB at k = 512
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute((const void*)dah_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(dah_kernel, dim3((unsigned)a.nsq), dim3(kDahThreads), lds, s, a);
   return hipGetLastError();
 }
