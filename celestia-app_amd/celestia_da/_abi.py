@@ -50,7 +50,21 @@ EXPORTS = (
     "dagpu_profile_enable",
     "dagpu_profile_read",
     "dagpu_dah_hash",
+    "dagpu_nmt_roots",
+    "dagpu_wrapper_roots",
+    "dagpu_merkle_roots",
+    "dagpu_subtree_width",
+    "dagpu_blob_commitments",
+    "dagpu_split_workspace_size",
+    "dagpu_split_rows_device",
+    "dagpu_split_cols_device",
+    "dagpu_split_finish_device",
 )
+
+PREFIX_NONE = 0
+PREFIX_SELF = 1
+PREFIX_PARITY = 2
+PREFIX_FLAGS = 3
 
 PROFILE_KERNELS = ("rs_row", "rs_col", "nmt_leaves", "nmt_trees", "dah", "decode")
 
@@ -93,6 +107,18 @@ def lib() -> ctypes.CDLL:
         L.dagpu_repair_workspace_size.restype = sz
         L.dagpu_repair.argtypes = [vp, ctypes.c_uint32, vp, vp, vp, vp]
         L.dagpu_dah_hash.argtypes = [vp, vp, sz, vp]
+        L.dagpu_nmt_roots.argtypes = [vp, sz, vp, vp, sz, ctypes.c_int, vp, ctypes.c_int, vp, vp]
+        L.dagpu_wrapper_roots.argtypes = [vp, ctypes.c_uint64, sz, vp, vp, vp, sz, vp, vp]
+        L.dagpu_merkle_roots.argtypes = [vp, sz, vp, vp, sz, vp]
+        L.dagpu_subtree_width.argtypes = [ctypes.c_uint64, ctypes.c_uint32]
+        L.dagpu_blob_commitments.argtypes = [vp, sz, vp, vp, vp, ctypes.c_uint32, vp]
+        L.dagpu_split_workspace_size.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+        L.dagpu_split_workspace_size.restype = sz
+        L.dagpu_split_rows_device.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, vp, vp,
+                                              vp, vp, vp]
+        L.dagpu_split_cols_device.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, vp, vp,
+                                              vp, vp, vp, vp]
+        L.dagpu_split_finish_device.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp, vp, vp, vp]
         L.dagpu_profile_enable.argtypes = [vp, ctypes.c_int]
         L.dagpu_profile_read.argtypes = [vp, vp, vp, ctypes.c_int]
         _lib = L

@@ -23,102 +23,11 @@
 #include "../../include/dagpu.h"
 #include "host_sha256.hpp"
 #include "kernels.hpp"
+#include "runtime.hpp"
 
 using namespace dagpu;
 
-struct DevBuf {
-  void* p = nullptr;
-  size_t n = 0;
-  hipError_t ensure(size_t bytes) {
-    if (bytes <= n) return hipSuccess;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    n = 0;
-    hipError_t e = hipMalloc(&p, bytes);
-    if (e == hipSuccess) n = bytes;
-    return e;
-  }
-  void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    n = 0;
-  }
-};
-
-struct ProfRec {
-  int id;
-  hipEvent_t a, b;
-};
-
-struct dagpu_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  std::mutex mu;
-  std::string err;
-  DevBuf ods, eds, rr, cr, dah, status, ws;
-  // profiling
-  bool prof = false;
-  std::mutex prof_mu;
-  std::vector<ProfRec> pending;
-  std::vector<hipEvent_t> pool;
-  double prof_ms[DAGPU_PROFILE_KERNELS] = {};
-  uint64_t prof_n[DAGPU_PROFILE_KERNELS] = {};
-};
-
 namespace {
-
-constexpr size_t kSS = kShareSize;
-
-bool is_pow2(uint64_t v) { return v != 0 && (v & (v - 1)) == 0; }
-
-int set_err(dagpu_ctx* c, int code, const std::string& msg) {
-  if (c) c->err = msg;
-  return code;
-}
-
-int hip_fail(dagpu_ctx* c, hipError_t e, const char* what) {
-  char buf[256];
-  snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
-  return set_err(c, DAGPU_ERR_DEVICE, buf);
-}
-
-#define HIP_TRY(ctx, expr)                                   \
-  do {                                                       \
-    hipError_t e_ = (expr);                                  \
-    if (e_ != hipSuccess) return hip_fail((ctx), e_, #expr); \
-  } while (0)
-
-hipEvent_t pool_get(dagpu_ctx* c) {
-  if (!c->pool.empty()) {
-    hipEvent_t e = c->pool.back();
-    c->pool.pop_back();
-    return e;
-  }
-  hipEvent_t e = nullptr;
-  (void)hipEventCreate(&e);
-  return e;
-}
-
-// RAII bracket: records events around one kernel launch when profiling is on.
-struct ProfScope {
-  dagpu_ctx* c;
-  int id;
-  hipStream_t s;
-  hipEvent_t a = nullptr, b = nullptr;
-  ProfScope(dagpu_ctx* c_, int id_, hipStream_t s_) : c(c_), id(id_), s(s_) {
-    if (!c->prof) return;
-    std::lock_guard<std::mutex> g(c->prof_mu);
-    a = pool_get(c);
-    b = pool_get(c);
-    (void)hipEventRecord(a, s);
-  }
-  ~ProfScope() {
-    if (!a) return;
-    (void)hipEventRecord(b, s);
-    std::lock_guard<std::mutex> g(c->prof_mu);
-    c->pending.push_back({id, a, b});
-  }
-};
 
 size_t eds_bytes(uint64_t k) { return 4ull * k * k * kSS; }
 size_t ods_bytes(uint64_t k) { return 1ull * k * k * kSS; }
@@ -210,15 +119,6 @@ int enqueue_roots(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_eds, ui
   return DAGPU_OK;
 }
 
-int check_k(dagpu_ctx* ctx, uint64_t k) {
-  if (!is_pow2(k)) return set_err(ctx, DAGPU_ERR_ARG, "square width must be a power of two");
-  if (k > (uint64_t)kMaxK) {
-    return set_err(ctx, DAGPU_ERR_UNSUPPORTED,
-                   "square width k > " + std::to_string(kMaxK) + " is not supported");
-  }
-  return DAGPU_OK;
-}
-
 // Runs one uniform-k group from host memory.  Caller holds ctx->mu.
 int run_group_host(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* ods, uint8_t* eds_out,
                    uint8_t* rr, uint8_t* cr, uint8_t* dah, int32_t* status) {
@@ -288,6 +188,8 @@ void dagpu_destroy(dagpu_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   c->ods.release(); c->eds.release(); c->rr.release(); c->cr.release();
   c->dah.release(); c->status.release(); c->ws.release();
+  for (DevBuf* b : {&c->t_leaf_data, &c->t_leaves, &c->t_inner, &c->t_meta, &c->t_out, &c->t_status, &c->t_flags})
+    b->release();
   for (auto& r : c->pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
   for (auto e : c->pool) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);

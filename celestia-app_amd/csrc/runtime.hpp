@@ -1,0 +1,119 @@
+// runtime.hpp -- internal host runtime shared by the C-ABI translation units
+// (dagpu.cpp, trees.cpp, split.cpp): the context, device buffers, error
+// helpers and the per-kernel profiling bracket.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/dagpu.h"
+#include "kernels.hpp"
+
+using namespace dagpu;
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= n) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipSuccess) n = bytes;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+struct ProfRec {
+  int id;
+  hipEvent_t a, b;
+};
+
+struct dagpu_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  std::string err;
+  DevBuf ods, eds, rr, cr, dah, status, ws;
+  // generic forests / commitments / split square (trees.cpp, split.cpp)
+  DevBuf t_leaf_data, t_leaves, t_inner, t_meta, t_out, t_status, t_flags;
+  // profiling
+  bool prof = false;
+  std::mutex prof_mu;
+  std::vector<ProfRec> pending;
+  std::vector<hipEvent_t> pool;
+  double prof_ms[DAGPU_PROFILE_KERNELS] = {};
+  uint64_t prof_n[DAGPU_PROFILE_KERNELS] = {};
+};
+
+constexpr size_t kSS = dagpu::kShareSize;
+
+inline bool is_pow2(uint64_t v) { return v != 0 && (v & (v - 1)) == 0; }
+
+inline int set_err(dagpu_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+inline int hip_fail(dagpu_ctx* c, hipError_t e, const char* what) {
+  char buf[256];
+  snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+  return set_err(c, DAGPU_ERR_DEVICE, buf);
+}
+
+#define HIP_TRY(ctx, expr)                                   \
+  do {                                                       \
+    hipError_t e_ = (expr);                                  \
+    if (e_ != hipSuccess) return hip_fail((ctx), e_, #expr); \
+  } while (0)
+
+inline hipEvent_t pool_get(dagpu_ctx* c) {
+  if (!c->pool.empty()) {
+    hipEvent_t e = c->pool.back();
+    c->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+// RAII bracket: records events around one kernel launch when profiling is on.
+struct ProfScope {
+  dagpu_ctx* c;
+  int id;
+  hipStream_t s;
+  hipEvent_t a = nullptr, b = nullptr;
+  ProfScope(dagpu_ctx* c_, int id_, hipStream_t s_) : c(c_), id(id_), s(s_) {
+    if (!c->prof) return;
+    std::lock_guard<std::mutex> g(c->prof_mu);
+    a = pool_get(c);
+    b = pool_get(c);
+    (void)hipEventRecord(a, s);
+  }
+  ~ProfScope() {
+    if (!a) return;
+    (void)hipEventRecord(b, s);
+    std::lock_guard<std::mutex> g(c->prof_mu);
+    c->pending.push_back({id, a, b});
+  }
+};
+
+inline int check_k(dagpu_ctx* ctx, uint64_t k) {
+  if (!is_pow2(k)) return set_err(ctx, DAGPU_ERR_ARG, "square width must be a power of two");
+  if (k > (uint64_t)kMaxK) {
+    return set_err(ctx, DAGPU_ERR_UNSUPPORTED,
+                   "square width k > " + std::to_string(kMaxK) + " is not supported");
+  }
+  return DAGPU_OK;
+}

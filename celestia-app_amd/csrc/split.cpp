@@ -1,0 +1,228 @@
+// split.cpp -- one oversized square split over `parts` GPUs (BASELINE configs[4]
+// stress square).  The square is the same rsmt2d extension +
+// wrapper NMT roots + DAH as the single-GPU path (pkg/da/data_availability_header.go:44-108);
+// only the placement differs.  Rank g owns Q0 rows R_g = [g*k/P, (g+1)*k/P)
+// and, after one all-to-all, EDS columns C_g = [g*2k/P, (g+1)*2k/P):
+//
+//   1 rows    row-encode R_g -> [Q0|Q1] rows, check their namespace order, pack P
+//             send blocks (block h = rows R_g x columns C_h)
+//   2 caller  all-to-all (RCCL over xGMI): block h -> rank h.  Rank h's receive
+//             buffer is then rows 0..k-1 of its column slab, in row order.
+//   3 cols    column-encode the slab (rows k..2k-1 = Q2|Q3 columns of C_h; Q3
+//             by columns of Q1 equals Q3 by rows of Q2), hash every cell once,
+//             full column roots of C_h, and NMT subtree roots of every row over
+//             C_h (2k/P leaves: a power of two, so each is a node of the row tree)
+//   4 caller  all-gather subtree records and column roots, max-reduce status
+//   5 finish  top log2(P) levels of every row tree -> row roots; DAH
+//
+// Q2/Q3 never move back; the only data-path exchange is step 2.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/dagpu.h"
+#include "forest.hpp"
+#include "kernels.hpp"
+#include "runtime.hpp"
+
+namespace {
+
+size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+int check_split(dagpu_ctx* ctx, uint32_t k, uint32_t parts, uint32_t part) {
+  int rc = check_k(ctx, k);
+  if (rc) return rc;
+  if (!is_pow2(parts) || parts > k) return set_err(ctx, DAGPU_ERR_ARG, "parts must be a power of two <= k");
+  if (part >= parts) return set_err(ctx, DAGPU_ERR_ARG, "part out of range");
+  return DAGPU_OK;
+}
+
+// workspace pieces (bytes) for one rank
+struct SplitWs {
+  uint8_t* rows_tmp;    // (k/P) x 2k shares
+  uint8_t* leaves;      // 2k x W NMT leaf records
+  uint8_t* col_inner;   // column forest inner levels
+  uint8_t* row_inner;   // row subtree inner levels
+  uint8_t* top_inner;   // finishing forest inner levels
+  int64_t* meta;        // forest metadata (three plans)
+};
+
+struct SplitPlans {
+  dagpu::ForestPlan cols, rows, top;
+};
+
+SplitPlans make_plans(uint32_t k, uint32_t parts) {
+  const long w = 2L * k, W = w / parts;
+  SplitPlans p;
+  p.cols = dagpu::ForestPlan::uniform_plan(W, w, 1, W);   // tree c: leaf r at r*W + c
+  p.rows = dagpu::ForestPlan::uniform_plan(w, W, W, 1);   // tree r: leaf c at r*W + c
+  p.top = dagpu::ForestPlan::uniform_plan(w, parts, 1, w);  // tree r: leaf g at g*w + r
+  return p;
+}
+
+size_t split_ws_bytes(uint32_t k, uint32_t parts, SplitWs* out, void* base) {
+  const size_t w = 2 * (size_t)k, W = w / parts, rows = k / parts;
+  SplitPlans p = make_plans(k, parts);
+  size_t off = 0;
+  auto take = [&](size_t bytes) { size_t o = off; off += al256(bytes > 0 ? bytes : 1); return o; };
+  const size_t o_tmp = take(rows * w * kSS);
+  const size_t o_leaves = take(w * W * dagpu::kRecNmt);
+  const size_t o_ci = take((size_t)p.cols.inner_records * dagpu::kRecNmt);
+  const size_t o_ri = take((size_t)p.rows.inner_records * dagpu::kRecNmt);
+  const size_t o_ti = take((size_t)p.top.inner_records * dagpu::kRecNmt);
+  const size_t o_meta = take((p.cols.meta.size() + p.rows.meta.size() + p.top.meta.size()) * sizeof(int64_t));
+  if (out) {
+    uint8_t* b = (uint8_t*)base;
+    out->rows_tmp = b + o_tmp;
+    out->leaves = b + o_leaves;
+    out->col_inner = b + o_ci;
+    out->row_inner = b + o_ri;
+    out->top_inner = b + o_ti;
+    out->meta = (int64_t*)(b + o_meta);
+  }
+  return off;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t dagpu_split_workspace_size(uint32_t k, uint32_t parts) {
+  if (k == 0 || parts == 0 || !is_pow2(k) || !is_pow2(parts) || parts > k) return 0;
+  return split_ws_bytes(k, parts, nullptr, nullptr) + 256;
+}
+
+int dagpu_split_rows_device(dagpu_ctx* ctx, uint32_t k, uint32_t parts, uint32_t part,
+                            const uint8_t* d_ods_rows, uint8_t* d_send, int32_t* d_status,
+                            void* d_workspace, void* stream) {
+  if (!ctx || !d_ods_rows || !d_send || !d_status || !d_workspace) return DAGPU_ERR_ARG;
+  int rc = check_split(ctx, k, parts, part);
+  if (rc) return rc;
+  (void)part;  // every rank runs the same code on its own rows
+  hipStream_t s = (hipStream_t)stream;
+  const long w = 2L * k, W = w / parts, rows = k / parts;
+  SplitWs ws;
+  split_ws_bytes(k, parts, &ws, d_workspace);
+  HIP_TRY(ctx, hipMemsetAsync(d_status, 0, sizeof(int32_t), s));
+  // nmt push order over whole Q0 rows (a row's Q0 part spans several slabs)
+  HIP_TRY(ctx, dagpu::launch_ns_order_check(d_ods_rows, rows, k, (long)k * kSS, kSS, d_status,
+                                            dagpu::kStatusPushOrder, s));
+  EncodeArgs ea{};
+  ea.in = d_ods_rows;
+  ea.in_vec_stride = (long)k * kSS;
+  ea.in_shard_stride = kSS;
+  ea.copy = ws.rows_tmp;
+  ea.copy_vec_stride = w * kSS;
+  ea.copy_shard_stride = kSS;
+  ea.out = ws.rows_tmp + (long)k * kSS;
+  ea.out_vec_stride = w * kSS;
+  ea.out_shard_stride = kSS;
+  ea.nsq = 1;
+  ea.nvec = rows;
+  ea.nchunk = 1;
+  ea.shard_bytes = kSS;
+  {
+    ProfScope p(ctx, 0, s);
+    HIP_TRY(ctx, launch_rs_encode((int)k, ea, s));
+  }
+  // send block h = rows x columns [h*W, (h+1)*W), row-major
+  for (uint32_t h = 0; h < parts; h++) {
+    HIP_TRY(ctx, hipMemcpy2DAsync(d_send + (size_t)h * rows * W * kSS, (size_t)W * kSS,
+                                  ws.rows_tmp + (size_t)h * W * kSS, (size_t)w * kSS, (size_t)W * kSS,
+                                  (size_t)rows, hipMemcpyDeviceToDevice, s));
+  }
+  return DAGPU_OK;
+}
+
+int dagpu_split_cols_device(dagpu_ctx* ctx, uint32_t k, uint32_t parts, uint32_t part, uint8_t* d_slab,
+                            uint8_t* d_col_roots, uint8_t* d_row_sub, int32_t* d_status,
+                            void* d_workspace, void* stream) {
+  if (!ctx || !d_slab || !d_col_roots || !d_row_sub || !d_status || !d_workspace) return DAGPU_ERR_ARG;
+  int rc = check_split(ctx, k, parts, part);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const long w = 2L * k, W = w / parts;
+  SplitWs ws;
+  split_ws_bytes(k, parts, &ws, d_workspace);
+  SplitPlans pl = make_plans(k, parts);
+  // column encode: vector c = column c of the slab (k data shards) -> rows k..2k-1
+  EncodeArgs ea{};
+  ea.in = d_slab;
+  ea.in_vec_stride = kSS;
+  ea.in_shard_stride = W * kSS;
+  ea.out = d_slab + (long)k * W * kSS;
+  ea.out_vec_stride = kSS;
+  ea.out_shard_stride = W * kSS;
+  ea.copy = nullptr;
+  ea.nsq = 1;
+  ea.nvec = W;
+  ea.nchunk = 1;
+  ea.shard_bytes = kSS;
+  {
+    ProfScope p(ctx, 1, s);
+    HIP_TRY(ctx, launch_rs_encode((int)k, ea, s));
+  }
+  // every cell of the slab hashed once (wrapper namespace rule by global coordinates)
+  dagpu::ForestLeafArgs la{};
+  la.data = d_slab;
+  la.data_stride = kSS;
+  la.dlen = kSS;
+  la.nleaves = w * W;
+  la.pmode = dagpu::kPfxGrid;
+  la.grid_k = (int)k;
+  la.grid_w = W;
+  la.grid_r0 = 0;
+  la.grid_c0 = (long)part * W;
+  la.rfc = 0;
+  la.out = ws.leaves;
+  {
+    ProfScope p(ctx, 2, s);
+    HIP_TRY(ctx, dagpu::launch_forest_leaves(la, s));
+  }
+  {
+    ProfScope p(ctx, 3, s);
+    // full column trees (push order of Q0 columns checked at level 1)
+    HIP_TRY(ctx, dagpu::forest_enqueue(pl.cols, ws.leaves, ws.col_inner, ws.meta, 1, 1, 0, d_status, d_col_roots,
+                                       0, 0, s));
+    // row subtrees over this slab (row order was checked on the row owners)
+    HIP_TRY(ctx, dagpu::forest_enqueue(pl.rows, ws.leaves, ws.row_inner, ws.meta + pl.cols.meta.size(), 1, 0, 0,
+                                       nullptr, d_row_sub, 1, 0, s));
+  }
+  HIP_TRY(ctx, hipStreamSynchronize(s));  // plans' metadata uploads complete
+  return DAGPU_OK;
+}
+
+int dagpu_split_finish_device(dagpu_ctx* ctx, uint32_t k, uint32_t parts, const uint8_t* d_row_sub_all,
+                              const uint8_t* d_col_roots_all, uint8_t* d_row_roots, uint8_t* d_dah,
+                              void* d_workspace, void* stream) {
+  if (!ctx || !d_row_sub_all || !d_col_roots_all || !d_row_roots || !d_dah || !d_workspace)
+    return DAGPU_ERR_ARG;
+  int rc = check_split(ctx, k, parts, 0);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  SplitWs ws;
+  split_ws_bytes(k, parts, &ws, d_workspace);
+  SplitPlans pl = make_plans(k, parts);
+  {
+    ProfScope p(ctx, 3, s);
+    HIP_TRY(ctx, dagpu::forest_enqueue(pl.top, d_row_sub_all, ws.top_inner,
+                                       ws.meta + pl.cols.meta.size() + pl.rows.meta.size(), 1, 0, 0, nullptr,
+                                       d_row_roots, 0, 0, s));
+  }
+  SquareArgs sa{};
+  sa.row_roots = d_row_roots;
+  sa.col_roots = (uint8_t*)d_col_roots_all;
+  sa.dah = d_dah;
+  sa.k = (int)k;
+  sa.nsq = 1;
+  {
+    ProfScope p(ctx, 4, s);
+    HIP_TRY(ctx, launch_dah(sa, s));
+  }
+  HIP_TRY(ctx, hipStreamSynchronize(s));
+  return DAGPU_OK;
+}
+
+}  // extern "C"

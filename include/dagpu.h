@@ -151,6 +151,90 @@ int dagpu_profile_read(dagpu_ctx* ctx, double* total_ms, uint64_t* launches, int
 int dagpu_dah_hash(const uint8_t* row_roots, const uint8_t* col_roots, size_t w,
                    uint8_t* out32);
 
+/* ---- Generic trees (batched; host buffers in, host buffers out) ---------- */
+
+/* Leaf prefix modes of dagpu_nmt_roots (what is hashed for a push of `d`):
+ *   NONE   0x00 | d            d is nmt namespaced data (ns = d[0:29])
+ *   SELF   0x00 | d[0:29] | d  (wrapper Q0 cell; blob commitment leaf)
+ *   PARITY 0x00 | 0xFF*29 | d  (wrapper cell outside Q0)
+ *   FLAGS  per-push SELF / PARITY byte in prefix_flags */
+#define DAGPU_PREFIX_NONE 0
+#define DAGPU_PREFIX_SELF 1
+#define DAGPU_PREFIX_PARITY 2
+#define DAGPU_PREFIX_FLAGS 3
+
+/* Roots of many namespaced Merkle trees: nmt.New(sha256.New(),
+ * NamespaceIDSize(29), IgnoreMaxNamespace(ignore_max_ns)) followed by Push of
+ * every leaf and Root() (nmt v0.20.0; hasher mirror
+ * test/util/malicious/hasher.go:161-309).  Tree t has leaf_counts[t] pushes,
+ * packed tree after tree in `leaves`, leaf_len bytes each.  roots: ntrees * 90
+ * B (an empty tree gives 0^29 | 0^29 | SHA256("")).  status[t] (optional):
+ * DAGPU_ERR_PUSH_ORDER when a pushed namespace is below its predecessor's
+ * (ErrInvalidPushOrder); the call then returns that status. */
+int dagpu_nmt_roots(dagpu_ctx* ctx, size_t ntrees, const uint32_t* leaf_counts,
+                    const uint8_t* leaves, size_t leaf_len, int prefix_mode,
+                    const uint8_t* prefix_flags, int ignore_max_ns, uint8_t* roots,
+                    int32_t* status);
+
+/* rsmt2d.Tree drop-in for wrapper.NewConstructor(squareSize)
+ * (pkg/wrapper/nmt_wrapper.go:73-124): tree t is the
+ * ErasuredNamespacedMerkleTree of axis index axis_index[t] after
+ * leaf_counts[t] Push calls of share_len-byte shares (packed in `shares`);
+ * returns every Root().  Same errors: square_size 0, pushes past 2*squareSize,
+ * shares shorter than 29 B, namespace push order. */
+int dagpu_wrapper_roots(dagpu_ctx* ctx, uint64_t square_size, size_t ntrees,
+                        const uint32_t* axis_index, const uint32_t* leaf_counts,
+                        const uint8_t* shares, size_t share_len, uint8_t* roots,
+                        int32_t* status);
+
+/* merkle.HashFromByteSlices (celestia-core v0.34 crypto/merkle, RFC-6962) for
+ * many lists: list t has counts[t] items of item_len bytes (packed); out32 gets
+ * ntrees 32-B roots (an empty list gives SHA256("")). */
+int dagpu_merkle_roots(dagpu_ctx* ctx, size_t ntrees, const uint32_t* counts,
+                       const uint8_t* items, size_t item_len, uint8_t* out32);
+
+/* inclusion.SubTreeWidth (pkg/inclusion/blob_share_commitment_rules.go:85-101). */
+int dagpu_subtree_width(uint64_t share_count, uint32_t subtree_root_threshold);
+
+/* inclusion.CreateCommitment (pkg/inclusion/commitment.go:19-75) for blobs
+ * already split into shares (shares.SplitBlobs): blob b has namespace
+ * namespaces[b*29..] and share_counts[b] 512-B shares (packed in `shares`).
+ * Subtree widths from subtree_root_threshold (appconsts
+ * DefaultSubtreeRootThreshold = 64); commitments: nblobs * 32 B. */
+int dagpu_blob_commitments(dagpu_ctx* ctx, size_t nblobs, const uint8_t* namespaces,
+                           const uint32_t* share_counts, const uint8_t* shares,
+                           uint32_t subtree_root_threshold, uint8_t* commitments);
+
+/* ---- One oversized square split over P GPUs (configs[4] stress) ---------
+ * Same result as dagpu_extend_batch_device on the whole square; rank g of P
+ * (P a power of two <= k) owns Q0 rows [g*k/P, (g+1)*k/P) and EDS columns
+ * [g*2k/P, (g+1)*2k/P).  The caller runs the collectives (RCCL over xGMI)
+ * between the steps; all pointers are device memory on `stream`:
+ *   1 dagpu_split_rows_device   d_ods_rows (k/P rows of k shares) -> d_send:
+ *                               P blocks of (k/P) x (2k/P) shares, block h for
+ *                               rank h; zeroes then sets *d_status (push order)
+ *   2 all-to-all of d_send      rank h receives the P blocks in rank order =
+ *                               rows 0..k-1 of its slab (2k rows x 2k/P shares)
+ *   3 dagpu_split_cols_device   fills slab rows k..2k-1, writes the slab's
+ *                               2k/P column roots (90 B) and 2k row-subtree
+ *                               records (96 B: minNs[32] maxNs[32] digest[32])
+ *   4 all-gather row-subtree records (P x 2k x 96 B, rank order) and column
+ *     roots (2k x 90 B, column order); max-reduce the status words
+ *   5 dagpu_split_finish_device row roots (2k x 90 B) and the DAH (32 B)
+ * Steps 3 and 5 synchronise `stream` before returning.
+ * d_workspace: dagpu_split_workspace_size(k, P) bytes (0 = invalid k / P). */
+size_t dagpu_split_workspace_size(uint32_t k, uint32_t parts);
+int dagpu_split_rows_device(dagpu_ctx* ctx, uint32_t k, uint32_t parts, uint32_t part,
+                            const uint8_t* d_ods_rows, uint8_t* d_send, int32_t* d_status,
+                            void* d_workspace, void* stream);
+int dagpu_split_cols_device(dagpu_ctx* ctx, uint32_t k, uint32_t parts, uint32_t part,
+                            uint8_t* d_slab, uint8_t* d_col_roots, uint8_t* d_row_sub,
+                            int32_t* d_status, void* d_workspace, void* stream);
+int dagpu_split_finish_device(dagpu_ctx* ctx, uint32_t k, uint32_t parts,
+                              const uint8_t* d_row_sub_all, const uint8_t* d_col_roots_all,
+                              uint8_t* d_row_roots, uint8_t* d_dah, void* d_workspace,
+                              void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -194,3 +194,97 @@ def extend_and_dah(ods: List[bytes], k: int):
     rr = [axis_root(eds, k, 0, i) for i in range(w)]
     cr = [axis_root(eds, k, 1, i) for i in range(w)]
     return eds, rr, cr, rfc6962(rr + cr)
+
+
+# ---- generic nmt / commitments (test oracle for dagpu_nmt_roots & co) -------------
+
+def nmt_leaf_generic(namespaced_data: bytes) -> bytes:
+    """nmt HashLeaf (test/util/malicious/hasher.go:186-209): ns | ns | H(0x00 | d)."""
+    ns = namespaced_data[:29]
+    return ns + ns + hashlib.sha256(b"\x00" + namespaced_data).digest()
+
+
+def nmt_node_generic(l: bytes, r: bytes, ignore_max: bool) -> bytes:
+    """nmt HashNode + computeNsRange (hasher.go:271-309)."""
+    mx = l[29:58] if (ignore_max and r[:29] == PARITY_NS) else r[29:58]
+    return l[:29] + mx + hashlib.sha256(b"\x01" + l + r).digest()
+
+
+def nmt_root_generic(pushes: List[bytes], ignore_max: bool = True) -> bytes:
+    """nmt computeRoot: RFC-6962 split at the largest power of two < n; empty
+    tree = 0^29 | 0^29 | SHA256("") (hasher.go:161-168).  Raises ValueError on
+    a push-order violation (nmt Push, ErrInvalidPushOrder)."""
+    for a, b in zip(pushes, pushes[1:]):
+        if b[:29] < a[:29]:
+            raise ValueError("invalid push order")
+
+    def rec(nodes):
+        if len(nodes) == 0:
+            return b"\x00" * 58 + hashlib.sha256(b"").digest()
+        if len(nodes) == 1:
+            return nodes[0]
+        split = 1
+        while split * 2 < len(nodes):
+            split *= 2
+        return nmt_node_generic(rec(nodes[:split]), rec(nodes[split:]), ignore_max)
+
+    return rec([nmt_leaf_generic(p) for p in pushes])
+
+
+def _round_up_pow2(v: int) -> int:
+    r = 1
+    while r < v:
+        r <<= 1
+    return r
+
+
+def subtree_width(share_count: int, threshold: int = 64) -> int:
+    """inclusion.SubTreeWidth (pkg/inclusion/blob_share_commitment_rules.go:85-101)
+    with BlobMinSquareSize (:76-78)."""
+    s = share_count // threshold + (1 if share_count % threshold else 0)
+    s = _round_up_pow2(s)
+    import math
+    return min(s, _round_up_pow2(int(math.ceil(math.sqrt(share_count)))))
+
+
+def mmr_sizes(total: int, max_tree: int) -> List[int]:
+    """inclusion.MerkleMountainRangeSizes (pkg/inclusion/commitment.go:85-107)."""
+    out = []
+    while total:
+        if total >= max_tree:
+            t = max_tree
+        else:
+            up = _round_up_pow2(total)
+            t = up if up == total else up // 2
+        out.append(t)
+        total -= t
+    return out
+
+
+def sparse_shares(ns: bytes, data: bytes, version: int = 0) -> List[bytes]:
+    """SparseShareSplitter.Write for one blob (pkg/shares/split_sparse_shares.go:21-63,
+    share_builder.go:56-80,155-221, info_byte.go:15-25)."""
+    shares = []
+    first = True
+    while True:
+        raw = bytearray(ns) + bytes([(version << 1) | (1 if first else 0)])
+        if first:
+            raw += len(data).to_bytes(4, "big")
+        room = 512 - len(raw)
+        raw += data[:room]
+        data = data[room:]
+        shares.append(bytes(raw) + b"\x00" * (512 - len(raw)))
+        first = False
+        if not data:
+            return shares
+
+
+def create_commitment(ns: bytes, data: bytes, threshold: int = 64, version: int = 0) -> bytes:
+    """inclusion.CreateCommitment (pkg/inclusion/commitment.go:19-75)."""
+    shares = sparse_shares(ns, data, version)
+    sizes = mmr_sizes(len(shares), subtree_width(len(shares), threshold))
+    roots, cur = [], 0
+    for sz in sizes:
+        roots.append(nmt_root_generic([ns + s for s in shares[cur:cur + sz]], True))
+        cur += sz
+    return rfc6962(roots)
