@@ -1,0 +1,161 @@
+"""One oversized square split over P GPUs (BASELINE configs[4] stress square;
+SURVEY.md §8e), one process per GPU.
+
+The result is the square's ordinary EDS row/column roots and DAH
+(da.ExtendShares + NewDataAvailabilityHeader, pkg/da/data_availability_header.go:44-108);
+the split only changes placement.  Rank g owns Q0 rows [g*k/P, (g+1)*k/P) and,
+after ONE all-to-all (RCCL over xGMI), EDS columns [g*2k/P, (g+1)*2k/P).  The
+five steps are documented in include/dagpu.h; the kernels are split.cpp /
+nmt_forest.hip / rs_gf16.hip.  The collectives are torch.distributed calls on
+device tensors (backend "nccl" = RCCL); a gloo group stages through host memory.
+
+`extend_split_local` runs all P parts in one process on one GPU, with the
+all-to-all done as device copies: the single-GPU check of every kernel and of
+the block layout the collective sees.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _abi
+from .da import Context, DAError, ErrInvalidPushOrder
+from ._abi import ROOT_SIZE, SHARE_SIZE
+
+REC = 96  # row-subtree record: minNs[32] | maxNs[32] | digest[32]
+
+
+def _stream(s: Optional[torch.cuda.Stream]) -> int:
+    return (s or torch.cuda.current_stream()).cuda_stream
+
+
+class SplitPart:
+    """Device buffers and steps of one rank (part) of a split square."""
+
+    def __init__(self, k: int, parts: int, part: int, ctx: Context, device: torch.device):
+        if parts < 1 or parts & (parts - 1) or parts > k:
+            raise DAError(_abi.ERR_ARG, "parts must be a power of two <= k")
+        self.k, self.parts, self.part, self.ctx = k, parts, part, ctx
+        self.w = 2 * k
+        self.W = self.w // parts
+        self.rows = k // parts
+        L = ctx._L
+        ws = L.dagpu_split_workspace_size(k, parts)
+        if ws == 0:
+            raise DAError(_abi.ERR_ARG, f"invalid split k={k} parts={parts}")
+        u8 = dict(dtype=torch.uint8, device=device)
+        self.ws = torch.empty(ws, **u8)
+        self.send = torch.empty(self.rows * self.w * SHARE_SIZE, **u8)
+        self.slab = torch.empty(self.w * self.W * SHARE_SIZE, **u8)
+        self.col_roots = torch.empty(self.W * ROOT_SIZE, **u8)
+        self.row_sub = torch.empty(self.w * REC, **u8)
+        self.status = torch.zeros(1, dtype=torch.int32, device=device)
+
+    @property
+    def slab_top(self) -> torch.Tensor:
+        """Rows 0..k-1 of the column slab: the all-to-all receive buffer."""
+        return self.slab[: self.k * self.W * SHARE_SIZE]
+
+    def step_rows(self, ods_rows: torch.Tensor, stream=None) -> None:
+        assert ods_rows.numel() == self.rows * self.k * SHARE_SIZE and ods_rows.is_contiguous()
+        self.ctx.check(self.ctx._L.dagpu_split_rows_device(
+            self.ctx.handle, self.k, self.parts, self.part, ods_rows.data_ptr(), self.send.data_ptr(),
+            self.status.data_ptr(), self.ws.data_ptr(), _stream(stream)))
+
+    def step_cols(self, stream=None) -> None:
+        self.ctx.check(self.ctx._L.dagpu_split_cols_device(
+            self.ctx.handle, self.k, self.parts, self.part, self.slab.data_ptr(), self.col_roots.data_ptr(),
+            self.row_sub.data_ptr(), self.status.data_ptr(), self.ws.data_ptr(), _stream(stream)))
+
+    def step_finish(self, row_sub_all: torch.Tensor, col_roots_all: torch.Tensor,
+                    stream=None) -> Tuple[torch.Tensor, torch.Tensor]:
+        assert row_sub_all.numel() == self.parts * self.w * REC
+        assert col_roots_all.numel() == self.w * ROOT_SIZE
+        row_roots = torch.empty(self.w * ROOT_SIZE, dtype=torch.uint8, device=self.slab.device)
+        dah = torch.empty(32, dtype=torch.uint8, device=self.slab.device)
+        self.ctx.check(self.ctx._L.dagpu_split_finish_device(
+            self.ctx.handle, self.k, self.parts, row_sub_all.data_ptr(), col_roots_all.data_ptr(),
+            row_roots.data_ptr(), dah.data_ptr(), self.ws.data_ptr(), _stream(stream)))
+        return row_roots, dah
+
+
+def _check_status(status: int) -> None:
+    if status & 1:
+        raise ErrInvalidPushOrder(_abi.ERR_PUSH_ORDER,
+                                  "invalid push order: namespaces of original data square are not sorted")
+
+
+def extend_split_local(ods: torch.Tensor, k: int, parts: int, ctx: Context,
+                       stream=None) -> Tuple[bytes, bytes, bytes]:
+    """All P parts in this process on one GPU (all-to-all as device copies).
+    ods: k*k*512 B device tensor.  Returns (row_roots, col_roots, dah) bytes."""
+    dev = ods.device
+    ps = [SplitPart(k, parts, g, ctx, dev) for g in range(parts)]
+    rows_b = ps[0].rows * k * SHARE_SIZE
+    for g, p in enumerate(ps):
+        p.step_rows(ods[g * rows_b:(g + 1) * rows_b], stream)
+    blk = ps[0].rows * ps[0].W * SHARE_SIZE
+    for h, ph in enumerate(ps):  # rank h receives block h of every rank g, in rank order
+        for g, pg in enumerate(ps):
+            ph.slab_top[g * blk:(g + 1) * blk].copy_(pg.send[h * blk:(h + 1) * blk])
+    for p in ps:
+        p.step_cols(stream)
+    row_sub_all = torch.cat([p.row_sub for p in ps])
+    col_all = torch.cat([p.col_roots for p in ps])
+    status = max(int(p.status.item()) for p in ps)
+    rr, dah = ps[0].step_finish(row_sub_all, col_all, stream)
+    torch.cuda.synchronize(dev)
+    _check_status(status)
+    return rr.cpu().numpy().tobytes(), col_all.cpu().numpy().tobytes(), dah.cpu().numpy().tobytes()
+
+
+# ---- the collectives (torch.distributed; nccl = RCCL over xGMI) -------------
+
+def all_to_all_blocks(dist, out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
+    """Equal-split all-to-all: block h of `inp` goes to rank h; `out` receives
+    the blocks of ranks 0..P-1 in rank order.  gloo stages through host memory."""
+    if dist.get_backend(group) == "nccl" or out.device.type == "cpu":
+        dist.all_to_all_single(out, inp, group=group)
+        return
+    o, i = out.cpu(), inp.cpu()
+    dist.all_to_all_single(o, i, group=group)
+    out.copy_(o)
+
+
+def all_gather_flat(dist, out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
+    """Rank-ordered concatenation of every rank's `inp` into `out`."""
+    if dist.get_backend(group) == "nccl" or out.device.type == "cpu":
+        dist.all_gather_into_tensor(out, inp, group=group)
+        return
+    parts = [torch.empty_like(inp, device="cpu") for _ in range(dist.get_world_size(group))]
+    dist.all_gather(parts, inp.cpu(), group=group)
+    out.copy_(torch.cat(parts))
+
+
+def max_status(dist, status: torch.Tensor, group=None) -> int:
+    if dist.get_backend(group) == "nccl" or status.device.type == "cpu":
+        t = status.clone()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        return int(t.item())
+    t = status.cpu()
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return int(t.item())
+
+
+def extend_split_distributed(dist, part: SplitPart, ods_rows: torch.Tensor, group=None,
+                             stream=None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """One rank's share of the split: `ods_rows` are this rank's k/P Q0 rows
+    (device).  Returns device tensors (row_roots 2k*90, col_roots 2k*90, dah 32),
+    identical on every rank.  Raises ErrInvalidPushOrder like NewDAH."""
+    part.step_rows(ods_rows, stream)
+    all_to_all_blocks(dist, part.slab_top, part.send, group)
+    part.step_cols(stream)
+    row_sub_all = torch.empty(part.parts * part.row_sub.numel(), dtype=torch.uint8, device=part.slab.device)
+    col_all = torch.empty(part.parts * part.col_roots.numel(), dtype=torch.uint8, device=part.slab.device)
+    all_gather_flat(dist, row_sub_all, part.row_sub, group)
+    all_gather_flat(dist, col_all, part.col_roots, group)
+    status = max_status(dist, part.status, group)
+    rr, dah = part.step_finish(row_sub_all, col_all, stream)
+    _check_status(status)
+    return rr, col_all, dah
