@@ -53,7 +53,9 @@ def dist_init():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        import datetime
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                timeout=datetime.timedelta(seconds=300))
         return dist, rank, world, local
     return None, 0, 1, 0
 
@@ -119,9 +121,16 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--mode", choices=["extend", "mixed", "repair"], default="extend",
-                    help="extend: configs[1] (headline); mixed: configs[2]; repair: configs[3]")
+    ap.add_argument("--mode", choices=["extend", "mixed", "repair", "split"], default="extend",
+                    help="extend: configs[1] (headline); mixed: configs[2]; repair: configs[3]; "
+                         "split: configs[4] oversized square over all ranks")
+    ap.add_argument("--split-k", type=int, nargs="*", default=[256, 512],
+                    help="split stress square widths (k); also run after the headline when N > 1")
+    ap.add_argument("--split-steps", type=int, default=3)
+    ap.add_argument("--no-split", action="store_true", help="skip the split stress at N > 1")
     args = ap.parse_args()
+    if args.mode == "split":
+        return bench_split_main(args)
     if args.mode == "mixed":
         return bench_mixed(args)
     if args.mode == "repair":
@@ -230,8 +239,73 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(k, args.cpu_seconds, args.cpu_threads)
         out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+    if world > 1 and not args.no_split:
+        # configs[4] stress: one oversized square split over all ranks (RCCL all-to-all)
+        del ds
+        torch.cuda.empty_cache()
+        out["split_stress"] = {str(sk): bench_split(dist, rank, world, local, ctx, sk, args.split_steps, 1)
+                               for sk in args.split_k}
     if rank == 0:
         print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def bench_split(dist, rank, world, local, ctx, k, steps, warmup):
+    """configs[4] stress: ONE k x k square split over all `world` ranks (rows ->
+    one all-to-all -> column slabs; celestia_da.split).  Returns squares/s, the
+    per-square time (max over ranks) and whether the DAH equals the single-GPU
+    path's DAH for the same square."""
+    from celestia_da import split, synth
+    from celestia_da.device import DeviceSquares
+
+    dev = torch.device("cuda", local)
+    ods = synth.random_blob_square(k, 512_000 + k).reshape(-1)
+    rows = k // world
+    mine = torch.from_numpy(ods[rank * rows * k * SHARE:(rank + 1) * rows * k * SHARE].copy()).to(dev)
+    part = split.SplitPart(k, world, rank, ctx, dev)
+    for _ in range(warmup):
+        _, _, dah = split.extend_split_distributed(dist, part, mine)
+    torch.cuda.synchronize()
+    barrier(dist)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        _, _, dah = split.extend_split_distributed(dist, part, mine)
+    torch.cuda.synchronize()
+    barrier(dist)
+    el = max_over_ranks(dist, time.perf_counter() - t0, local)
+    ok = None
+    if rank == 0:  # same square through the ordinary single-GPU pipeline
+        ds = DeviceSquares(k, 1, device=local, ctx=ctx)
+        ds.ods[0].copy_(torch.from_numpy(ods))
+        ds.extend()
+        torch.cuda.synchronize()
+        ok = bool(torch.equal(ds.dah[0].cpu(), dah.cpu()))
+        del ds
+    del part
+    torch.cuda.empty_cache()
+    return {"k": k, "parts": world, "squares_per_s": steps / el, "ms_per_square": el / steps * 1e3,
+            "rs_gbs": rs_bytes(k) * steps / el / 1e9, "dah_matches_single_gpu": ok,
+            "collective": f"all_to_all_single over {world} ranks, {dist.get_backend() if dist else 'none'}"}
+
+
+def bench_split_main(args):
+    dist, rank, world, local = dist_init()
+    torch.cuda.set_device(local)
+    from celestia_da import da
+
+    ctx = da.Context(local)
+    res = {str(k): bench_split(dist, rank, world, local, ctx, k, args.steps, args.warmup) for k in args.split_k}
+    if rank == 0:
+        first = res[str(args.split_k[-1])]
+        print(json.dumps({"metric": "oversized square EDS+DAH squares/sec (configs[4] stress, split over all GPUs)",
+                          "value": first["squares_per_s"], "unit": "squares/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "ms_per_step": first["ms_per_square"],
+                          "higher_is_better": True, "scaling": "strong", "dtype": "u8",
+                          "data": "synthetic random-namespace blob shares", "config": {
+                              "workload": "configs[4] stress square split with all-to-all", "k": args.split_k,
+                              "parallelism": f"rows/columns over {world} GPU(s)"}, "split": res}), flush=True)
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -114,7 +114,11 @@ def extend_split_local(ods: torch.Tensor, k: int, parts: int, ctx: Context,
 
 def all_to_all_blocks(dist, out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
     """Equal-split all-to-all: block h of `inp` goes to rank h; `out` receives
-    the blocks of ranks 0..P-1 in rank order.  gloo stages through host memory."""
+    the blocks of ranks 0..P-1 in rank order.  gloo stages through host memory;
+    dist=None is the single-rank case."""
+    if dist is None:
+        out.copy_(inp)
+        return
     if dist.get_backend(group) == "nccl" or out.device.type == "cpu":
         dist.all_to_all_single(out, inp, group=group)
         return
@@ -125,6 +129,9 @@ def all_to_all_blocks(dist, out: torch.Tensor, inp: torch.Tensor, group=None) ->
 
 def all_gather_flat(dist, out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
     """Rank-ordered concatenation of every rank's `inp` into `out`."""
+    if dist is None:
+        out.copy_(inp)
+        return
     if dist.get_backend(group) == "nccl" or out.device.type == "cpu":
         dist.all_gather_into_tensor(out, inp, group=group)
         return
@@ -134,6 +141,8 @@ def all_gather_flat(dist, out: torch.Tensor, inp: torch.Tensor, group=None) -> N
 
 
 def max_status(dist, status: torch.Tensor, group=None) -> int:
+    if dist is None:
+        return int(status.item())
     if dist.get_backend(group) == "nccl" or status.device.type == "cpu":
         t = status.clone()
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
