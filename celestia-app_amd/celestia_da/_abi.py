@@ -83,6 +83,14 @@ def lib() -> ctypes.CDLL:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(
                 f"HIP extension not built: {LIB_PATH} missing (run __graft_entry__.build())")
+        # Load PyTorch's bundled HIP runtime first when torch is installed:
+        # libdagpu.so and torch then share ONE libamdhip64.so.7 (same soname).
+        # Loading /opt/rocm's copy first would make torch bind to it and fail
+        # its own device init ("No HIP GPUs are available").
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         L.dagpu_version.restype = ctypes.c_int
         L.dagpu_init.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]

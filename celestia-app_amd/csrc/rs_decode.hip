@@ -296,6 +296,175 @@ __attribute__((amdgpu_waves_per_eu(DecOcc<K>::waves, 8))) void leo8_decode_kerne
   }
 }
 
+// ---------------------------------------------------------------------------
+// k = 128 (n = 256) decode over FOUR wave-parts per dword column (64 elements
+// per thread, no spills).  Element index bits: 0-5 are local in the "block"
+// layout (part q holds i = 64q + j), bits 4-5 become the part index in the
+// "transposed" layout (part q holds i = 64a + 16q + b, slot 16a + b), where
+// bits 0-3 and 6-7 are local.  Both layout changes are the same 4x4 block
+// transpose through LDS.  Schedule:
+//   block:      premultiply, IFFT layers 1..32
+//   transpose
+//   transposed: IFFT layers 64, 128 (constants independent of q), formal
+//               derivative, FFT layers 128, 64
+//   transpose
+//   block:      FFT layers 32..1, postmultiply of missing shards
+// The formal derivative (leopard8.go FormalDerivative: for i in 1..n-1,
+// work[i-w, i) ^= work[i, i+w), w = lowbit(i)) has the closed form
+//   D(x)_e = x_e ^ XOR_{s : bit s of e == 0} x_{e | 2^s}   (original x),
+// so the local bits are applied in place in ascending order and the two part
+// bits (4, 5) come from the partner parts' original values via LDS.
+// ---------------------------------------------------------------------------
+constexpr int kD4Threads = 256;
+
+// 4x4 (part, 16-element group) transpose in 4 chunks of 4 group-slots:
+// element 16c + b of part q <-> element 16q + b of part c.
+template <int Q>
+__device__ __forceinline__ void xpose4(uint32_t (&w)[64], uint32_t (*xch)[4][4][64], int lane) {
+#pragma unroll
+  for (int h = 0; h < 4; h++) {
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+#pragma unroll
+      for (int bb = 0; bb < 4; bb++) xch[c][Q][bb][lane] = w[16 * c + 4 * h + bb];
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+#pragma unroll
+      for (int bb = 0; bb < 4; bb++) w[16 * c + 4 * h + bb] = xch[Q][c][bb][lane];
+    __syncthreads();
+  }
+}
+
+// Runtime multiply y * exp(lm) from the LDS copy of the 2-bit lookup tables
+// (tab[lm] = kGf8.t[0..3][lm]); lm is wave-uniform, so the ds_read broadcasts.
+__device__ __forceinline__ uint32_t gf8_mul_lds(uint32_t y, const uint4* tab, uint32_t lm) {
+  const uint4 t = tab[lm];
+  const uint32_t p0 = __builtin_amdgcn_perm(t.x, t.x, y & 0x03030303u);
+  const uint32_t p1 = __builtin_amdgcn_perm(t.y, t.y, (y >> 2) & 0x03030303u);
+  const uint32_t p2 = __builtin_amdgcn_perm(t.z, t.z, (y >> 4) & 0x03030303u);
+  const uint32_t p3 = __builtin_amdgcn_perm(t.w, t.w, (y >> 6) & 0x03030303u);
+  return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(p0, p1, p2, 0x96), p3, 0u, 0x96);
+}
+
+template <int Q>
+__device__ __forceinline__ void decode128_part(const DecodeArgs& a, long v, int lane, uint32_t col, bool active,
+                                               uint32_t (*xch)[4][4][64], const uint4* tab) {
+  constexpr int K = 128, N = 256;
+  const long sq = v / a.nvec, vec = v % a.nvec;
+  uint8_t* base = a.data + sq * a.sq_stride + vec * a.vec_stride;
+  const auto rsrc = make_rsrc(base);
+  const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
+  const uint8_t* err = a.err + v * 256;
+  const uint32_t ss = (uint32_t)a.shard_stride;
+  // presence of the shard behind work index i: bit (i & 63) of pm[i >> 6]
+  // (wave-uniform ballots); this part's error locators, one per lane
+  uint64_t pm[4];
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const int i = 64 * c + lane;
+    const int sh = i < K ? K + i : i - K;
+    pm[c] = __ballot(pres[(long)sh * a.p_shard_stride] != 0);
+  }
+  const uint32_t my_err = err[64 * Q + lane];
+
+  uint32_t w[64];
+#pragma unroll
+  for (int j = 0; j < 64; j++) {  // work[i] = present ? shard * errLocs[i] : 0, [parity K][data K]
+    const int i = 64 * Q + j;
+    const int sh = i < K ? K + i : i - K;
+    const bool p = (pm[Q] >> j) & 1;
+    uint32_t x = 0;
+    if (p && active) x = __builtin_amdgcn_raw_buffer_load_b32(rsrc, col, (uint32_t)sh * ss, 0);
+    w[j] = p ? gf8_mul_lds(x, tab, __builtin_amdgcn_readlane(my_err, j)) : 0u;
+  }
+  ifft_dec_local<N, 64, 64 * Q, 1>(w);  // IFFT layers 1..32
+  xpose4<Q>(w, xch, lane);
+  {  // IFFT radix-4 step dist 64 (iend = 64): layers 64 then 128
+    constexpr int l01 = kGf8.skew[63], l02 = kGf8.skew[127], l23 = kGf8.skew[191];
+#pragma unroll
+    for (int b = 0; b < 16; b++) {
+      ifft2(w[b], w[16 + b], l01);
+      ifft2(w[32 + b], w[48 + b], l23);
+      ifft2(w[b], w[32 + b], l02);
+      ifft2(w[16 + b], w[48 + b], l02);
+    }
+  }
+  {  // formal derivative; slot 16a + b is element 64a + 16Q + b
+    uint32_t t[64];
+    uint32_t (*xd)[64] = &xch[0][0][0];  // [4 parts * 16 slots][64 lanes] per chunk
+#pragma unroll
+    for (int h = 0; h < 4; h++) {  // cross bits 4 (part ^ 1) and 5 (part ^ 2), original values
+#pragma unroll
+      for (int u = 0; u < 16; u++) xd[Q * 16 + u][lane] = w[16 * h + u];
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < 16; u++) {
+        uint32_t acc = 0;
+        if constexpr ((Q & 1) == 0) acc ^= xd[(Q | 1) * 16 + u][lane];
+        if constexpr ((Q & 2) == 0) acc ^= xd[(Q | 2) * 16 + u][lane];
+        t[16 * h + u] = acc;
+      }
+      __syncthreads();
+    }
+    // local bits 0-3 (slot bits 0-3) and 6-7 (slot bits 4-5), ascending in place
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+      uint32_t acc = w[j] ^ t[j];
+#pragma unroll
+      for (int sb = 0; sb < 6; sb++)
+        if (((j >> sb) & 1) == 0) acc ^= w[j | (1 << sb)];
+      w[j] = acc;
+    }
+  }
+  {  // FFT radix-4 step dist4 = 256, dist = 64 (iend = 64): layers 128 then 64
+    constexpr int l01 = kGf8.skew[63], l02 = kGf8.skew[127], l23 = kGf8.skew[191];
+#pragma unroll
+    for (int b = 0; b < 16; b++) {
+      fft2(w[b], w[32 + b], l02);
+      fft2(w[16 + b], w[48 + b], l02);
+      fft2(w[b], w[16 + b], l01);
+      fft2(w[32 + b], w[48 + b], l23);
+    }
+  }
+  xpose4<Q>(w, xch, lane);
+  fft_dec_local<N, 64, 64 * Q, 64>(w);  // FFT layers 32..1
+  if (!active) return;
+#pragma unroll
+  for (int j = 0; j < 64; j++) {  // missing shard s = work[pos] * (255 - errLocs[pos])
+    const int pos = 64 * Q + j;
+    const int sh = pos < K ? pos + K : pos - K;
+    if (((pm[Q] >> j) & 1) == 0) {  // shard sh (work index pos) was missing
+      const uint32_t y = gf8_mul_lds(w[j], tab, 255u - __builtin_amdgcn_readlane(my_err, j));
+      __builtin_amdgcn_raw_buffer_store_b32(y, rsrc, col, (uint32_t)sh * ss, 0);
+    }
+  }
+}
+
+// One block = 4 waves (parts) x 64 dword columns = 256 B of one vector.
+__global__ __launch_bounds__(kD4Threads) __attribute__((amdgpu_waves_per_eu(3, 8)))
+void leo8_decode128_kernel(DecodeArgs a, int nchunk256) {
+  const long blk = blockIdx.x;
+  const int chunk = (int)(blk % nchunk256);
+  const long v = blk / nchunk256;
+  if (a.flags[v] == 0) return;  // uniform
+  __shared__ uint32_t xch[4][4][4][64];
+  __shared__ uint4 tab[256];
+  tab[threadIdx.x] = make_uint4(kGf8.t[0][threadIdx.x], kGf8.t[1][threadIdx.x], kGf8.t[2][threadIdx.x],
+                                kGf8.t[3][threadIdx.x]);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t col = (uint32_t)chunk * 256u + (uint32_t)lane * 4u;
+  const bool active = col < (uint32_t)a.shard_bytes;
+  switch (q) {
+    case 0: decode128_part<0>(a, v, lane, col, active, xch, tab); break;
+    case 1: decode128_part<1>(a, v, lane, col, active, xch, tab); break;
+    case 2: decode128_part<2>(a, v, lane, col, active, xch, tab); break;
+    default: decode128_part<3>(a, v, lane, col, active, xch, tab); break;
+  }
+}
+
 // Marks rebuilt shards present (separate launch so decode kernels of the same
 // pass read a stable presence map).
 __global__ __launch_bounds__(256) void mark_present_kernel(DecodeArgs a) {
@@ -333,7 +502,16 @@ hipError_t launch_leo8_decode_only(const DecodeArgs& a, hipStream_t s, bool mark
     case 16: e = launch_dec<16, 1>(a, s); break;
     case 32: e = launch_dec<32, 1>(a, s); break;
     case 64: e = launch_dec<64, 1>(a, s); break;
-    case 128: e = launch_dec<128, 2>(a, s); break;
+    case 128: {
+#ifdef DAGPU_DEC128_H2
+      e = launch_dec<128, 2>(a, s);
+#else
+      const long nc = (a.shard_bytes + 255) / 256;
+      hipLaunchKernelGGL(leo8_decode128_kernel, dim3((unsigned)(nv * nc)), dim3(kD4Threads), 0, s, a, (int)nc);
+      e = hipGetLastError();
+#endif
+      break;
+    }
     default: return hipErrorInvalidValue;
   }
   if (e != hipSuccess) return e;
