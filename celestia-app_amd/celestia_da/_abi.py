@@ -59,6 +59,10 @@ EXPORTS = (
     "dagpu_split_rows_device",
     "dagpu_split_cols_device",
     "dagpu_split_finish_device",
+    "dagpu_row_nodes_size",
+    "dagpu_row_nodes_workspace_size",
+    "dagpu_row_nodes_device",
+    "dagpu_row_nodes_gather_device",
 )
 
 PREFIX_NONE = 0
@@ -127,6 +131,12 @@ def lib() -> ctypes.CDLL:
         L.dagpu_split_cols_device.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, vp, vp,
                                               vp, vp, vp, vp]
         L.dagpu_split_finish_device.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp, vp, vp, vp]
+        L.dagpu_row_nodes_size.argtypes = [ctypes.c_uint32]
+        L.dagpu_row_nodes_size.restype = sz
+        L.dagpu_row_nodes_workspace_size.argtypes = [ctypes.c_uint32]
+        L.dagpu_row_nodes_workspace_size.restype = sz
+        L.dagpu_row_nodes_device.argtypes = [vp, ctypes.c_uint32, vp, vp, vp, vp]
+        L.dagpu_row_nodes_gather_device.argtypes = [vp, ctypes.c_uint32, vp, sz, vp, vp, vp]
         L.dagpu_profile_enable.argtypes = [vp, ctypes.c_int]
         L.dagpu_profile_read.argtypes = [vp, vp, vp, ctypes.c_int]
         _lib = L

@@ -69,6 +69,10 @@ hipError_t launch_forest_roots(const uint8_t* leaves, const uint8_t* inner, cons
 hipError_t launch_ns_order_check(const uint8_t* base, long nvec, long nper, long vec_stride, long elem_stride,
                                  int32_t* status, int bit, hipStream_t s);
 
+// Gather (row, depth, position) nodes of exported row trees as packed 90-B nodes.
+hipError_t launch_node_gather(const uint8_t* nodes, int w, const uint32_t* req, long n, uint8_t* out,
+                              hipStream_t s);
+
 // Host-side level plan of one forest.  Leaves (level 0) are either packed tree
 // after tree (ragged: counts[t] leaves each) or uniform with (tstride,
 // lstride) addressing inside a caller-owned leaf array.  Levels >= 1 are packed

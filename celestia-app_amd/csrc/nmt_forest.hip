@@ -336,6 +336,35 @@ hipError_t launch_ns_order_check(const uint8_t* base, long nvec, long nper, long
 }
 
 // ---------------------------------------------------------------------------
+// Node gather for exported row-tree levels (inclusion.EDSSubTreeRootCacher):
+// request r = (row, depth, position); level L = log2(w) - depth; record at
+// lvl_off(L) + row * (w >> L) + position with lvl_off(L) = sum_{l<L} w*(w>>l).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void node_gather_kernel(const uint8_t* nodes, int w, int logw, const uint32_t* req,
+                                                          long n, uint8_t* out) {
+  const long t = (long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n) return;
+  const uint32_t row = req[3 * t], depth = req[3 * t + 1], pos = req[3 * t + 2];
+  const int L = logw - (int)depth;
+  long off = 0;
+  for (int l = 0; l < L; l++) off += (long)w * (w >> l);
+  const uint8_t* p = nodes + (off + (long)row * (w >> L) + pos) * kRecNmt;
+  uint32_t mn[8], mx[8], dg[8];
+  load8(p, mn); load8(p + 32, mx); load8(p + 64, dg);
+  write_root(out + t * kNodeSize, mn, mx, dg);
+}
+
+hipError_t launch_node_gather(const uint8_t* nodes, int w, const uint32_t* req, long n, uint8_t* out,
+                              hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  int logw = 0;
+  while ((1 << logw) < w) logw++;
+  hipLaunchKernelGGL(node_gather_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, nodes, w, logw, req,
+                     n, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Host planner.
 // ---------------------------------------------------------------------------
 ForestPlan ForestPlan::uniform_plan(long ntrees, long leaves, long tstride, long lstride) {

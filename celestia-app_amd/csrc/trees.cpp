@@ -226,6 +226,56 @@ int dagpu_merkle_roots(dagpu_ctx* ctx, size_t ntrees, const uint32_t* counts, co
   return DAGPU_OK;
 }
 
+size_t dagpu_row_nodes_size(uint32_t k) {
+  if (k == 0 || !is_pow2(k) || k > (uint32_t)kMaxK) return 0;
+  const long w = 2L * k;
+  long recs = 0;
+  for (long per = w; per >= 1; per >>= 1) recs += w * per;
+  return (size_t)recs * kRecNmt;
+}
+
+size_t dagpu_row_nodes_workspace_size(uint32_t k) {
+  if (k == 0 || !is_pow2(k) || k > (uint32_t)kMaxK) return 0;
+  const long w = 2L * k;
+  return (size_t)w * sizeof(int64_t) + 256;  // plan metadata (root indices)
+}
+
+int dagpu_row_nodes_device(dagpu_ctx* ctx, uint32_t k, const uint8_t* d_eds, uint8_t* d_nodes, void* d_workspace,
+                           void* stream) {
+  if (!ctx || !d_eds || !d_nodes || !d_workspace) return DAGPU_ERR_ARG;
+  int rc = check_k(ctx, k);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const long w = 2L * k;
+  // leaves (level 0): every cell with the wrapper namespace rule, row-major
+  ForestLeafArgs la{};
+  la.data = d_eds;
+  la.data_stride = kShareSize;
+  la.dlen = kShareSize;
+  la.nleaves = w * w;
+  la.pmode = kPfxGrid;
+  la.grid_k = (int)k;
+  la.grid_w = w;
+  la.out = d_nodes;
+  HIP_TRY(ctx, launch_forest_leaves(la, s));
+  // every row tree, all levels kept: level L packed right after level L-1
+  ForestPlan plan = ForestPlan::uniform_plan(w, w, w, 1);
+  HIP_TRY(ctx, forest_enqueue(plan, d_nodes, d_nodes + (size_t)w * w * kRecNmt, (int64_t*)d_workspace, 1, 0, 0,
+                              nullptr, d_nodes + (size_t)w * w * kRecNmt + (size_t)plan.base[plan.nlevels] * kRecNmt,
+                              1, 0, s));
+  HIP_TRY(ctx, hipStreamSynchronize(s));  // plan metadata upload complete
+  return DAGPU_OK;
+}
+
+int dagpu_row_nodes_gather_device(dagpu_ctx* ctx, uint32_t k, const uint8_t* d_nodes, size_t n,
+                                  const uint32_t* d_requests, uint8_t* d_out, void* stream) {
+  if (!ctx || !d_nodes || (n && (!d_requests || !d_out))) return DAGPU_ERR_ARG;
+  int rc = check_k(ctx, k);
+  if (rc) return rc;
+  HIP_TRY(ctx, launch_node_gather(d_nodes, 2 * (int)k, d_requests, (long)n, d_out, (hipStream_t)stream));
+  return DAGPU_OK;
+}
+
 int dagpu_subtree_width(uint64_t share_count, uint32_t subtree_root_threshold) {
   if (subtree_root_threshold == 0) return DAGPU_ERR_ARG;
   return (int)subtree_width(share_count, subtree_root_threshold);

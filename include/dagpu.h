@@ -235,6 +235,23 @@ int dagpu_split_finish_device(dagpu_ctx* ctx, uint32_t k, uint32_t parts,
                               uint8_t* d_row_roots, uint8_t* d_dah, void* d_workspace,
                               void* stream);
 
+/* ---- Row-tree inner nodes (nmt.NodeVisitor / inclusion.EDSSubTreeRootCacher,
+ * pkg/inclusion/nmt_caching.go:81-128; share commitments from the EDS,
+ * get_commit.go:12-30) ------------------------------------------------------
+ * dagpu_row_nodes_device hashes every node of every row NMT of one EDS (device
+ * memory) into d_nodes (dagpu_row_nodes_size(k) bytes): 96-B records minNs[32]
+ * maxNs[32] digest[32]; level L (0 = leaves, log2(2k) = root) is packed after
+ * level L-1, row-major, so node (row, L, p) is record
+ * sum_{l<L} 2k*(2k>>l) + row*(2k>>L) + p.  Synchronises `stream`.
+ * dagpu_row_nodes_gather_device reads n (row, depth, position) uint32 triples
+ * (depth 0 = root) and writes n packed 90-B nodes. */
+size_t dagpu_row_nodes_size(uint32_t k);
+size_t dagpu_row_nodes_workspace_size(uint32_t k);
+int dagpu_row_nodes_device(dagpu_ctx* ctx, uint32_t k, const uint8_t* d_eds, uint8_t* d_nodes,
+                           void* d_workspace, void* stream);
+int dagpu_row_nodes_gather_device(dagpu_ctx* ctx, uint32_t k, const uint8_t* d_nodes, size_t n,
+                                  const uint32_t* d_requests, uint8_t* d_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
