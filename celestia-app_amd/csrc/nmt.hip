@@ -39,26 +39,50 @@ namespace dagpu {
 // Kernel 1: leaf digests.  digest(r,c) = SHA256(0x00 | P | share), where
 // P = share[0:29] if r<k && c<k else 0xFF*29 (ParitySharesNamespace).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void nmt_leaf_kernel(SquareArgs a) {
+// One lane per leaf.  The share is read one full 128-B line at a time (eight
+// back-to-back 16-B loads per lane), so each line is fetched from HBM once even
+// though a lane consumes it over two SHA blocks (reading 64 B per block let
+// lines be evicted between the halves: +37 % FETCH_SIZE, r01).  Message block b
+// needs share uint4 4b-2 .. 4b+2: line s (uint4 8s .. 8s+7) feeds blocks 2s
+// and 2s+1, with two uint4 carried over.  An LDS-staged coalesced variant
+// (DAGPU_LEAF_LDS) fetches the same bytes but runs ~10 % slower (occupancy).
+constexpr int kLeafWave = 256;
+
+__global__ __launch_bounds__(kLeafWave) void nmt_leaf_kernel(SquareArgs a) {
   const int k = a.k;
   const long w = 2L * k;
   const long cells = w * w;
-  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
-  if (gid >= cells * a.nsq) return;
+  const long total = cells * a.nsq;
+  const long gid = (long)blockIdx.x * kLeafWave + threadIdx.x;
+  if (gid >= total) return;
+  const bool valid = true;
   const long sq = gid / cells;
   const long cell = gid - sq * cells;
   const long r = cell / w, c = cell - (cell / w) * w;
   const bool q0 = (r < k) && (c < k);
-
-  // Message 0x00 | P | share (542 B) as big-endian words: word J >= 8 is share
-  // bytes 4J-30..4J-27 = perm(dw[J-8], dw[J-7]) (share starts at byte 30).
   const uint4* src = (const uint4*)(a.eds + sq * a.eds_sq_stride + cell * kShareSize);
+  uint4 cur[8];
+  auto stage = [&](int st) {
+#pragma unroll
+    for (int q = 0; q < 8; q++) cur[q] = src[8 * st + q];
+  };
+  // one SHA block from 5 consecutive uint4 (dwords 16b-8 .. 16b+8 of the share)
+  auto mid_block = [&](uint32_t (&st)[8], const uint4& u0, const uint4& u1, const uint4& u2, const uint4& u3,
+                       const uint4& u4) {
+    const uint32_t d[20] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w, u2.x, u2.y,
+                            u2.z, u2.w, u3.x, u3.y, u3.z, u3.w, u4.x, u4.y, u4.z, u4.w};
+    uint32_t m[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) m[j] = __builtin_amdgcn_perm(d[j], d[j + 1], 0x06070001u);
+    sha256_compress(st, m);
+  };
+
   uint32_t st[8];
   sha256_init(st);
-  uint32_t m[16];
-  uint4 carry;
+  stage(0);
   {  // block 0: 0x00 | P(29) | share[0:34]
-    const uint4 q0v = src[0], q1v = src[1], q2v = src[2];
+    uint32_t m[16];
+    const uint4 q0v = cur[0], q1v = cur[1], q2v = cur[2];
     const uint32_t d[12] = {q0v.x, q0v.y, q0v.z, q0v.w, q1v.x, q1v.y,
                             q1v.z, q1v.w, q2v.x, q2v.y, q2v.z, q2v.w};
     if (q0) {
@@ -73,7 +97,7 @@ __global__ __launch_bounds__(256) void nmt_leaf_kernel(SquareArgs a) {
       m[7] = 0xFFFF0000u;
     }
     m[7] |= __builtin_amdgcn_perm(d[0], d[0], (PZ << 24) | (PZ << 16) | 0x0001u);
-    if (q0) {  // dense Q0 namespace table (29 B, zero padded to 32)
+    if (q0 && valid) {  // dense Q0 namespace table (29 B, zero padded to 32)
       uint4* nsp = (uint4*)(a.ns_table + (sq * k * k + r * k + c) * 32);
       nsp[0] = make_uint4(d[0], d[1], d[2], d[3]);
       nsp[1] = make_uint4(d[4], d[5], d[6], d[7] & 0xFFu);
@@ -81,23 +105,20 @@ __global__ __launch_bounds__(256) void nmt_leaf_kernel(SquareArgs a) {
 #pragma unroll
     for (int j = 8; j < 16; j++) m[j] = __builtin_amdgcn_perm(d[j - 8], d[j - 7], 0x06070001u);
     sha256_compress(st, m);
-    carry = q2v;
   }
-  // blocks 1..7: words 16b..16b+15 read dwords 16b-8 .. 16b+8
+  mid_block(st, cur[2], cur[3], cur[4], cur[5], cur[6]);  // block 1
+  uint4 prev0 = cur[6], prev1 = cur[7];
 #pragma unroll 1
-  for (int b = 1; b <= 7; b++) {
-    const uint4 n0 = src[4 * b - 1], n1 = src[4 * b], n2 = src[4 * b + 1], n3 = src[4 * b + 2];
-    const uint32_t d[20] = {carry.x, carry.y, carry.z, carry.w, n0.x, n0.y, n0.z,
-                            n0.w,    n1.x,    n1.y,    n1.z,    n1.w, n2.x, n2.y,
-                            n2.z,    n2.w,    n3.x,    n3.y,    n3.z, n3.w};
-#pragma unroll
-    for (int j = 0; j < 16; j++) m[j] = __builtin_amdgcn_perm(d[j], d[j + 1], 0x06070001u);
-    sha256_compress(st, m);
-    carry = n3;
+  for (int s2 = 1; s2 <= 3; s2++) {  // blocks 2 s2 and 2 s2 + 1
+    stage(s2);
+    mid_block(st, prev0, prev1, cur[0], cur[1], cur[2]);
+    mid_block(st, cur[2], cur[3], cur[4], cur[5], cur[6]);
+    prev0 = cur[6];
+    prev1 = cur[7];
   }
   {  // block 8: share[482:512] | 0x80 | zeros | bit length
-    const uint4 n0 = src[31];
-    const uint32_t d[8] = {carry.x, carry.y, carry.z, carry.w, n0.x, n0.y, n0.z, n0.w};
+    uint32_t m[16];
+    const uint32_t d[8] = {prev0.x, prev0.y, prev0.z, prev0.w, prev1.x, prev1.y, prev1.z, prev1.w};
 #pragma unroll
     for (int j = 0; j < 7; j++) m[j] = __builtin_amdgcn_perm(d[j], d[j + 1], 0x06070001u);
     m[7] = __builtin_amdgcn_perm(d[7], d[7], (0x0607u << 16) | (PZ << 8) | PZ) | 0x8000u;
@@ -125,8 +146,11 @@ __device__ __forceinline__ void load_ns(const uint8_t* share, bool q0, uint32_t 
 }
 
 // ---------------------------------------------------------------------------
-// Kernel 2: one tree level.  Tree id t in [0, nsq*2w): sq = t / 2w,
-// axis = (t / w) & 1, idx = t % w.  Level L has w >> L nodes per tree.
+// Kernel 2: one tree level.  Level L has per = w >> L nodes per tree; a
+// square's level-L records are [row trees: w x per, tree-major][column trees:
+// per x w, NODE-major], so consecutive lanes of a column level walk across
+// columns and read consecutive digests / records (coalesced) just like the
+// lanes of a row level walk along a row.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kParityRef = 0xFFFFFFFFu;
 
@@ -145,6 +169,22 @@ __device__ __forceinline__ void ns_by_ref(const uint8_t* ns_sq, uint32_t ref, ui
 
 // Level 1: pairs of leaves.  Leaf node = ns | ns | digest; a Q0 leaf whose
 // namespace equals the parity namespace gets kParityRef (same bytes).
+__device__ __forceinline__ void level_coords(long gid, int w, int per, long& sq, int& axis, int& idx, int& p) {
+  const long blk = 2L * w * per;  // records of one square at this level
+  sq = gid / blk;
+  const long g = gid - sq * blk;
+  axis = g >= (long)w * per;
+  const long g2 = g - (axis ? (long)w * per : 0);
+  if (axis == 0) { idx = (int)(g2 / per); p = (int)(g2 - (long)idx * per); }
+  else { p = (int)(g2 / w); idx = (int)(g2 - (long)p * w); }
+}
+
+// record index of node (axis, idx, p) of square sq at a level with `per` nodes per tree
+__device__ __forceinline__ long level_rec(long sq, int w, int per, int axis, int idx, int p) {
+  const long base = sq * 2L * w * per;
+  return axis == 0 ? base + (long)idx * per + p : base + (long)w * per + (long)p * w + idx;
+}
+
 __global__ __launch_bounds__(256) void nmt_level1_kernel(SquareArgs a, uint8_t* out_rec, int final_level) {
   const int k = a.k;
   const int w = 2 * k;
@@ -152,11 +192,9 @@ __global__ __launch_bounds__(256) void nmt_level1_kernel(SquareArgs a, uint8_t* 
   const long gid = (long)blockIdx.x * 256 + threadIdx.x;
   const long total = a.nsq * 2L * w * half;
   if (gid >= total) return;
-  const long t = gid / half;
-  const int p = (int)(gid - t * half);
-  const long sq = t / (2L * w);
-  const int axis = (int)((t / w) & 1);
-  const int idx = (int)(t % w);
+  long sq;
+  int axis, idx, p;
+  level_coords(gid, w, half, sq, axis, idx, p);
   const uint8_t* dig = a.digests + sq * (long)w * w * kDigest;
   const uint8_t* ns_sq = a.ns_table + sq * (long)k * k * 32;
   const int j0 = 2 * p, j1 = 2 * p + 1;
@@ -212,11 +250,12 @@ __global__ __launch_bounds__(256) void nmt_level_kernel(SquareArgs a, const uint
   const long gid = (long)blockIdx.x * 256 + threadIdx.x;
   const long total = a.nsq * 2L * w * per;
   if (gid >= total) return;
-  const long t = gid / per;
-  const long sq = t / (2L * w);
+  long sq;
+  int axis, idx, p;
+  level_coords(gid, w, per, sq, axis, idx, p);
   const uint8_t* ns_sq = a.ns_table + sq * (long)k * k * 32;
-  const uint4* li = (const uint4*)(in_rec + (2 * gid) * 48);
-  const uint4* ri = li + 3;
+  const uint4* li = (const uint4*)(in_rec + level_rec(sq, w, 2 * per, axis, idx, 2 * p) * 48);
+  const uint4* ri = (const uint4*)(in_rec + level_rec(sq, w, 2 * per, axis, idx, 2 * p + 1) * 48);
   const uint4 l0 = li[0], l1 = li[1], l2 = li[2], r0 = ri[0], r1 = ri[1], r2 = ri[2];
   const uint32_t dl[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
   const uint32_t dr[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
@@ -235,8 +274,6 @@ __global__ __launch_bounds__(256) void nmt_level_kernel(SquareArgs a, const uint
   for (int i = 0; i < 8; i++) dg[i] = bswap32(st[i]);
   const bool rpar = r2.x == kParityRef;
   if (final_level) {
-    const int axis = (int)((t / w) & 1);
-    const int idx = (int)(t % w);
     uint8_t* dst = (axis == 0 ? a.row_roots : a.col_roots) + (sq * w + idx) * kNodeSize;
     if (rpar) write_root(dst, lmn, lmx, dg);
     else write_root(dst, lmn, rmx, dg);
@@ -334,8 +371,8 @@ __global__ __launch_bounds__(kDahThreads) void dah_kernel(SquareArgs a) {
 hipError_t launch_nmt_leaves(const SquareArgs& a, hipStream_t s) {
   const long w = 2L * a.k;
   const long total = w * w * a.nsq;
-  const long blocks = (total + 255) / 256;
-  hipLaunchKernelGGL(nmt_leaf_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a);
+  const long blocks = (total + kLeafWave - 1) / kLeafWave;
+  hipLaunchKernelGGL(nmt_leaf_kernel, dim3((unsigned)blocks), dim3(kLeafWave), 0, s, a);
   return hipGetLastError();
 }
 
