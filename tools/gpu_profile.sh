@@ -4,7 +4,7 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp; cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/prof; mkdir -p $OUT
 TAG=${1:-r01}
-timeout -k 10 120 ./tools/valu_bench > $OUT/valu_bench_$TAG.log 2>&1 || { echo "valu_bench failed"; cat $OUT/valu_bench_$TAG.log; exit 1; }
+timeout -k 10 120 "$GRAFT_REPO_ROOT/tools/valu_bench" > $OUT/valu_bench_$TAG.log 2>&1 || { echo "valu_bench failed"; cat $OUT/valu_bench_$TAG.log; exit 1; }
 cat $OUT/valu_bench_$TAG.log
 BENCH="bench.py --steps 5 --warmup 1 --no-cpu --batch 64 --distinct 8"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_$TAG -o run -- python3 $BENCH > $OUT/trace_$TAG.log 2>&1 || { echo "trace failed"; tail -20 $OUT/trace_$TAG.log; exit 1; }
@@ -15,3 +15,5 @@ for P in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_WAV
   echo "pmc $P ok"
 done
 find $OUT -name "*.csv" | head -50
+timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/calib_$TAG -o run -- "$GRAFT_REPO_ROOT/tools/fetch_calib" > $OUT/calib_$TAG.log 2>&1 || { echo "calib failed"; exit 1; }
+echo "calib ok"
