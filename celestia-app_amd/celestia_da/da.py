@@ -261,6 +261,74 @@ class DataAvailabilityHeader:
         if len(self.hash()) != HASH_SIZE:
             raise DAError(_abi.ERR_ARG, f"wrong hash: expected size to be {HASH_SIZE} bytes")
 
+    def to_proto(self) -> bytes:
+        """ToProto (pkg/da/data_availability_header.go:110-119) serialised as the
+        celestia.core.v1.da.DataAvailabilityHeader message
+        (proto/celestia/core/v1/da/data_availability_header.proto): field 1
+        repeated bytes row_roots, field 2 repeated bytes column_roots."""
+        out = bytearray()
+        for tag, roots in ((0x0A, self.row_roots), (0x12, self.column_roots)):
+            for r in roots:
+                out.append(tag)
+                out += _varint(len(r))
+                out += r
+        return bytes(out)
+
+
+def _varint(v: int) -> bytes:
+    b = bytearray()
+    while True:
+        if v < 0x80:
+            b.append(v)
+            return bytes(b)
+        b.append((v & 0x7F) | 0x80)
+        v >>= 7
+
+
+def data_availability_header_from_proto(buf: bytes) -> DataAvailabilityHeader:
+    """DataAvailabilityHeaderFromProto (:121-132): decode the proto message, then
+    ValidateBasic.  Unknown fields are skipped as proto3 requires."""
+    rows, cols = [], []
+    i, n = 0, len(buf)
+
+    def varint():
+        nonlocal i
+        v, shift = 0, 0
+        while True:
+            if i >= n:
+                raise DAError(_abi.ERR_ARG, "proto: truncated varint")
+            c = buf[i]
+            i += 1
+            v |= (c & 0x7F) << shift
+            if c < 0x80:
+                return v
+            shift += 7
+
+    while i < n:
+        key = varint()
+        field, wt = key >> 3, key & 7
+        if wt == 2:
+            ln = varint()
+            if i + ln > n:
+                raise DAError(_abi.ERR_ARG, "proto: truncated bytes field")
+            val = bytes(buf[i:i + ln])
+            i += ln
+            if field == 1:
+                rows.append(val)
+            elif field == 2:
+                cols.append(val)
+        elif wt == 0:
+            varint()
+        elif wt == 1:
+            i += 8
+        elif wt == 5:
+            i += 4
+        else:
+            raise DAError(_abi.ERR_ARG, f"proto: unsupported wire type {wt}")
+    dah = DataAvailabilityHeader(rows, cols)
+    dah.validate_basic()
+    return dah
+
 
 def nil_dah_hash() -> bytes:
     """(*DataAvailabilityHeader)(nil).Hash() == merkle.HashFromByteSlices(nil)."""

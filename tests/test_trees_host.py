@@ -74,3 +74,52 @@ def test_nmt_push_order_on_host():
     t.push(b"\x02" * 40)
     with pytest.raises(trees.ErrInvalidPushOrder):
         t.push(b"\x01" * 40)
+
+
+# ---- DataAvailabilityHeader proto (pkg/da/data_availability_header.go:110-132,
+# TestDataAvailabilityHeaderProtoConversion :101-134) -------------------------------
+
+def _proto_class():
+    """The reference's .proto message built at run time with the protobuf
+    runtime (an independent encoder to check the hand-written wire format)."""
+    from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
+    fdp = descriptor_pb2.FileDescriptorProto(name="dah_test.proto", package="celestia.core.v1.da", syntax="proto3")
+    m = fdp.message_type.add(name="DataAvailabilityHeader")
+    for num, name in ((1, "row_roots"), (2, "column_roots")):
+        m.field.add(name=name, number=num, type=descriptor_pb2.FieldDescriptorProto.TYPE_BYTES,
+                    label=descriptor_pb2.FieldDescriptorProto.LABEL_REPEATED)
+    pool = descriptor_pool.DescriptorPool()
+    pool.Add(fdp)
+    desc = pool.FindMessageTypeByName("celestia.core.v1.da.DataAvailabilityHeader")
+    return message_factory.GetMessageClass(desc)
+
+
+def test_dah_proto_round_trip():
+    import numpy as np
+    import oracle
+    from celestia_da import da, synth
+
+    mind = da.DataAvailabilityHeader(*_min_roots())
+    k = 128
+    _, rr, cr, _ = oracle.extend_and_dah(synth.random_blob_square(k, 1), k, nthreads=8, want_eds=False)
+    big = da.DataAvailabilityHeader([rr[i].tobytes() for i in range(2 * k)], [cr[i].tobytes() for i in range(2 * k)])
+    cls = _proto_class()
+    for dah in (mind, big):
+        wire = dah.to_proto()
+        back = da.data_availability_header_from_proto(wire)
+        assert back.row_roots == dah.row_roots and back.column_roots == dah.column_roots
+        assert back.hash() == dah.hash()
+        ref = cls(row_roots=dah.row_roots, column_roots=dah.column_roots)
+        assert ref.SerializeToString() == wire
+        assert da.data_availability_header_from_proto(ref.SerializeToString()).hash() == dah.hash()
+    with pytest.raises(da.DAError, match="minimum valid"):
+        da.data_availability_header_from_proto(b"")
+
+
+def _min_roots():
+    import oracle
+    from celestia_da import da
+    import numpy as np
+    share = np.frombuffer(da.tail_padding_share(), np.uint8).reshape(1, 512)
+    _, rr, cr, _ = oracle.extend_and_dah(share, 1)
+    return [rr[i].tobytes() for i in range(2)], [cr[i].tobytes() for i in range(2)]
