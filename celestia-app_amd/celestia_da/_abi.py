@@ -53,6 +53,7 @@ EXPORTS = (
     "dagpu_nmt_roots",
     "dagpu_wrapper_roots",
     "dagpu_merkle_roots",
+    "dagpu_merkle_levels",
     "dagpu_subtree_width",
     "dagpu_blob_commitments",
     "dagpu_split_workspace_size",
@@ -122,6 +123,7 @@ def lib() -> ctypes.CDLL:
         L.dagpu_nmt_roots.argtypes = [vp, sz, vp, vp, sz, ctypes.c_int, vp, ctypes.c_int, vp, vp]
         L.dagpu_wrapper_roots.argtypes = [vp, ctypes.c_uint64, sz, vp, vp, vp, sz, vp, vp]
         L.dagpu_merkle_roots.argtypes = [vp, sz, vp, vp, sz, vp]
+        L.dagpu_merkle_levels.argtypes = [vp, sz, vp, sz, vp, ctypes.POINTER(sz)]
         L.dagpu_subtree_width.argtypes = [ctypes.c_uint64, ctypes.c_uint32]
         L.dagpu_blob_commitments.argtypes = [vp, sz, vp, vp, vp, ctypes.c_uint32, vp]
         L.dagpu_split_workspace_size.argtypes = [ctypes.c_uint32, ctypes.c_uint32]

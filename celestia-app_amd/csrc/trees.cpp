@@ -276,6 +276,44 @@ int dagpu_row_nodes_gather_device(dagpu_ctx* ctx, uint32_t k, const uint8_t* d_n
   return DAGPU_OK;
 }
 
+int dagpu_merkle_levels(dagpu_ctx* ctx, size_t n, const uint8_t* items, size_t item_len, uint8_t* out32,
+                        size_t* n_nodes) {
+  if (!ctx || !n_nodes || (n && (!items || !out32))) return DAGPU_ERR_ARG;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  (void)hipSetDevice(ctx->device);
+  std::vector<long> cnt{(long)n};
+  ForestPlan plan = ForestPlan::ragged_plan(cnt);
+  const size_t total = n + (size_t)plan.inner_records;
+  if (*n_nodes < total) {
+    *n_nodes = total;
+    return set_err(ctx, DAGPU_ERR_ARG, "output too small for every tree level");
+  }
+  *n_nodes = total;
+  if (n == 0) return DAGPU_OK;
+  hipStream_t s = ctx->stream;
+  long stride = 0;
+  int rc = upload_leaves(ctx, items, (long)n, (long)item_len, &stride, s);
+  if (rc) return rc;
+  HIP_TRY(ctx, ctx->t_leaves.ensure(total * kRecRfc + 64));
+  HIP_TRY(ctx, ctx->t_meta.ensure(plan.meta.size() * sizeof(int64_t) + 8));
+  HIP_TRY(ctx, ctx->t_out.ensure(64));
+  ForestLeafArgs la{};
+  la.data = (const uint8_t*)ctx->t_leaf_data.p;
+  la.data_stride = stride;
+  la.dlen = (long)item_len;
+  la.nleaves = (long)n;
+  la.pmode = kPfxNone;
+  la.rfc = 1;
+  la.out = (uint8_t*)ctx->t_leaves.p;
+  HIP_TRY(ctx, launch_forest_leaves(la, s));
+  uint8_t* inner = (uint8_t*)ctx->t_leaves.p + n * kRecRfc;  // levels right after the leaves
+  HIP_TRY(ctx, forest_enqueue(plan, (const uint8_t*)ctx->t_leaves.p, inner, (int64_t*)ctx->t_meta.p, 0, 0, 1,
+                              nullptr, (uint8_t*)ctx->t_out.p, 0, 0, s));
+  HIP_TRY(ctx, hipMemcpyAsync(out32, ctx->t_leaves.p, total * kRecRfc, hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipStreamSynchronize(s));
+  return DAGPU_OK;
+}
+
 int dagpu_subtree_width(uint64_t share_count, uint32_t subtree_root_threshold) {
   if (subtree_root_threshold == 0) return DAGPU_ERR_ARG;
   return (int)subtree_width(share_count, subtree_root_threshold);

@@ -193,6 +193,13 @@ int dagpu_wrapper_roots(dagpu_ctx* ctx, uint64_t square_size, size_t ntrees,
 int dagpu_merkle_roots(dagpu_ctx* ctx, size_t ntrees, const uint32_t* counts,
                        const uint8_t* items, size_t item_len, uint8_t* out32);
 
+/* Every node of ONE RFC-6962 tree (merkle.ProofsFromByteSlices, celestia-core
+ * crypto/merkle; pkg/proof/proof.go:87): the n leaf hashes, then each level
+ * (ceil-halving, an odd last node promoted unchanged) up to the root, 32 B each.
+ * *n_nodes: in = capacity of out32 in nodes, out = nodes written (or needed). */
+int dagpu_merkle_levels(dagpu_ctx* ctx, size_t n, const uint8_t* items, size_t item_len,
+                        uint8_t* out32, size_t* n_nodes);
+
 /* inclusion.SubTreeWidth (pkg/inclusion/blob_share_commitment_rules.go:85-101). */
 int dagpu_subtree_width(uint64_t share_count, uint32_t subtree_root_threshold);
 
