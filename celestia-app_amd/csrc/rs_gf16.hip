@@ -21,9 +21,12 @@
 #include <stdint.h>
 
 #include <mutex>
+#include <vector>
 
 #include "gf16_host.hpp"
 #include "kernels.hpp"
+#include "leo8.hpp"
+#include "sha256.hpp"
 
 namespace dagpu {
 
@@ -335,6 +338,244 @@ __global__ __launch_bounds__(256) void mark_present16_kernel(DecodeArgs a) {
   if (threadIdx.x == 0 && a.progress) atomicAdd(a.progress, 1);
 }
 
+// ---------------------------------------------------------------------------
+// Register-resident GF(2^16) encode (k = m = 256, 512).
+//
+// A wave owns the 64 thread-columns of one 512-B chunk of a vector (lane l:
+// 64-B block l >> 3, symbols 4(l & 7) .. +3 as a lo-byte dword and a hi-byte
+// dword); a workgroup of P = m / 64 waves holds the whole transform, wave q
+// keeping 64 elements (128 VGPRs).  Index bits 0-5 are local in the "block"
+// layout (wave q holds 64q + j); a P x P block transpose through LDS makes
+// bits 6.. local ("transposed" layout: wave q holds the elements whose bits
+// 6-log2P .. 5 equal q), where the top IFFT/FFT layers run.  Multiplies use
+// per-skew-position product tables (16 dwords: for each 2-bit group of the
+// symbol, the 4 possible products' lo and hi bytes) read with scalar loads --
+// the position is wave-uniform -- and 16 v_perm lookups per 4 symbols; a
+// position whose skew is 65535 (leopard "skip") has an all-zero table.
+// ---------------------------------------------------------------------------
+// Positions < 2m = 1024 cover every encoder skew index (IFFT m-1+iend+2d <
+// 2m, FFT iend-1 < m).  __constant__ so that the wave-uniform table reads
+// become scalar loads into SGPRs (64 KiB, the constant-segment limit).
+constexpr int kTabPos = 1024;
+__constant__ uint32_t g_ptab16[kTabPos * 16];
+
+__device__ __forceinline__ void mul16_add(uint32_t& xlo, uint32_t& xhi, uint32_t ylo, uint32_t yhi, int pos) {
+  const uint32_t* t = g_ptab16 + pos * 16;
+  uint32_t pl[8], ph[8];
+#pragma unroll
+  for (int g = 0; g < 4; g++) {
+    const uint32_t sl = (ylo >> (2 * g)) & 0x03030303u;
+    const uint32_t sh = (yhi >> (2 * g)) & 0x03030303u;
+    pl[g] = __builtin_amdgcn_perm(t[g], t[g], sl);
+    ph[g] = __builtin_amdgcn_perm(t[8 + g], t[8 + g], sl);
+    pl[4 + g] = __builtin_amdgcn_perm(t[4 + g], t[4 + g], sh);
+    ph[4 + g] = __builtin_amdgcn_perm(t[12 + g], t[12 + g], sh);
+  }
+  // 8 products + x per output byte plane: four 3-input XORs
+  xlo = xor3(xor3(xor3(xlo, pl[0], pl[1]), xor3(pl[2], pl[3], pl[4]), pl[5]), pl[6], pl[7]);
+  xhi = xor3(xor3(xor3(xhi, ph[0], ph[1]), xor3(ph[2], ph[3], ph[4]), ph[5]), ph[6], ph[7]);
+}
+
+struct W16 {
+  uint32_t lo[64], hi[64];
+};
+
+// ifftDIT2: y ^= x; x ^= y * skew[pos]
+__device__ __forceinline__ void ifft2_16(W16& w, int i, int j, int pos) {
+  w.lo[j] ^= w.lo[i];
+  w.hi[j] ^= w.hi[i];
+  mul16_add(w.lo[i], w.hi[i], w.lo[j], w.hi[j], pos);
+}
+// fftDIT2: x ^= y * skew[pos]; y ^= x
+__device__ __forceinline__ void fft2_16(W16& w, int i, int j, int pos) {
+  mul16_add(w.lo[i], w.hi[i], w.lo[j], w.hi[j], pos);
+  w.lo[j] ^= w.lo[i];
+  w.hi[j] ^= w.hi[i];
+}
+
+// Block layout, encoder IFFT radix-4 steps with dist D..16 (bits 0-5);
+// base = m - 1 + 64 q (ifftDITEncoder skew index m - 1 + iend).
+template <int D>
+__device__ __forceinline__ void ifft16_block(W16& w, int base) {
+#pragma unroll
+  for (int r = 0; r < 64; r += 4 * D) {
+    const int p01 = base + r + D, p02 = p01 + D, p23 = p01 + 2 * D;
+#pragma unroll
+    for (int i = r; i < r + D; i++) {
+      ifft2_16(w, i, i + D, p01);
+      ifft2_16(w, i + 2 * D, i + 3 * D, p23);
+      ifft2_16(w, i, i + 2 * D, p02);
+      ifft2_16(w, i + D, i + 3 * D, p02);
+    }
+  }
+  if constexpr (D * 16 <= 64) ifft16_block<D * 4>(w, base);
+}
+
+// Block layout, fftDIT radix-4 step with dist DIST (dist4 = 4 DIST) and the
+// ones below it; base = 64 q (skew index iend - 1).  The final radix-2 layer
+// exists when the last dist4 is 2.
+template <int DIST>
+__device__ __forceinline__ void fft16_block(W16& w, int base) {
+#pragma unroll
+  for (int r = 0; r < 64; r += 4 * DIST) {
+    const int iend = r + DIST;
+    const int p01 = base + iend - 1, p02 = base + iend + DIST - 1, p23 = base + iend + 2 * DIST - 1;
+#pragma unroll
+    for (int i = r; i < r + DIST; i++) {
+      fft2_16(w, i, i + 2 * DIST, p02);
+      fft2_16(w, i + DIST, i + 3 * DIST, p02);
+      fft2_16(w, i, i + DIST, p01);
+      fft2_16(w, i + 2 * DIST, i + 3 * DIST, p23);
+    }
+  }
+  if constexpr (DIST >= 4) {
+    fft16_block<DIST / 4>(w, base);
+  } else if constexpr (DIST == 2) {
+#pragma unroll
+    for (int r = 0; r < 64; r += 2) fft2_16(w, r, r + 1, base + r);
+  }
+}
+
+// P x P block transpose: element (wave Q, slot (c << R) | l) <-> (wave c,
+// slot (Q << R) | l), R = 6 - log2 P, S group-slots per LDS round.
+template <int P, int S>
+__device__ __forceinline__ void xpose16(W16& w, uint32_t* lds, int q, int lane) {
+  constexpr int R = P == 8 ? 3 : 4;
+  constexpr int G = 1 << R;
+  // lds[(dst * P + src) * S + u][2][64]
+#pragma unroll
+  for (int l0 = 0; l0 < G; l0 += S) {
+#pragma unroll
+    for (int c = 0; c < P; c++)
+#pragma unroll
+      for (int u = 0; u < S; u++) {
+        uint32_t* d = lds + (((c * P + q) * S + u) * 2) * 64 + lane;
+        d[0] = w.lo[(c << R) | (l0 + u)];
+        d[64] = w.hi[(c << R) | (l0 + u)];
+      }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < P; c++)
+#pragma unroll
+      for (int u = 0; u < S; u++) {
+        const uint32_t* d = lds + (((q * P + c) * S + u) * 2) * 64 + lane;
+        w.lo[(c << R) | (l0 + u)] = d[0];
+        w.hi[(c << R) | (l0 + u)] = d[64];
+      }
+    __syncthreads();
+  }
+}
+
+template <int M>
+__global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(3, 8))) void leo16_encode_reg_kernel(EncodeArgs a) {
+  constexpr int P = M / 64;
+  constexpr int S = P == 8 ? 1 : 2;
+  __shared__ uint32_t lds[P * P * S * 2 * 64];
+  const long blk = blockIdx.x;
+  const int chunk = (int)(blk % a.nchunk);
+  const long sv = blk / a.nchunk;
+  const long vec = sv % a.nvec;
+  const long sq = sv / a.nvec;
+  if (a.vec_flags && a.vec_flags[sv] == 0) return;  // uniform
+  const int lane = threadIdx.x & 63;
+  const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t col = (uint32_t)chunk * 512u + (uint32_t)(lane >> 3) * 64u + (uint32_t)(lane & 7) * 4u;
+  const bool active = col < (uint32_t)a.shard_bytes;
+  const uint32_t cl = active ? col : 0u;  // inactive lanes read valid memory, store nothing
+  const auto in_rsrc = make_rsrc(a.in + sq * a.in_sq_stride + vec * a.in_vec_stride);
+  const uint32_t in_stride = (uint32_t)a.in_shard_stride;
+  W16 w;
+#pragma unroll
+  for (int j = 0; j < 64; j++) {
+    const uint32_t so = (uint32_t)(64 * q + j) * in_stride;
+    w.lo[j] = __builtin_amdgcn_raw_buffer_load_b32(in_rsrc, cl, so, 0);
+    w.hi[j] = __builtin_amdgcn_raw_buffer_load_b32(in_rsrc, cl + 32u, so, 0);
+  }
+  if (a.copy && active) {
+    const auto cp = make_rsrc(a.copy + sq * a.copy_sq_stride + vec * a.copy_vec_stride);
+    const uint32_t cs = (uint32_t)a.copy_shard_stride;
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+      const uint32_t so = (uint32_t)(64 * q + j) * cs;
+      __builtin_amdgcn_raw_buffer_store_b32(w.lo[j], cp, col, so, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(w.hi[j], cp, col + 32u, so, 0);
+    }
+  }
+  // ---- IFFT (ifftDITEncoder, skew index M - 1 + iend) ----
+  ifft16_block<1>(w, M - 1 + 64 * q);  // bits 0-5
+  xpose16<P, S>(w, lds, q, lane);
+  if constexpr (M == 512) {  // slot 8h + b: h = bits 6-8, b = bits 0-2
+#pragma unroll
+    for (int hr = 0; hr < 8; hr += 4) {  // radix-4 dist 64 (bits 6, 7), groups r = 64 hr
+      const int p01 = M - 1 + 64 * hr + 64, p02 = p01 + 64, p23 = p01 + 128;
+#pragma unroll
+      for (int b = 0; b < 8; b++) {
+        const int s0 = hr * 8 + b;
+        ifft2_16(w, s0, s0 + 8, p01);
+        ifft2_16(w, s0 + 16, s0 + 24, p23);
+        ifft2_16(w, s0, s0 + 16, p02);
+        ifft2_16(w, s0 + 8, s0 + 24, p02);
+      }
+    }
+#pragma unroll
+    for (int s0 = 0; s0 < 32; s0++) ifft2_16(w, s0, s0 + 32, M - 1 + 256);  // last layer, dist 256
+    // ---- FFT (fftDIT, skew index iend - 1) ----
+#pragma unroll
+    for (int s0 = 0; s0 < 16; s0++) {  // dist4 = 512, dist = 128 (bits 8, 7)
+      fft2_16(w, s0, s0 + 32, 255);
+      fft2_16(w, s0 + 16, s0 + 48, 255);
+      fft2_16(w, s0, s0 + 16, 127);
+      fft2_16(w, s0 + 32, s0 + 48, 383);
+    }
+#pragma unroll
+    for (int g2 = 0; g2 < 4; g2++)  // dist4 = 128 step, first sub-layer (bit 6)
+#pragma unroll
+      for (int b = 0; b < 8; b++) fft2_16(w, 16 * g2 + b, 16 * g2 + b + 8, 128 * g2 + 63);
+    xpose16<P, S>(w, lds, q, lane);
+#pragma unroll
+    for (int j = 0; j < 32; j++) fft2_16(w, j, j + 32, 64 * q + 31);  // its second sub-layer (bit 5)
+    fft16_block<8>(w, 64 * q);                                         // bits 4 .. 0
+  } else {  // M == 256: slot 16a + b: a = bits 6-7, b = bits 0-3
+    constexpr int p01 = M - 1 + 64, p02 = p01 + 64, p23 = p01 + 128;
+#pragma unroll
+    for (int b = 0; b < 16; b++) {  // radix-4 dist 64 (bits 6, 7)
+      ifft2_16(w, b, 16 + b, p01);
+      ifft2_16(w, 32 + b, 48 + b, p23);
+      ifft2_16(w, b, 32 + b, p02);
+      ifft2_16(w, 16 + b, 48 + b, p02);
+    }
+#pragma unroll
+    for (int b = 0; b < 16; b++) {  // FFT dist4 = 256, dist = 64 (bits 7, 6)
+      fft2_16(w, b, 32 + b, 127);
+      fft2_16(w, 16 + b, 48 + b, 127);
+      fft2_16(w, b, 16 + b, 63);
+      fft2_16(w, 32 + b, 48 + b, 191);
+    }
+    xpose16<P, S>(w, lds, q, lane);
+    fft16_block<16>(w, 64 * q);  // bits 5 .. 0
+  }
+  if (!active) return;
+  const auto out_rsrc = make_rsrc(a.out + sq * a.out_sq_stride + vec * a.out_vec_stride);
+  const uint32_t os = (uint32_t)a.out_shard_stride;
+  if (a.mismatch) {  // prerepairSanityCheck: parity must equal Encode(data)
+    uint32_t diff = 0;
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+      const uint32_t so = (uint32_t)(64 * q + j) * os;
+      diff |= w.lo[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, col, so, 0);
+      diff |= w.hi[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, col + 32u, so, 0);
+    }
+    if (diff) atomicOr(&a.mismatch[sq], a.mismatch_bit);
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 64; j++) {
+    const uint32_t so = (uint32_t)(64 * q + j) * os;
+    __builtin_amdgcn_raw_buffer_store_b32(w.lo[j], out_rsrc, col, so, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(w.hi[j], out_rsrc, col + 32u, so, 0);
+  }
+}
+
 // Tables are module globals: upload once per device.
 std::mutex g_tab_mu;
 bool g_tab_done[64];
@@ -351,6 +592,29 @@ hipError_t ensure_tables() {
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_exp16), t.exp.data(), 65536 * 2)) != hipSuccess) return e;
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_skew16), t.skew.data(), 65536 * 2)) != hipSuccess) return e;
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_walsh16), t.walsh.data(), 65536 * 2)) != hipSuccess) return e;
+  {  // per skew position: products of every 2-bit group value with skew[pos]
+    std::vector<uint32_t> pt((size_t)kTabPos * 16, 0u);
+    for (int pos = 0; pos < kTabPos; pos++) {
+      const unsigned lm = t.skew[pos];
+      if (lm == kMod16) continue;  // leopard skips the multiply: zero table
+      for (int g = 0; g < 8; g++)
+        for (int e2 = 0; e2 < 4; e2++) {
+          const unsigned x = (unsigned)e2 << (2 * g);
+          unsigned prod = 0;
+          if (x) {
+            unsigned sidx = (unsigned)t.log[x] + lm;
+            sidx = (sidx + (sidx >> 16)) & 0xFFFFu;
+            prod = t.exp[sidx];
+          }
+          // g < 4: groups of the symbol's low byte -> t[g] (lo) / t[8+g] (hi)
+          // g >= 4: groups of the high byte        -> t[4+g-4] (lo) / t[12+g-4] (hi)
+          const int lo_idx = g < 4 ? g : 4 + (g - 4), hi_idx = 8 + lo_idx;
+          pt[(size_t)pos * 16 + lo_idx] |= (prod & 0xFFu) << (8 * e2);
+          pt[(size_t)pos * 16 + hi_idx] |= ((prod >> 8) & 0xFFu) << (8 * e2);
+        }
+    }
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_ptab16), pt.data(), pt.size() * 4)) != hipSuccess) return e;
+  }
   // > 64 KiB of dynamic LDS (errlocs 128 KiB, k = 512 decode 128 KiB)
   if ((e = hipFuncSetAttribute((const void*)leo16_errlocs_kernel,
                                hipFuncAttributeMaxDynamicSharedMemorySize, kErrLds)) != hipSuccess)
@@ -370,6 +634,17 @@ hipError_t launch_leo16_encode(int k, const EncodeArgs& a, hipStream_t s) {
   if (!gf16_k_ok(k) || a.shard_bytes % 64) return hipErrorInvalidValue;
   hipError_t e = ensure_tables();
   if (e != hipSuccess) return e;
+#ifndef DAGPU_GF16_LDS_ENCODE
+  {  // register-resident kernel; nchunk = 512-B chunks of the shard
+    EncodeArgs b = a;
+    b.nchunk = (a.shard_bytes + 511) / 512;
+    const long blocks = b.nsq * b.nvec * b.nchunk;
+    if (blocks <= 0) return hipSuccess;
+    if (k == 256) hipLaunchKernelGGL(leo16_encode_reg_kernel<256>, dim3((unsigned)blocks), dim3(256), 0, s, b);
+    else hipLaunchKernelGGL(leo16_encode_reg_kernel<512>, dim3((unsigned)blocks), dim3(512), 0, s, b);
+    return hipGetLastError();
+  }
+#endif
   const long blocks = a.nsq * a.nvec * (a.shard_bytes / 64);
   if (blocks <= 0) return hipSuccess;
   hipLaunchKernelGGL(leo16_encode_kernel, dim3((unsigned)blocks), dim3(kThreads16),
