@@ -107,8 +107,28 @@ __global__ __launch_bounds__(256) void forest_leaf_kernel(ForestLeafArgs a) {
     const long r = a.grid_r0 + i / a.grid_w, c = a.grid_c0 + i % a.grid_w;
     pm = (r < a.grid_k && c < a.grid_k) ? kPfxSelf : kPfxParity;
   }
-  const MsgShape sh = msg_shape(a.dlen, a.pmode != kPfxNone);
   uint32_t st[8];
+  if (a.dlen == kShareSize && a.pmode != kPfxNone && !a.rfc && (a.data_stride & 15) == 0 &&
+      (((uintptr_t)a.data) & 15) == 0) {
+    // 512-B shares with a namespace prefix (wrapper cells, blob commitments,
+    // split-square slabs): the share-specialised leaf hash of the square pipeline
+    uint32_t ns[8];
+    share_leaf_sha256((const uint4*)d32, pm == kPfxSelf, st, ns);
+    if (pm == kPfxParity) {
+#pragma unroll
+      for (int j = 0; j < 7; j++) ns[j] = 0xFFFFFFFFu;
+      ns[7] = 0xFFu;
+    }
+    uint4* o = (uint4*)(a.out + i * kRecNmt);
+    o[0] = make_uint4(ns[0], ns[1], ns[2], ns[3]);
+    o[1] = make_uint4(ns[4], ns[5], ns[6], ns[7]);
+    o[2] = o[0];
+    o[3] = o[1];
+    o[4] = make_uint4(bswap32(st[0]), bswap32(st[1]), bswap32(st[2]), bswap32(st[3]));
+    o[5] = make_uint4(bswap32(st[4]), bswap32(st[5]), bswap32(st[6]), bswap32(st[7]));
+    return;
+  }
+  const MsgShape sh = msg_shape(a.dlen, a.pmode != kPfxNone);
   sha256_init(st);
 #pragma unroll 1
   for (long b = 0; b < sh.nblk; b++) {

@@ -125,4 +125,72 @@ __device__ __forceinline__ void write_root(uint8_t* dst, const uint32_t (&mn)[8]
   }
 }
 
+// SHA-256 state of the leaf message 0x00 | P | share for a 512-B share at
+// `src` (16-B aligned), P = share[0:29] when q0 else the parity namespace.
+// ns receives share[0:29] (zero padded to 8 dwords) for the caller's tables.
+__device__ __forceinline__ void share_leaf_sha256(const uint4* src, bool q0, uint32_t (&st)[8],
+                                                  uint32_t (&ns)[8]) {
+  uint4 cur[8];
+  auto stage = [&](int sg) {
+#pragma unroll
+    for (int q = 0; q < 8; q++) cur[q] = src[8 * sg + q];
+  };
+  // one SHA block from 5 consecutive uint4 (dwords 16b-8 .. 16b+8 of the share)
+  auto mid_block = [&](const uint4& u0, const uint4& u1, const uint4& u2, const uint4& u3, const uint4& u4) {
+    const uint32_t d[20] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w, u2.x, u2.y,
+                            u2.z, u2.w, u3.x, u3.y, u3.z, u3.w, u4.x, u4.y, u4.z, u4.w};
+    uint32_t m[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) m[j] = __builtin_amdgcn_perm(d[j], d[j + 1], 0x06070001u);
+    sha256_compress(st, m);
+  };
+  sha256_init(st);
+  stage(0);
+  {  // block 0: 0x00 | P(29) | share[0:34]
+    uint32_t m[16];
+    const uint4 q0v = cur[0], q1v = cur[1], q2v = cur[2];
+    const uint32_t d[12] = {q0v.x, q0v.y, q0v.z, q0v.w, q1v.x, q1v.y,
+                            q1v.z, q1v.w, q2v.x, q2v.y, q2v.z, q2v.w};
+    if (q0) {
+      m[0] = __builtin_amdgcn_perm(d[0], d[0], (PZ << 24) | 0x000102u);
+#pragma unroll
+      for (int j = 1; j <= 6; j++) m[j] = __builtin_amdgcn_perm(d[j - 1], d[j], 0x07000102u);
+      m[7] = __builtin_amdgcn_perm(d[6], d[7], (0x0700u << 16) | (PZ << 8) | PZ);
+    } else {
+      m[0] = 0x00FFFFFFu;
+#pragma unroll
+      for (int j = 1; j <= 6; j++) m[j] = 0xFFFFFFFFu;
+      m[7] = 0xFFFF0000u;
+    }
+    m[7] |= __builtin_amdgcn_perm(d[0], d[0], (PZ << 24) | (PZ << 16) | 0x0001u);
+#pragma unroll
+    for (int j = 0; j < 7; j++) ns[j] = d[j];
+    ns[7] = d[7] & 0xFFu;
+#pragma unroll
+    for (int j = 8; j < 16; j++) m[j] = __builtin_amdgcn_perm(d[j - 8], d[j - 7], 0x06070001u);
+    sha256_compress(st, m);
+  }
+  mid_block(cur[2], cur[3], cur[4], cur[5], cur[6]);  // block 1
+  uint4 prev0 = cur[6], prev1 = cur[7];
+#pragma unroll 1
+  for (int s2 = 1; s2 <= 3; s2++) {  // blocks 2 s2 and 2 s2 + 1
+    stage(s2);
+    mid_block(prev0, prev1, cur[0], cur[1], cur[2]);
+    mid_block(cur[2], cur[3], cur[4], cur[5], cur[6]);
+    prev0 = cur[6];
+    prev1 = cur[7];
+  }
+  {  // block 8: share[482:512] | 0x80 | zeros | bit length
+    uint32_t m[16];
+    const uint32_t d[8] = {prev0.x, prev0.y, prev0.z, prev0.w, prev1.x, prev1.y, prev1.z, prev1.w};
+#pragma unroll
+    for (int j = 0; j < 7; j++) m[j] = __builtin_amdgcn_perm(d[j], d[j + 1], 0x06070001u);
+    m[7] = __builtin_amdgcn_perm(d[7], d[7], (0x0607u << 16) | (PZ << 8) | PZ) | 0x8000u;
+#pragma unroll
+    for (int j = 8; j < 15; j++) m[j] = 0u;
+    m[15] = 542u * 8u;
+    sha256_compress(st, m);
+  }
+}
+
 }  // namespace dagpu
