@@ -128,6 +128,7 @@ def main():
                     help="split stress square widths (k); also run after the headline when N > 1")
     ap.add_argument("--split-steps", type=int, default=3)
     ap.add_argument("--no-split", action="store_true", help="skip the split stress at N > 1")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end measurement")
     args = ap.parse_args()
     if args.mode == "split":
         return bench_split_main(args)
@@ -246,6 +247,11 @@ def main():
         "kernel_sum_ms_per_step": kernel_ms_step,
         "roofline": roof,
     }
+    if world == 1 and not args.no_e2e:
+        del ds
+        torch.cuda.empty_cache()
+        out["end_to_end"] = bench_e2e(ctx, local, k, np.stack([host[i % nd] for i in range(B)]),
+                                      max(4, args.steps))
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(k, args.cpu_seconds, args.cpu_threads)
         out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
@@ -260,6 +266,50 @@ def main():
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def bench_e2e(ctx, local, k, host_ods, steps):
+    """C2 end to end: ODS batches start in pinned host memory,
+    go up over PCIe, through the same device pipeline, and the roots + DAHs come
+    back (drop-in host mode without the EDS).  Two buffers on two streams so one
+    batch's copies overlap the other's kernels.  Not the headline `value`."""
+    from celestia_da.device import DeviceSquares
+
+    B = host_ods.shape[0]
+    pin = torch.from_numpy(host_ods).pin_memory()
+    w = 2 * k
+    bufs = []
+    for _ in range(2):
+        ds = DeviceSquares(k, B, device=local, ctx=ctx)
+        out = {"rr": torch.empty((B, w, 90), dtype=torch.uint8).pin_memory(),
+               "cr": torch.empty((B, w, 90), dtype=torch.uint8).pin_memory(),
+               "dah": torch.empty((B, 32), dtype=torch.uint8).pin_memory()}
+        bufs.append((ds, out, torch.cuda.Stream(device=local)))
+
+    def one(i):
+        ds, out, st = bufs[i % 2]
+        with torch.cuda.stream(st):
+            ds.ods.copy_(pin, non_blocking=True)
+            ds.extend(st)
+            out["rr"].copy_(ds.row_roots, non_blocking=True)
+            out["cr"].copy_(ds.col_roots, non_blocking=True)
+            out["dah"].copy_(ds.dah, non_blocking=True)
+
+    for i in range(2):
+        one(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        one(i)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ok = bool(torch.equal(bufs[0][1]["dah"], bufs[0][0].dah.cpu()))
+    del bufs
+    torch.cuda.empty_cache()
+    return {"squares_per_s": B * steps / el, "ms_per_batch": el / steps * 1e3, "batch": B,
+            "h2d_bytes_per_square": k * k * SHARE, "d2h_bytes_per_square": 2 * w * 90 + 32,
+            "dah_roundtrip_ok": ok,
+            "note": "pinned host ODS -> H2D -> extend -> D2H roots+DAH, 2 streams double-buffered"}
 
 
 def bench_split(dist, rank, world, local, ctx, k, steps, warmup):
