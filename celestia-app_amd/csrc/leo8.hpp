@@ -66,15 +66,5 @@ __device__ __forceinline__ void fft2(uint32_t& x, uint32_t& y, const int lm) {
   y ^= x;
 }
 
-// x = y * exp(log_m) with a RUNTIME log_m (decode multipliers): the four
-// table dwords come from constant memory (wave-uniform index -> scalar loads).
-__device__ __forceinline__ uint32_t gf8_mul_rt(uint32_t y, uint32_t lm) {
-  const uint32_t t0 = kGf8.t[0][lm], t1 = kGf8.t[1][lm], t2 = kGf8.t[2][lm], t3 = kGf8.t[3][lm];
-  const uint32_t p0 = __builtin_amdgcn_perm(t0, t0, y & 0x03030303u);
-  const uint32_t p1 = __builtin_amdgcn_perm(t1, t1, (y >> 2) & 0x03030303u);
-  const uint32_t p2 = __builtin_amdgcn_perm(t2, t2, (y >> 4) & 0x03030303u);
-  const uint32_t p3 = __builtin_amdgcn_perm(t3, t3, (y >> 6) & 0x03030303u);
-  return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(p0, p1, p2, 0x96), p3, 0u, 0x96);
-}
 
 }  // namespace dagpu

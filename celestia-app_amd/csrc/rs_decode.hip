@@ -13,11 +13,11 @@
 //        work[i] = present ? shard*errLocs[i] : 0
 //        IFFT_n (decoder skew: fftSkew[iend-1]) ; formal derivative ; FFT_n
 //        missing shard = work[pos] * (255 - errLocs[pos])
-// The transform runs register-resident exactly like the encoder.  For k = 128
-// (n = 256 elements per dword column) one workgroup splits the column over two
-// halves of 128 elements each (waves 0-1 / waves 2-3): only the last IFFT
-// layer, the derivative's middle step and the first FFT layer cross halves, and
-// those exchange values through LDS in 32-element chunks.
+// The transform runs register-resident exactly like the encoder: one thread
+// holds all n elements of its dword column for k <= 64, and for k = 128 four
+// waves share a column (leo8_decode128_kernel, layout transposes through LDS).
+// Runtime multiplies (error locators) read the 2-bit lookup tables from an LDS
+// copy with a wave-uniform index; presence comes from wave ballots.
 // MDS codes have a unique decoding, so any correct decoder is bit-exact; this
 // one is also step-for-step the reference algorithm.
 #include <hip/hip_runtime.h>
@@ -163,137 +163,73 @@ __device__ __forceinline__ void derivative_local(uint32_t (&w)[E]) {
 }
 
 template <int K>
-struct DecOcc { static constexpr int waves = K >= 64 ? 2 : (K >= 32 ? 4 : 8); };  // k=128 at 1 wave/SIMD (no spill) measured 30 % slower in C4
+struct DecOcc { static constexpr int waves = K >= 64 ? 2 : (K >= 32 ? 4 : 8); };
 
-// Whole decode of one dword column for half HH (compile-time) of H halves.
-// With H == 2 the two halves live in the same workgroup (waves 0-1: HH = 0,
-// waves 2-3: HH = 1) and meet at the same sequence of barriers.
-template <int K, int H, int HH>
-__device__ __forceinline__ void decode_half(const DecodeArgs& a, long v, int t, uint32_t col, bool active,
-                                            uint32_t (*xch)[32][128]) {
+__device__ __forceinline__ uint32_t gf8_mul_lds(uint32_t y, const uint4* tab, uint32_t lm);
+
+// Decode of one dword column for k <= 64 (n = 2k <= 128 elements per thread,
+// the whole transform register-resident).  Presence comes from wave ballots and
+// the error locators from one per-lane byte load + v_readlane (wave-uniform),
+// the runtime multiplies from the LDS copy of the lookup tables.
+template <int K>
+__device__ __forceinline__ void decode_small(const DecodeArgs& a, long v, int lane, uint32_t col, bool active,
+                                             const uint4* tab) {
   constexpr int N = 2 * K;
-  constexpr int E = N / H;
+  constexpr int NB = (N + 63) / 64;  // 64-element ballot words
   const long sq = v / a.nvec, vec = v % a.nvec;
   uint8_t* base = a.data + sq * a.sq_stride + vec * a.vec_stride;
   const auto rsrc = make_rsrc(base);
   const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
   const uint8_t* err = a.err + v * 256;
   const uint32_t ss = (uint32_t)a.shard_stride;
-
+  uint64_t pm[NB];
+  uint32_t e8[NB];
+#pragma unroll
+  for (int c = 0; c < NB; c++) {
+    const int i = 64 * c + lane;
+    const int sh = i < K ? K + i : i - K;
+    pm[c] = __ballot(i < N && pres[(long)(i < N ? sh : 0) * a.p_shard_stride] != 0);
+    e8[c] = i < N ? err[i] : 0u;
+  }
   // 1. work[i] = present ? shard * errLocs[i] : 0   ([parity K][data K])
-  uint32_t w[E];
+  uint32_t w[N];
 #pragma unroll
-  for (int j = 0; j < E; j++) {
-    const int i = HH * E + j;
-    const int s = i < K ? K + i : i - K;
-    const bool p = pres[(long)s * a.p_shard_stride] != 0;
+  for (int i = 0; i < N; i++) {
+    const int sh = i < K ? K + i : i - K;
+    const bool p = (pm[i >> 6] >> (i & 63)) & 1;
     uint32_t x = 0;
-    if (p && active) x = __builtin_amdgcn_raw_buffer_load_b32(rsrc, col, (uint32_t)s * ss, 0);
-    w[j] = p ? gf8_mul_rt(x, err[i]) : 0u;
+    if (p && active) x = __builtin_amdgcn_raw_buffer_load_b32(rsrc, col, (uint32_t)sh * ss, 0);
+    w[i] = p ? gf8_mul_lds(x, tab, __builtin_amdgcn_readlane(e8[i >> 6], i & 63)) : 0u;
   }
-
-  if constexpr (H == 1) {
-    ifft_dec_local<N, N, 0, 1>(w);
-    derivative_local<N>(w);
-    fft_dec_local<N, N, 0, N>(w);
-  } else {
-    static_assert(N == 256, "split decode is specialised for n = 256");
-    constexpr int D = N / 4;  // 64: last IFFT / first FFT radix-4 distance
-    constexpr int l01 = kGf8.skew[D - 1], l02 = kGf8.skew[2 * D - 1], l23 = kGf8.skew[3 * D - 1];
-    // ---- IFFT: local radix-4 layers (dist 1, 4, 16) ----
-    ifft_dec_local<N, E, HH * E, 1>(w);
-    // ---- last layer (dist = 64, one group): sub-layer 1 local ----
-#pragma unroll
-    for (int i = 0; i < D; i++) ifft2(w[i], w[i + D], HH == 0 ? l01 : l23);
-    // sub-layer 2 crosses halves: lower j <-> upper j
-#pragma unroll
-    for (int c = 0; c < E / 32; c++) {
-#pragma unroll
-      for (int q = 0; q < 32; q++) xch[HH][q][t] = w[32 * c + q];
-      __syncthreads();
-#pragma unroll
-      for (int q = 0; q < 32; q++) {
-        const uint32_t o = xch[1 - HH][q][t];
-        if constexpr (HH == 0) {  // x = mine, y = o: y' = y ^ x; x ^= y' * L
-          const uint32_t y2 = o ^ w[32 * c + q];
-          if (l02 != kGf8Mod) gf8_muladd(w[32 * c + q], y2, l02);
-        } else {                  // y = mine, x = o: y' = y ^ x
-          w[32 * c + q] ^= o;
-        }
-      }
-      __syncthreads();
-    }
-    // ---- formal derivative: lower local steps, lower ^= upper(pre-local), upper local ----
-    if constexpr (HH == 0) derivative_local<E>(w);
-#pragma unroll
-    for (int c = 0; c < E / 32; c++) {
-      if constexpr (HH == 1) {
-#pragma unroll
-        for (int q = 0; q < 32; q++) xch[1][q][t] = w[32 * c + q];
-      }
-      __syncthreads();
-      if constexpr (HH == 0) {
-#pragma unroll
-        for (int q = 0; q < 32; q++) w[32 * c + q] ^= xch[1][q][t];
-      }
-      __syncthreads();
-    }
-    if constexpr (HH == 1) derivative_local<E>(w);
-    // ---- FFT first layer (dist4 = 256, dist = 64): sub-layer 1 crosses ----
-#pragma unroll
-    for (int c = 0; c < E / 32; c++) {
-#pragma unroll
-      for (int q = 0; q < 32; q++) xch[HH][q][t] = w[32 * c + q];
-      __syncthreads();
-#pragma unroll
-      for (int q = 0; q < 32; q++) {
-        const uint32_t o = xch[1 - HH][q][t];
-        // x = lower, y = upper: x' = x ^ y*L; y' = y ^ x'  (both halves compute x')
-        uint32_t xx = HH == 0 ? w[32 * c + q] : o;
-        const uint32_t yy = HH == 0 ? o : w[32 * c + q];
-        if (l02 != kGf8Mod) gf8_muladd(xx, yy, l02);
-        w[32 * c + q] = HH == 0 ? xx : (yy ^ xx);
-      }
-      __syncthreads();
-    }
-    // sub-layer 2: (i, i+D) lower with l01, (i+2D, i+3D) upper with l23
-#pragma unroll
-    for (int i = 0; i < D; i++) fft2(w[i], w[i + D], HH == 0 ? l01 : l23);
-    // ---- remaining FFT layers (dist4 = 64, 16, 4) local ----
-    fft_dec_local<N, E, HH * E, E / 2>(w);
-  }
-
-  // 5. missing shard s: work[pos] * (255 - errLocs[pos]), pos = s >= K ? s-K : s+K
+  ifft_dec_local<N, N, 0, 1>(w);
+  derivative_local<N>(w);
+  fft_dec_local<N, N, 0, N>(w);
   if (!active) return;
 #pragma unroll
-  for (int j = 0; j < E; j++) {
-    const int pos = HH * E + j;
-    const int s = pos < K ? pos + K : pos - K;
-    if (pres[(long)s * a.p_shard_stride] == 0) {
-      const uint32_t y = gf8_mul_rt(w[j], 255u - err[pos]);
-      __builtin_amdgcn_raw_buffer_store_b32(y, rsrc, col, (uint32_t)s * ss, 0);
+  for (int pos = 0; pos < N; pos++) {  // missing shard = work[pos] * (255 - errLocs[pos])
+    const int sh = pos < K ? pos + K : pos - K;
+    if (((pm[pos >> 6] >> (pos & 63)) & 1) == 0) {
+      const uint32_t y = gf8_mul_lds(w[pos], tab, 255u - __builtin_amdgcn_readlane(e8[pos >> 6], pos & 63));
+      __builtin_amdgcn_raw_buffer_store_b32(y, rsrc, col, (uint32_t)sh * ss, 0);
     }
   }
 }
 
-template <int K, int H>
-__global__ __launch_bounds__(128 * H)
+// One block = 2 waves x 64 dword columns = 512 B of one vector.
+template <int K>
+__global__ __launch_bounds__(128)
 __attribute__((amdgpu_waves_per_eu(DecOcc<K>::waves, 8))) void leo8_decode_kernel(DecodeArgs a) {
   const long blk = blockIdx.x;
   const int chunk = (int)(blk % a.nchunk);
   const long v = blk / a.nchunk;  // flattened (square, vector)
   if (a.flags[v] == 0) return;   // uniform: nothing to decode for this vector
-  const int t = threadIdx.x & 127;
+  __shared__ uint4 tab[256];
+  for (int i = threadIdx.x; i < 256; i += 128)
+    tab[i] = make_uint4(kGf8.t[0][i], kGf8.t[1][i], kGf8.t[2][i], kGf8.t[3][i]);
+  __syncthreads();
+  const int t = threadIdx.x;
   const uint32_t col = (uint32_t)chunk * 512u + (uint32_t)t * 4u;
-  const bool active = col < (uint32_t)a.shard_bytes;
-  if constexpr (H == 1) {
-    decode_half<K, 1, 0>(a, v, t, col, active, nullptr);
-  } else {
-    __shared__ uint32_t xch[2][32][128];
-    const int h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 7);  // wave-uniform
-    if (h == 0) decode_half<K, H, 0>(a, v, t, col, active, xch);
-    else decode_half<K, H, 1>(a, v, t, col, active, xch);
-  }
+  decode_small<K>(a, v, t & 63, col, col < (uint32_t)a.shard_bytes, tab);
 }
 
 // ---------------------------------------------------------------------------
@@ -476,10 +412,10 @@ __global__ __launch_bounds__(256) void mark_present_kernel(DecodeArgs a) {
   if (threadIdx.x == 0 && a.progress) atomicAdd(a.progress, 1);
 }
 
-template <int K, int H>
+template <int K>
 static hipError_t launch_dec(const DecodeArgs& a, hipStream_t s) {
   const long blocks = a.nsq * a.nvec * a.nchunk;
-  hipLaunchKernelGGL((leo8_decode_kernel<K, H>), dim3((unsigned)blocks), dim3(128 * H), 0, s, a);
+  hipLaunchKernelGGL((leo8_decode_kernel<K>), dim3((unsigned)blocks), dim3(128), 0, s, a);
   return hipGetLastError();
 }
 
@@ -495,21 +431,17 @@ hipError_t launch_leo8_decode_only(const DecodeArgs& a, hipStream_t s, bool mark
   if (nv <= 0) return hipSuccess;
   hipError_t e = hipSuccess;
   switch (a.k) {
-    case 1: e = launch_dec<1, 1>(a, s); break;
-    case 2: e = launch_dec<2, 1>(a, s); break;
-    case 4: e = launch_dec<4, 1>(a, s); break;
-    case 8: e = launch_dec<8, 1>(a, s); break;
-    case 16: e = launch_dec<16, 1>(a, s); break;
-    case 32: e = launch_dec<32, 1>(a, s); break;
-    case 64: e = launch_dec<64, 1>(a, s); break;
+    case 1: e = launch_dec<1>(a, s); break;
+    case 2: e = launch_dec<2>(a, s); break;
+    case 4: e = launch_dec<4>(a, s); break;
+    case 8: e = launch_dec<8>(a, s); break;
+    case 16: e = launch_dec<16>(a, s); break;
+    case 32: e = launch_dec<32>(a, s); break;
+    case 64: e = launch_dec<64>(a, s); break;
     case 128: {
-#ifdef DAGPU_DEC128_H2
-      e = launch_dec<128, 2>(a, s);
-#else
       const long nc = (a.shard_bytes + 255) / 256;
       hipLaunchKernelGGL(leo8_decode128_kernel, dim3((unsigned)(nv * nc)), dim3(kD4Threads), 0, s, a, (int)nc);
       e = hipGetLastError();
-#endif
       break;
     }
     default: return hipErrorInvalidValue;
