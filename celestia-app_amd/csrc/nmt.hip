@@ -229,7 +229,7 @@ __global__ __launch_bounds__(256) void nmt_level_kernel(SquareArgs a, const uint
 // Kernel 3: DAH = RFC-6962 root over rowRoots || colRoots (2w items of 90 B).
 // leaf = SHA256(0x00 | root) (91 B, 2 blocks); inner = SHA256(0x01 | l | r).
 // ---------------------------------------------------------------------------
-constexpr int kDahThreads = 256;
+constexpr int kDahThreads = 1024;  // one lane per leaf up to k = 256
 
 __global__ __launch_bounds__(kDahThreads) void dah_kernel(SquareArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];  // (n + n/2) * 8 dwords
