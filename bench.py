@@ -129,6 +129,8 @@ def main():
     ap.add_argument("--split-steps", type=int, default=3)
     ap.add_argument("--no-split", action="store_true", help="skip the split stress at N > 1")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end measurement")
+    ap.add_argument("--replay-blocks", type=int, default=8192, help="configs[4] block replay length")
+    ap.add_argument("--no-replay", action="store_true", help="skip the block replay measurement")
     args = ap.parse_args()
     if args.mode == "split":
         return bench_split_main(args)
@@ -247,6 +249,8 @@ def main():
         "kernel_sum_ms_per_step": kernel_ms_step,
         "roofline": roof,
     }
+    if not args.no_replay:
+        out["block_replay"] = bench_replay(dist, rank, world, local, ctx, ds, args.replay_blocks)
     if world == 1 and not args.no_e2e:
         del ds
         torch.cuda.empty_cache()
@@ -310,6 +314,51 @@ def bench_e2e(ctx, local, k, host_ods, steps):
             "h2d_bytes_per_square": k * k * SHARE, "d2h_bytes_per_square": 2 * w * 90 + 32,
             "dah_roundtrip_ok": ok,
             "note": "pinned host ODS -> H2D -> extend -> D2H roots+DAH, 2 streams double-buffered"}
+
+
+def bench_replay(dist, rank, world, local, ctx, ds, n_blocks):
+    """configs[4] block replay: n_blocks consecutive k x k squares, contiguous
+    shards per rank (celestia_da.replay.shard_range), processed in batches of
+    the resident `ds` (its 64 distinct squares stand for the blocks, cycled), every
+    DAH gathered to all ranks and checked against the batch's own DAHs.  Timed
+    from the first batch to the gathered DAHs, max over ranks."""
+    from celestia_da import replay
+
+    B = ds.n
+    mine = replay.shard_range(n_blocks, rank, world)
+    per_rank = (n_blocks + world - 1) // world
+    out = torch.zeros((per_rank, 32), dtype=torch.uint8, device=ds.dah.device)
+    ds.extend()
+    torch.cuda.synchronize()
+    ref = ds.dah.clone()
+    barrier(dist)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    done = 0
+    while done < len(mine):
+        m = min(B, len(mine) - done)
+        ds.extend()
+        out[done:done + m].copy_(ds.dah[:m], non_blocking=True)
+        done += m
+    if dist is not None:
+        allg = torch.empty((world * per_rank, 32), dtype=torch.uint8, device=out.device)
+        dist.all_gather_into_tensor(allg, out)
+    else:
+        allg = out
+    torch.cuda.synchronize()
+    barrier(dist)
+    el = max_over_ranks(dist, time.perf_counter() - t0, local)
+    # block i of rank r's shard is batch slot (i % B) of that rank's squares
+    ok = True
+    for r in range(world):
+        n_r = len(replay.shard_range(n_blocks, r, world))
+        got = allg[r * per_rank:r * per_rank + n_r].cpu()
+        if r == rank:
+            want = ref.cpu()[torch.arange(n_r) % B]
+            ok = ok and bool(torch.equal(got, want))
+    return {"blocks": n_blocks, "squares_per_s": n_blocks / el, "seconds": el, "per_rank": per_rank,
+            "dah_gather_ok": ok, "note": "contiguous shards, 64 distinct resident squares cycled per rank, "
+                                        "all DAHs all-gathered"}
 
 
 def bench_split(dist, rank, world, local, ctx, k, steps, warmup):
