@@ -29,6 +29,9 @@ import torch  # noqa: E402
 SHARE = 512
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 VALU_PEAK_TOPS = 78.64         # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz int32 ops/s (/1e12)
+# measured SHA-256 compression ceiling of this chip (tools/valu_bench, profiles/valu_bench_r01.log):
+# 28.6 G compressions/s = 39.6 T int32 ops/s; VOP3 forms issue at ~1 wave-instr/clk/CU, not 2
+VALU_MEASURED_TOPS = 39.6
 # Minimal CDNA4 int32 ops per SHA-256 compression with v_alignbit rotates,
 # v_bitop3 (xor3/ch/maj) and v_add3: 64 rounds x 14 + 48 schedule words x 10 + 8.
 OPS_PER_COMPRESSION = 64 * 14 + 48 * 10 + 8
@@ -218,7 +221,8 @@ def main():
         ach = comp * OPS_PER_COMPRESSION / (per[dom] * 1e-3) / 1e12
         roof = {"kernel": dom, "bound": "valu", "achieved": ach, "peak": VALU_PEAK_TOPS,
                 "unit": "Tint32op/s", "frac": ach / VALU_PEAK_TOPS,
-                "work": f"{comp} SHA-256 compressions x {OPS_PER_COMPRESSION} int32 ops"}
+                "work": f"{comp} SHA-256 compressions x {OPS_PER_COMPRESSION} int32 ops",
+                "measured_ceiling": VALU_MEASURED_TOPS, "frac_of_measured": ach / VALU_MEASURED_TOPS}
     roof["traffic"] = load_traffic(dom)
     roof["avg_launch_ms"] = per[dom]
 
