@@ -35,6 +35,10 @@ EXPORTS = (
     "dagpu_init",
     "dagpu_destroy",
     "dagpu_last_error",
+    "dagpu_host_alloc",
+    "dagpu_host_free",
+    "dagpu_host_register",
+    "dagpu_host_unregister",
     "dagpu_extend_shares",
     "dagpu_extend_batch",
     "dagpu_workspace_size",
@@ -103,6 +107,12 @@ def lib() -> ctypes.CDLL:
         L.dagpu_destroy.restype = None
         L.dagpu_last_error.argtypes = [vp]
         L.dagpu_last_error.restype = ctypes.c_char_p
+        L.dagpu_host_alloc.argtypes = [sz]
+        L.dagpu_host_alloc.restype = vp
+        L.dagpu_host_free.argtypes = [vp]
+        L.dagpu_host_free.restype = None
+        L.dagpu_host_register.argtypes = [vp, sz]
+        L.dagpu_host_unregister.argtypes = [vp]
         L.dagpu_extend_shares.argtypes = [vp, vp, sz, sz, vp, vp, vp, vp]
         L.dagpu_extend_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
         L.dagpu_workspace_size.argtypes = [ctypes.c_uint32, sz]

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <cmath>
@@ -119,12 +120,110 @@ int enqueue_roots(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_eds, ui
   return DAGPU_OK;
 }
 
+// Squares per pipeline chunk: about 128 MiB of ODS per host->device copy.
+// DAGPU_PIPELINE_CHUNK (squares) overrides it, e.g. to exercise many chunks in tests.
+size_t pipeline_chunk(uint32_t k, size_t n) {
+  size_t m = (size_t(128) << 20) / ods_bytes(k);
+  if (const char* e = getenv("DAGPU_PIPELINE_CHUNK")) {
+    const long v = atol(e);
+    if (v > 0) m = (size_t)v;
+  }
+  return m < 1 ? 1 : (m > n ? n : m);
+}
+
+int finish_status(dagpu_ctx* ctx, const int32_t* st, size_t n, int32_t* status) {
+  int first = DAGPU_OK;
+  for (size_t i = 0; i < n; i++) {
+    int v = (st[i] & kStatusPushOrder) ? DAGPU_ERR_PUSH_ORDER : DAGPU_OK;
+    if (status) status[i] = v;
+    if (v && !first) first = v;
+  }
+  if (first) set_err(ctx, first, "invalid push order: namespaces of original data square are not sorted");
+  return first;
+}
+
+// Host-mode batch of >= 2 chunks: chunk c's ODS goes up on copy_stream while
+// chunk c-1 is extended on ctx->stream; roots, DAHs and status come back into
+// page-locked staging per slot and are copied to the caller's arrays once the
+// slot's event fires (the caller's buffers may be pageable Go memory, whose
+// device->host copies would otherwise block this thread and the pipeline).
+// An EDS requested back is copied straight into eds_out.  Caller holds ctx->mu.
+int run_group_pipelined(dagpu_ctx* ctx, uint32_t k, size_t n, size_t m, const uint8_t* ods,
+                        uint8_t* eds_out, uint8_t* rr, uint8_t* cr, uint8_t* dah, int32_t* status) {
+  const size_t w = 2 * (size_t)k;
+  const size_t rb = w * kNodeSize, ob = ods_bytes(k), eb = eds_bytes(k);
+  const size_t wsb = dagpu_workspace_size(k, m);
+  hipStream_t s = ctx->stream, cs = ctx->copy_stream;
+  HIP_TRY(ctx, ctx->ods.ensure(2 * m * ob));
+  HIP_TRY(ctx, ctx->eds.ensure(2 * m * eb));
+  HIP_TRY(ctx, ctx->rr.ensure(2 * m * rb));
+  HIP_TRY(ctx, ctx->cr.ensure(2 * m * rb));
+  HIP_TRY(ctx, ctx->dah.ensure(2 * m * 32));
+  HIP_TRY(ctx, ctx->status.ensure(2 * m * sizeof(int32_t)));
+  HIP_TRY(ctx, ctx->ws.ensure(2 * wsb));
+  const size_t hslot = m * (2 * rb + 32 + sizeof(int32_t));
+  HIP_TRY(ctx, ctx->h_out.ensure(2 * hslot));
+  std::vector<int32_t> st(n);
+  const size_t nchunks = (n + m - 1) / m;
+  auto slot_dev = [&](DevBuf& b, size_t per, int slot) { return (uint8_t*)b.p + slot * m * per; };
+  auto slot_host = [&](int slot) { return (uint8_t*)ctx->h_out.p + slot * hslot; };
+  // copy chunk c's outputs from its slot's staging to the caller (slot's event done)
+  auto drain = [&](size_t c) -> int {
+    const int slot = (int)(c & 1);
+    const size_t off = c * m, cnt = (n - off < m) ? n - off : m;
+    HIP_TRY(ctx, hipEventSynchronize(ctx->ev_done[slot]));
+    const uint8_t* h = slot_host(slot);
+    memcpy(rr + off * rb, h, cnt * rb);
+    memcpy(cr + off * rb, h + m * rb, cnt * rb);
+    memcpy(dah + off * 32, h + 2 * m * rb, cnt * 32);
+    memcpy(st.data() + off, h + 2 * m * rb + m * 32, cnt * sizeof(int32_t));
+    return DAGPU_OK;
+  };
+  for (size_t c = 0; c < nchunks; c++) {
+    const int slot = (int)(c & 1);
+    const size_t off = c * m, cnt = (n - off < m) ? n - off : m;
+    if (c >= 2) {  // the slot's previous chunk must be drained before reuse
+      int rc = drain(c - 2);
+      if (rc) return rc;
+      HIP_TRY(ctx, hipStreamWaitEvent(cs, ctx->ev_done[slot], 0));
+    }
+    uint8_t* d_ods = slot_dev(ctx->ods, ob, slot);
+    uint8_t* d_eds = slot_dev(ctx->eds, eb, slot);
+    uint8_t* d_rr = slot_dev(ctx->rr, rb, slot);
+    uint8_t* d_cr = slot_dev(ctx->cr, rb, slot);
+    uint8_t* d_dah = slot_dev(ctx->dah, 32, slot);
+    int32_t* d_st = (int32_t*)slot_dev(ctx->status, sizeof(int32_t), slot);
+    HIP_TRY(ctx, hipMemcpyAsync(d_ods, ods + off * ob, cnt * ob, hipMemcpyHostToDevice, cs));
+    HIP_TRY(ctx, hipEventRecord(ctx->ev_loaded[slot], cs));
+    HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->ev_loaded[slot], 0));
+    int rc = enqueue_rs(ctx, k, cnt, d_ods, d_eds, s);
+    if (rc) return rc;
+    rc = enqueue_roots(ctx, k, cnt, d_eds, d_rr, d_cr, d_dah, d_st, (uint8_t*)ctx->ws.p + slot * wsb, s);
+    if (rc) return rc;
+    if (eds_out)
+      HIP_TRY(ctx, hipMemcpyAsync(eds_out + off * eb, d_eds, cnt * eb, hipMemcpyDeviceToHost, s));
+    uint8_t* h = slot_host(slot);
+    HIP_TRY(ctx, hipMemcpyAsync(h, d_rr, cnt * rb, hipMemcpyDeviceToHost, s));
+    HIP_TRY(ctx, hipMemcpyAsync(h + m * rb, d_cr, cnt * rb, hipMemcpyDeviceToHost, s));
+    HIP_TRY(ctx, hipMemcpyAsync(h + 2 * m * rb, d_dah, cnt * 32, hipMemcpyDeviceToHost, s));
+    HIP_TRY(ctx, hipMemcpyAsync(h + 2 * m * rb + m * 32, d_st, cnt * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(ctx, hipEventRecord(ctx->ev_done[slot], s));
+  }
+  for (size_t c = nchunks >= 2 ? nchunks - 2 : 0; c < nchunks; c++) {
+    int rc = drain(c);
+    if (rc) return rc;
+  }
+  return finish_status(ctx, st.data(), n, status);
+}
+
 // Runs one uniform-k group from host memory.  Caller holds ctx->mu.
 int run_group_host(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* ods, uint8_t* eds_out,
                    uint8_t* rr, uint8_t* cr, uint8_t* dah, int32_t* status) {
   int rc = check_k(ctx, k);
   if (rc) return rc;
   const size_t w = 2 * (size_t)k;
+  const size_t m = pipeline_chunk(k, n);
+  if (n > m) return run_group_pipelined(ctx, k, n, m, ods, eds_out, rr, cr, dah, status);
   hipStream_t s = ctx->stream;
   HIP_TRY(ctx, ctx->ods.ensure(ods_bytes(k) * n));
   HIP_TRY(ctx, ctx->eds.ensure(eds_bytes(k) * n));
@@ -149,14 +248,7 @@ int run_group_host(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* ods, uin
   HIP_TRY(ctx, hipMemcpyAsync(st.data(), ctx->status.p, sizeof(int32_t) * n,
                               hipMemcpyDeviceToHost, s));
   HIP_TRY(ctx, hipStreamSynchronize(s));
-  int first = DAGPU_OK;
-  for (size_t i = 0; i < n; i++) {
-    int v = (st[i] & kStatusPushOrder) ? DAGPU_ERR_PUSH_ORDER : DAGPU_OK;
-    if (status) status[i] = v;
-    if (v && !first) first = v;
-  }
-  if (first) set_err(ctx, first, "invalid push order: namespaces of original data square are not sorted");
-  return first;
+  return finish_status(ctx, st.data(), n, status);
 }
 
 }  // namespace
@@ -174,8 +266,13 @@ int dagpu_init(int device, dagpu_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return DAGPU_ERR_DEVICE;
   dagpu_ctx* c = new dagpu_ctx();
   c->device = device;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete c;
+  bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) == hipSuccess;
+  for (int i = 0; ok && i < 2; i++)
+    ok = hipEventCreateWithFlags(&c->ev_loaded[i], hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&c->ev_done[i], hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    dagpu_destroy(c);
     return DAGPU_ERR_DEVICE;
   }
   *out = c;
@@ -185,15 +282,41 @@ int dagpu_init(int device, dagpu_ctx** out) {
 void dagpu_destroy(dagpu_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  (void)hipStreamSynchronize(c->stream);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+  c->h_out.release();
   c->ods.release(); c->eds.release(); c->rr.release(); c->cr.release();
   c->dah.release(); c->status.release(); c->ws.release();
   for (DevBuf* b : {&c->t_leaf_data, &c->t_leaves, &c->t_inner, &c->t_meta, &c->t_out, &c->t_status, &c->t_flags})
     b->release();
   for (auto& r : c->pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
   for (auto e : c->pool) (void)hipEventDestroy(e);
-  (void)hipStreamDestroy(c->stream);
+  for (int i = 0; i < 2; i++) {
+    if (c->ev_loaded[i]) (void)hipEventDestroy(c->ev_loaded[i]);
+    if (c->ev_done[i]) (void)hipEventDestroy(c->ev_done[i]);
+  }
+  if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
+}
+
+void* dagpu_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  return hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) == hipSuccess ? p : nullptr;
+}
+
+void dagpu_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
+int dagpu_host_register(void* p, size_t bytes) {
+  if (!p || !bytes) return DAGPU_ERR_ARG;
+  return hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess ? DAGPU_OK : DAGPU_ERR_DEVICE;
+}
+
+int dagpu_host_unregister(void* p) {
+  if (!p) return DAGPU_ERR_ARG;
+  return hipHostUnregister(p) == hipSuccess ? DAGPU_OK : DAGPU_ERR_DEVICE;
 }
 
 const char* dagpu_last_error(dagpu_ctx* c) { return c ? c->err.c_str() : "null context"; }

@@ -34,6 +34,26 @@ struct DevBuf {
   }
 };
 
+// Page-locked host staging (hipHostMalloc), grown on demand.
+struct HostBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= n) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    if (e == hipSuccess) n = bytes;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
 struct ProfRec {
   int id;
   hipEvent_t a, b;
@@ -45,6 +65,11 @@ struct dagpu_ctx {
   std::mutex mu;
   std::string err;
   DevBuf ods, eds, rr, cr, dah, status, ws;
+  // host-mode pipeline (dagpu.cpp run_group_pipelined): H2D on copy_stream,
+  // kernels + D2H on stream, two slots handed over with events
+  hipStream_t copy_stream = nullptr;
+  hipEvent_t ev_loaded[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
+  HostBuf h_out;
   // generic forests / commitments / split square (trees.cpp, split.cpp)
   DevBuf t_leaf_data, t_leaves, t_inner, t_meta, t_out, t_status, t_flags;
   // profiling

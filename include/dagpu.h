@@ -73,10 +73,21 @@ int dagpu_extend_shares(dagpu_ctx* ctx, const uint8_t* shares, size_t n_shares,
 
 /* Batched host-memory form (app/extend_block.go:14-22 block replay; mixed k).
  * k[i] = original square width of square i.  status[i] gets a dagpu_status.
- * Returns DAGPU_OK if every square succeeded, else the first failing status. */
+ * Returns DAGPU_OK if every square succeeded, else the first failing status.
+ * A run of equal k larger than ~128 MiB of ODS is pipelined: chunk c goes up
+ * on a copy stream while chunk c-1 is extended.  Host->device copies run at
+ * PCIe speed only from page-locked memory: allocate `ods` with
+ * dagpu_host_alloc or pin it with dagpu_host_register. */
 int dagpu_extend_batch(dagpu_ctx* ctx, const uint8_t* ods, const uint32_t* k, size_t n,
                        uint8_t* eds_or_null, uint8_t* row_roots, uint8_t* col_roots,
                        uint8_t* dah, int32_t* status);
+
+/* Page-locked host memory for dagpu_extend_batch inputs (hipHostMalloc /
+ * hipHostRegister).  dagpu_host_alloc returns NULL on failure. */
+void* dagpu_host_alloc(size_t bytes);
+void dagpu_host_free(void* p);
+int dagpu_host_register(void* p, size_t bytes);
+int dagpu_host_unregister(void* p);
 
 /* Device-resident batch, one k for all n squares; every pointer is device
  * memory; work is enqueued on `stream` (hipStream_t, NULL = default stream) and
