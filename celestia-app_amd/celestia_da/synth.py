@@ -32,9 +32,13 @@ def random_blob_square(k: int, seed: int) -> np.ndarray:
 
 def sort_shares(s: np.ndarray) -> np.ndarray:
     """Bytewise lexicographic sort of rows (bytes.Compare order)."""
-    # big-endian 64-bit words compare like the bytes they hold
+    # big-endian 64-bit words compare like the bytes they hold; the first 8
+    # words (64 bytes) decide unless two rows share them, then sort on all
     words = s.view(">u8")
-    order = np.lexsort(words.T[::-1])
+    order = np.lexsort(words[:, :8].T[::-1])
+    w8 = words[order, :8]
+    if (w8[1:] == w8[:-1]).all(axis=1).any():
+        order = np.lexsort(words.T[::-1])
     return np.ascontiguousarray(s[order])
 
 
