@@ -348,8 +348,8 @@ def bench_replay(dist, rank, world, local, ctx, ds, n_blocks):
             want = ref.cpu()[torch.arange(n_r) % B]
             ok = ok and bool(torch.equal(got, want))
     return {"blocks": n_blocks, "squares_per_s": n_blocks / el, "seconds": el, "per_rank": per_rank,
-            "dah_gather_ok": ok, "note": "contiguous shards, 64 distinct resident squares cycled per rank, "
-                                        "all DAHs all-gathered"}
+            "dah_gather_ok": ok, "note": f"contiguous shards, {B} distinct resident squares cycled per rank, "
+                                         "all DAHs all-gathered"}
 
 
 def bench_split(dist, rank, world, local, ctx, k, steps, warmup):
