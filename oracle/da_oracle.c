@@ -74,7 +74,7 @@ void orc_sha256(const uint8_t* msg, size_t len, uint8_t out[32]) {
   uint8_t tail[128];
   size_t rem = len - i;
   memset(tail, 0, sizeof tail);
-  memcpy(tail, msg + i, rem);
+  if (rem) memcpy(tail, msg + i, rem);  /* msg may be NULL when len == 0 */
   tail[rem] = 0x80;
   size_t tl = (rem + 9 <= 64) ? 64 : 128;
   uint64_t bits = (uint64_t)len * 8;

@@ -66,7 +66,8 @@ const uint16_t* orc_gf16_skew(void); /* 65535 */
 
 /* Systematic Leopard encode: k data shards (contiguous, k*shard bytes) ->
  * k parity shards.  GF(2^8) when 2k <= 256 else GF(2^16) (reedsolomon.New(k,k,
- * WithLeopardGF(true))).  shard must be a multiple of 64. */
+ * WithLeopardGF(true))).  k a power of two (the widths rsmt2d uses); shard
+ * must be a multiple of 64. */
 int orc_encode(int k, size_t shard, const uint8_t* data, uint8_t* parity);
 
 /* Leopard reconstruct (reedsolomon Reconstruct): shards is 2k*shard bytes,

@@ -14,9 +14,12 @@ CLIENT = os.path.join(os.path.dirname(__file__), "c_abi", "dagpu_c_client")
 REF = json.load(open(os.path.join(GOLDEN, "squares.json")))["reference"]
 
 
-def _run():
-    assert os.path.exists(CLIENT), "build the client first: make -C celestia-app_amd c_client"
-    p = subprocess.run([CLIENT], capture_output=True, text=True, timeout=120)
+CLIENT_ASAN = CLIENT + "_asan"
+
+
+def _run(client=CLIENT, env=None):
+    assert os.path.exists(client), "build the client first: make -C celestia-app_amd c_client"
+    p = subprocess.run([client], capture_output=True, text=True, timeout=300, env=env)
     return p.returncode, dict(line.split(" ", 1) for line in p.stdout.splitlines() if " " in line), p
 
 
@@ -29,9 +32,7 @@ def test_c_client_links_and_reports_device_errors_on_cpu():
     assert rc == 1 and out.get("init") == "-10", p.stdout + p.stderr
 
 
-@pytest.mark.gpu
-def test_c_client_golden_and_errors():
-    rc, out, p = _run()
+def _check_golden(rc, out, p):
     assert rc == 0, p.stdout + p.stderr
     assert out["init"] == "0" and p.stdout.strip().endswith("done")
     assert out["min_rc"] == "0" and out["min_dah"] == REF["min_dah"]["hash"]
@@ -46,3 +47,20 @@ def test_c_client_golden_and_errors():
     assert out["err_push_order"] == "-4"
     assert out["codec_zero"] == "0 1"
     assert out["threads_ok"] == "1"
+    assert out["pipelined"] == "-4 -4 1 1 -4"  # push-order status of square 21 only, same as unchunked
+
+
+@pytest.mark.gpu
+def test_c_client_golden_and_errors():
+    _check_golden(*_run())
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(CLIENT_ASAN), reason="host-ASan build absent (make -C celestia-app_amd asan)")
+def test_c_client_under_host_asan():
+    """Same calls with the library's host code (plans, staging, pipelined
+    batches, threads) built with AddressSanitizer; device code unchanged."""
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0", DAGPU_CLIENT_QUICK_EXIT="1")
+    rc, out, p = _run(CLIENT_ASAN, env)
+    assert "ERROR: AddressSanitizer" not in p.stderr, p.stderr[-4000:]
+    _check_golden(rc, out, p)
