@@ -28,6 +28,7 @@ ERR_BAD_ROOTS = -8
 ERR_ARG = -9
 ERR_DEVICE = -10
 ERR_UNSUPPORTED = -11
+ERR_PROOF = -12
 
 # Every symbol include/dagpu.h declares (checked by tests/test_abi_cpu.py).
 EXPORTS = (
@@ -35,6 +36,8 @@ EXPORTS = (
     "dagpu_init",
     "dagpu_destroy",
     "dagpu_last_error",
+    "dagpu_nmt_verify_inclusion",
+    "dagpu_merkle_verify",
     "dagpu_host_alloc",
     "dagpu_host_free",
     "dagpu_host_register",
@@ -107,6 +110,9 @@ def lib() -> ctypes.CDLL:
         L.dagpu_destroy.restype = None
         L.dagpu_last_error.argtypes = [vp]
         L.dagpu_last_error.restype = ctypes.c_char_p
+        i64 = ctypes.c_int64
+        L.dagpu_nmt_verify_inclusion.argtypes = [vp, vp, sz, sz, i64, i64, vp, sz, vp]
+        L.dagpu_merkle_verify.argtypes = [vp, vp, sz, i64, i64, vp, sz]
         L.dagpu_host_alloc.argtypes = [sz]
         L.dagpu_host_alloc.restype = vp
         L.dagpu_host_free.argtypes = [vp]

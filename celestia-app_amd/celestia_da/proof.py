@@ -1,8 +1,13 @@
 """Share inclusion proofs, host-side mirror of
 
   proof.NewShareInclusionProof      pkg/proof/proof.go:58-165
+  proof.NewTxInclusionProof         pkg/proof/proof.go:23-54 (square built by celestia_da.square)
+  proof.ParseNamespace              pkg/proof/querier.go:123-151
   merkle.ProofsFromByteSlices       celestia-core crypto/merkle (used at proof.go:87)
   nmt ProveRange                    nmt v0.20.0 (used at proof.go:139 via the wrapper tree)
+  verification: ShareProof.Validate / VerifyProof, RowProof.Validate (celestia-core
+  types/share_proof.go, row_proof.go), merkle Proof.Verify, nmt Proof.VerifyInclusion
+  -> dagpu_merkle_verify / dagpu_nmt_verify_inclusion (host code of the library)
 
 The square is extended and hashed on the GPU, every row-tree node stays in HBM
 (dagpu_row_nodes_device) and the RFC-6962 tree over rowRoots||colRoots is
@@ -40,6 +45,24 @@ class MerkleProof:
     leaf_hash: bytes
     aunts: List[bytes]
 
+    def verify(self, root: bytes, leaf: bytes) -> None:
+        """merkle Proof.Verify: raises DAError when the proof does not prove
+        `leaf` under `root`."""
+        if root is None:
+            raise DAError(_abi.ERR_ARG, "invalid root hash: cannot be nil")
+        if self.total < 0:
+            raise DAError(_abi.ERR_PROOF, "proof total must be positive")
+        if self.index < 0:
+            raise DAError(_abi.ERR_PROOF, "proof index cannot be negative")
+        # keep every buffer referenced until the call returns (addr() is a raw pointer)
+        r, lf, au = _bytes(root), _bytes(leaf), _bytes(b"".join(self.aunts))
+        rc = _abi.lib().dagpu_merkle_verify(_abi.addr(r), _abi.addr(lf), len(leaf), self.index, self.total,
+                                            _abi.addr(au), len(self.aunts))
+        if rc == _abi.ERR_PROOF:
+            raise DAError(rc, "invalid root hash")
+        if rc:
+            raise DAError(rc, "malformed merkle proof")
+
 
 @dataclass
 class NMTProof:
@@ -49,6 +72,19 @@ class NMTProof:
     nodes: List[bytes]
     leaf_hash: bytes = b""
 
+    def verify_inclusion(self, namespace: bytes, leaves: Sequence[bytes], root: bytes) -> bool:
+        """nmt Proof.VerifyInclusion (IgnoreMaxNamespace): `leaves` are the raw
+        shares (the tree prepends `namespace` to each)."""
+        if len(namespace) != 29 or len(root) != 90 or any(len(n) != 90 for n in self.nodes):
+            return False
+        ln = len(leaves[0]) if leaves else 0
+        if any(len(x) != ln for x in leaves):
+            return False
+        nsb, lv, nd, rt = _bytes(namespace), _bytes(b"".join(leaves)), _bytes(b"".join(self.nodes)), _bytes(root)
+        rc = _abi.lib().dagpu_nmt_verify_inclusion(_abi.addr(nsb), _abi.addr(lv), len(leaves), ln, self.start,
+                                                   self.end, _abi.addr(nd), len(self.nodes), _abi.addr(rt))
+        return rc == 0
+
 
 @dataclass
 class RowProof:
@@ -56,6 +92,18 @@ class RowProof:
     proofs: List[MerkleProof]
     start_row: int
     end_row: int
+
+    def validate(self, root: bytes) -> None:
+        """RowProof.Validate: every row root is proven under the data root."""
+        if self.end_row - self.start_row + 1 != len(self.row_roots):
+            raise DAError(_abi.ERR_PROOF, "the number of rows is different than the number of row roots")
+        if len(self.proofs) != len(self.row_roots):
+            raise DAError(_abi.ERR_PROOF, "the number of proofs is different than the number of row roots")
+        for p, r in zip(self.proofs, self.row_roots):
+            try:
+                p.verify(root, r)
+            except DAError:
+                raise DAError(_abi.ERR_PROOF, "row proof failed to verify") from None
 
 
 @dataclass
@@ -65,6 +113,42 @@ class ShareProof:
     namespace_id: bytes
     row_proof: RowProof
     namespace_version: int
+
+    def verify_proof(self) -> bool:
+        """ShareProof.VerifyProof: each row's shares under its row root."""
+        if self.namespace_version > 255:
+            return False
+        ns = bytes([self.namespace_version]) + self.namespace_id
+        cursor = 0
+        for i, p in enumerate(self.share_proofs):
+            used = p.end - p.start
+            if not p.verify_inclusion(ns, self.data[cursor:cursor + used], self.row_proof.row_roots[i]):
+                return False
+            cursor += used
+        return True
+
+    def validate(self, root: bytes) -> None:
+        """ShareProof.Validate: shapes, the row proof under the data root, then
+        the share proofs under the row roots."""
+        n = sum(p.end - p.start for p in self.share_proofs)
+        if len(self.share_proofs) != len(self.row_proof.row_roots):
+            raise DAError(_abi.ERR_PROOF, f"the number of share proofs {len(self.share_proofs)} must equal the "
+                                          f"number of row roots {len(self.row_proof.row_roots)}")
+        if len(self.data) != n:
+            raise DAError(_abi.ERR_PROOF, f"the number of shares {len(self.data)} must equal the number of "
+                                          f"shares in share proofs {n}")
+        for p in self.share_proofs:
+            if p.start < 0:
+                raise DAError(_abi.ERR_PROOF, f"proof index cannot be negative: {p.start}")
+            if p.end - p.start <= 0:
+                raise DAError(_abi.ERR_PROOF, f"proof total must be positive: {p.end - p.start}")
+        self.row_proof.validate(root)
+        if not self.verify_proof():
+            raise DAError(_abi.ERR_PROOF, "share proof failed to verify")
+
+
+def _bytes(b: bytes) -> np.ndarray:
+    return np.frombuffer(b, np.uint8) if len(b) else np.zeros(1, np.uint8)
 
 
 def merkle_levels(items: Sequence[bytes], ctx: Optional[Context] = None) -> List[List[bytes]]:
@@ -167,3 +251,37 @@ def new_share_inclusion_proof(shares: Sequence[bytes], namespace: bytes, share_r
                            start_row, end_row),
         namespace_version=namespace[0],
     )
+
+
+def parse_namespace(raw_shares: Sequence[bytes], start_share: int, end_share: int) -> bytes:
+    """proof.ParseNamespace (querier.go:123-151): the one namespace of shares
+    [start_share, end_share)."""
+    if start_share < 0:
+        raise DAError(_abi.ERR_ARG, f"start share {start_share} should be positive")
+    if end_share < 0:
+        raise DAError(_abi.ERR_ARG, f"end share {end_share} should be positive")
+    if end_share < start_share:
+        raise DAError(_abi.ERR_ARG, f"end share {end_share} cannot be lower than starting share {start_share}")
+    if end_share > len(raw_shares):
+        raise DAError(_abi.ERR_ARG, f"end share {end_share} is higher than block shares {len(raw_shares)}")
+    ns = bytes(raw_shares[start_share][:29])
+    for i, share in enumerate(raw_shares[start_share:end_share]):
+        if bytes(share[:29]) != ns:
+            raise DAError(_abi.ERR_ARG, f"shares range contain different namespaces at index {i}: "
+                                        f"{ns.hex()} and {bytes(share[:29]).hex()}")
+    return ns
+
+
+def new_tx_inclusion_proof(txs: Sequence[bytes], tx_index: int, app_version: int = 1,
+                           ctx: Optional[Context] = None) -> ShareProof:
+    """proof.NewTxInclusionProof: build the square from `txs`, find the tx's
+    share range and prove it (the shares of a PFB live in the PFB namespace)."""
+    from . import blobtx, shares as sh, square as sq
+    if tx_index >= len(txs):
+        raise DAError(_abi.ERR_ARG, f"txIndex {tx_index} out of bounds")
+    b = sq.Builder(sq.square_size_upper_bound(app_version), app_version, *txs)
+    data_square = b.export()
+    r = b.find_tx_share_range(tx_index)
+    _, is_blob = blobtx.unmarshal_blob_tx(txs[tx_index])
+    ns = sh.PAY_FOR_BLOB_NAMESPACE if is_blob else sh.TX_NAMESPACE
+    return new_share_inclusion_proof(data_square.square_bytes(), ns, (r.start, r.end), ctx)

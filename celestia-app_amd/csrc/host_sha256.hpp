@@ -112,5 +112,60 @@ inline void rfc6962_root(const std::vector<const uint8_t*>& items, size_t len, u
   rfc6962_rec(items, 0, items.size(), len, out);
 }
 
+// ---- proof verification (off the hot path: a light client checks a few nodes) ----
+
+constexpr size_t kNs = 29, kNodeLen = 90;
+
+// nmt HashLeaf (test/util/malicious/hasher.go:186-212 mirror of nmt v0.20.0):
+// ns || ns || SHA256(0x00 || ns || data)
+inline void nmt_hash_leaf(const uint8_t* ns, const uint8_t* data, size_t len, uint8_t out[kNodeLen]) {
+  uint8_t tmp[kNodeLen];
+  memcpy(tmp, ns, kNs);
+  memcpy(tmp + kNs, ns, kNs);
+  Sha256 s;
+  const uint8_t z = 0x00;
+  s.update(&z, 1);
+  s.update(ns, kNs);
+  s.update(data, len);
+  s.final(tmp + 2 * kNs);
+  memcpy(out, tmp, kNodeLen);
+}
+
+// nmt HashNode with IgnoreMaxNamespace (hasher.go:271-309): false when the
+// siblings are unordered (right.min < left.max, nmt ErrUnorderedSiblings).
+inline bool nmt_hash_node(const uint8_t* l, const uint8_t* r, uint8_t out[kNodeLen]) {
+  if (memcmp(r, l + kNs, kNs) < 0) return false;
+  bool rpar = true;
+  for (size_t i = 0; i < kNs; i++) rpar &= r[i] == 0xFF;
+  uint8_t tmp[kNodeLen];
+  memcpy(tmp, l, kNs);
+  memcpy(tmp + kNs, rpar ? l + kNs : r + kNs, kNs);
+  Sha256 s;
+  const uint8_t one = 0x01;
+  s.update(&one, 1);
+  s.update(l, kNodeLen);
+  s.update(r, kNodeLen);
+  s.final(tmp + 2 * kNs);
+  memcpy(out, tmp, kNodeLen);
+  return true;
+}
+
+inline void merkle_leaf_hash(const uint8_t* leaf, size_t len, uint8_t out[32]) {
+  Sha256 s;
+  const uint8_t z = 0x00;
+  s.update(&z, 1);
+  s.update(leaf, len);
+  s.final(out);
+}
+
+inline void merkle_inner_hash(const uint8_t* l, const uint8_t* r, uint8_t out[32]) {
+  Sha256 s;
+  const uint8_t one = 0x01;
+  s.update(&one, 1);
+  s.update(l, 32);
+  s.update(r, 32);
+  s.final(out);
+}
+
 }  // namespace host
 }  // namespace dagpu

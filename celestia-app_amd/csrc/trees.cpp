@@ -17,11 +17,13 @@
 
 #include <cmath>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "../../include/dagpu.h"
 #include "forest.hpp"
 #include "kernels.hpp"
+#include "host_sha256.hpp"
 #include "runtime.hpp"
 
 namespace {
@@ -312,6 +314,93 @@ int dagpu_merkle_levels(dagpu_ctx* ctx, size_t n, const uint8_t* items, size_t i
   HIP_TRY(ctx, hipMemcpyAsync(out32, ctx->t_leaves.p, total * kRecRfc, hipMemcpyDeviceToHost, s));
   HIP_TRY(ctx, hipStreamSynchronize(s));
   return DAGPU_OK;
+}
+
+int dagpu_nmt_verify_inclusion(const uint8_t* ns29, const uint8_t* leaves, size_t n, size_t leaf_len,
+                               int64_t start, int64_t end, const uint8_t* nodes, size_t nnodes,
+                               const uint8_t* root90) {
+  using namespace dagpu::host;
+  if (!ns29 || !root90 || (n && !leaves) || (nnodes && !nodes)) return DAGPU_ERR_ARG;
+  // Proof.VerifyInclusion: valid range, one leaf per proven index
+  if (start < 0 || start >= end || (int64_t)n != end - start) return DAGPU_ERR_PROOF;
+  std::vector<uint8_t> lh(n * kNodeLen);
+  for (size_t i = 0; i < n; i++) nmt_hash_leaf(ns29, leaves + i * leaf_len, leaf_len, &lh[i * kNodeLen]);
+  size_t next_leaf = 0, next_node = 0;
+  bool ok = true;
+  // nmt getSplitPoint: largest power of two strictly below length (length >= 2)
+  auto split = [](int64_t len) {
+    int64_t k = 1;
+    while (k * 2 < len) k *= 2;
+    return k;
+  };
+  // verifyLeafHashes.computeRoot: proof nodes fill the subtrees disjoint from
+  // [start, end), popped left to right; an absent right subtree is skipped.
+  std::function<bool(int64_t, int64_t, uint8_t*)> root_of = [&](int64_t lo, int64_t hi, uint8_t* out) -> bool {
+    if (hi - lo == 1 && start <= lo && lo < end) {
+      memcpy(out, &lh[next_leaf++ * kNodeLen], kNodeLen);
+      return true;
+    }
+    if (hi - lo == 1 || hi <= start || lo >= end) {
+      if (next_node >= nnodes) return false;
+      memcpy(out, nodes + next_node++ * kNodeLen, kNodeLen);
+      return true;
+    }
+    const int64_t k = split(hi - lo);
+    uint8_t l[kNodeLen], r[kNodeLen];
+    if (!root_of(lo, lo + k, l)) return false;  // a missing left subtree cannot verify
+    if (!root_of(lo + k, hi, r)) {
+      memcpy(out, l, kNodeLen);
+      return true;
+    }
+    if (!nmt_hash_node(l, r, out)) ok = false;
+    return true;
+  };
+  int64_t est = 1;
+  while (est < end) est *= 2;  // getSplitPoint(end) * 2: the subtree holding the range
+  uint8_t root[kNodeLen];
+  if (!root_of(0, est, root)) return DAGPU_ERR_PROOF;
+  for (; next_node < nnodes; next_node++) {  // remaining right-hand nodes
+    uint8_t t[kNodeLen];
+    if (!nmt_hash_node(root, nodes + next_node * kNodeLen, t)) ok = false;
+    memcpy(root, t, kNodeLen);
+  }
+  if (!ok || next_leaf != n) return DAGPU_ERR_PROOF;
+  return memcmp(root, root90, kNodeLen) == 0 ? DAGPU_OK : DAGPU_ERR_PROOF;
+}
+
+int dagpu_merkle_verify(const uint8_t* root32, const uint8_t* leaf, size_t leaf_len, int64_t index,
+                        int64_t total, const uint8_t* aunts, size_t naunts) {
+  using namespace dagpu::host;
+  if (!root32 || (leaf_len && !leaf) || (naunts && !aunts)) return DAGPU_ERR_ARG;
+  if (total < 0 || index < 0) return DAGPU_ERR_PROOF;
+  uint8_t h[32];
+  merkle_leaf_hash(leaf, leaf_len, h);
+  // crypto/merkle computeHashFromAunts, aunts ordered leaf to root
+  std::function<bool(int64_t, int64_t, size_t, uint8_t*)> up = [&](int64_t idx, int64_t tot, size_t na,
+                                                                     uint8_t* out) -> bool {
+    if (idx >= tot || idx < 0 || tot <= 0) return false;
+    if (tot == 1) {
+      if (na != 0) return false;
+      memcpy(out, h, 32);
+      return true;
+    }
+    if (na == 0) return false;
+    int64_t left = 1;
+    while (left * 2 < tot) left *= 2;
+    uint8_t sub[32];
+    const uint8_t* aunt = aunts + (na - 1) * 32;
+    if (idx < left) {
+      if (!up(idx, left, na - 1, sub)) return false;
+      merkle_inner_hash(sub, aunt, out);
+    } else {
+      if (!up(idx - left, tot - left, na - 1, sub)) return false;
+      merkle_inner_hash(aunt, sub, out);
+    }
+    return true;
+  };
+  uint8_t root[32];
+  if (!up(index, total, naunts, root)) return DAGPU_ERR_PROOF;
+  return memcmp(root, root32, 32) == 0 ? DAGPU_OK : DAGPU_ERR_PROOF;
 }
 
 int dagpu_subtree_width(uint64_t share_count, uint32_t subtree_root_threshold) {

@@ -48,7 +48,8 @@ typedef enum dagpu_status {
   DAGPU_ERR_BAD_ROOTS = -8,      /* rsmt2d "bad root input" */
   DAGPU_ERR_ARG = -9,
   DAGPU_ERR_DEVICE = -10,        /* HIP runtime failure */
-  DAGPU_ERR_UNSUPPORTED = -11    /* e.g. k above what this build implements */
+  DAGPU_ERR_UNSUPPORTED = -11,   /* e.g. k above what this build implements */
+  DAGPU_ERR_PROOF = -12          /* a proof does not verify against the given root */
 } dagpu_status;
 
 typedef struct dagpu_ctx dagpu_ctx;
@@ -210,6 +211,19 @@ int dagpu_merkle_roots(dagpu_ctx* ctx, size_t ntrees, const uint32_t* counts,
  * *n_nodes: in = capacity of out32 in nodes, out = nodes written (or needed). */
 int dagpu_merkle_levels(dagpu_ctx* ctx, size_t n, const uint8_t* items, size_t item_len,
                         uint8_t* out32, size_t* n_nodes);
+
+/* Proof verification on the host (light-client side of pkg/proof):
+ * nmt Proof.VerifyInclusion (nmt v0.20.0, IgnoreMaxNamespace, used by
+ * celestia-core ShareProof.VerifyProof): n leaves of leaf_len bytes each, given
+ * WITHOUT the namespace the tree prepends, proven at [start, end) by nnodes
+ * 90-B nodes against a 90-B root.  crypto/merkle Proof.Verify: leaf bytes,
+ * index/total and naunts 32-B aunts (leaf to root) against a 32-B root.
+ * DAGPU_OK = valid, DAGPU_ERR_PROOF = does not verify, DAGPU_ERR_ARG = malformed. */
+int dagpu_nmt_verify_inclusion(const uint8_t* ns29, const uint8_t* leaves, size_t n, size_t leaf_len,
+                               int64_t start, int64_t end, const uint8_t* nodes, size_t nnodes,
+                               const uint8_t* root90);
+int dagpu_merkle_verify(const uint8_t* root32, const uint8_t* leaf, size_t leaf_len, int64_t index,
+                        int64_t total, const uint8_t* aunts, size_t naunts);
 
 /* inclusion.SubTreeWidth (pkg/inclusion/blob_share_commitment_rules.go:85-101). */
 int dagpu_subtree_width(uint64_t share_count, uint32_t subtree_root_threshold);

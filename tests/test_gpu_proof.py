@@ -119,3 +119,52 @@ def test_share_inclusion_proofs(ctx, k):
             assert _verify_nmt(nmtp.nodes, w, nmtp.start, nmtp.end, leaves) == row_root
             assert _verify_merkle(mp, row_root) == data_root
         assert cursor == len(sp.data)
+
+
+@pytest.mark.parametrize("k", [4, 8, 32])
+def test_share_proofs_validate_with_library_verifiers(ctx, k):
+    """ShareProof.Validate (RowProof.Validate + VerifyProof through
+    dagpu_merkle_verify / dagpu_nmt_verify_inclusion) accepts every
+    single-namespace proof and rejects tampered ones; a range spanning several
+    namespaces does not verify (VerifyInclusion prepends one namespace)."""
+    ods, placed = _square(k, k + 100)
+    shares = [ods[i].tobytes() for i in range(k * k)]
+    eds = da.extend_shares(ods, ctx)
+    data_root = da.new_data_availability_header(eds).hash()
+    for start, ns, d in placed:
+        end = start + len(trees.split_blob(ns, d))
+        assert proof.parse_namespace(shares, start, end) == ns
+        sp = proof.new_share_inclusion_proof(shares, ns, (start, end), ctx)
+        sp.validate(data_root)
+        with pytest.raises(da.DAError):
+            sp.validate(bytes(32))
+        bad = list(sp.data)
+        bad[0] = bad[0][:200] + bytes([bad[0][200] ^ 1]) + bad[0][201:]
+        with pytest.raises(da.DAError, match="share proof failed"):
+            proof.ShareProof(bad, sp.share_proofs, sp.namespace_id, sp.row_proof, sp.namespace_version).validate(
+                data_root)
+        with pytest.raises(da.DAError):
+            proof.ShareProof(sp.data[1:], sp.share_proofs, sp.namespace_id, sp.row_proof,
+                             sp.namespace_version).validate(data_root)
+    whole = proof.new_share_inclusion_proof(shares, b"\x00" * 29, (0, k * k), ctx)
+    with pytest.raises(da.DAError, match="share proof failed"):
+        whole.validate(data_root)
+
+
+def test_tx_inclusion_proofs(ctx):
+    """proof.NewTxInclusionProof over a square built from txs: every normal tx
+    and every PFB is proven under the square's data root."""
+    import random
+    from celestia_da import square as sq
+    from test_square_host import normal_txs, random_blob_txs
+    rng = random.Random(21)
+    txs = normal_txs(rng, 6, size=700) + random_blob_txs(rng, 5, 3000, blobs_per=2)
+    square = sq.construct(txs)
+    k = square.size()
+    ods = np.frombuffer(b"".join(square.square_bytes()), np.uint8).reshape(k * k, 512)
+    data_root = da.new_data_availability_header(da.extend_shares(ods, ctx)).hash()
+    for i in range(len(txs)):
+        sp = proof.new_tx_inclusion_proof(txs, i, ctx=ctx)
+        sp.validate(data_root)
+    with pytest.raises(da.DAError):
+        proof.new_tx_inclusion_proof(txs, len(txs), ctx=ctx)
