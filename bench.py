@@ -491,7 +491,7 @@ def bench_repair(args):
     torch.cuda.synchronize()
     ok = bool(torch.equal(ds.eds, ref)) and int(status.abs().sum()) == 0
     ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-    out = {"metric": "Repair squares/sec (k=128, maximal erasure, roots re-verified)",
+    out = {"metric": f"Repair squares/sec (k={k}, maximal erasure, roots re-verified)",
            "value": B / (ms * 1e-3), "unit": "squares/s", "n_gpus": 1, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "bit_exact": ok,
            "decode_gbs": rs_bytes(k) * B / (ms * 1e-3) / 1e9,

@@ -576,6 +576,198 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(3, 8))) void 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Register-resident GF(2^16) decode for k = 256 (n = 2k = 512 work elements):
+// the encoder's M = 512 structure (8 waves x 64 elements, one 512-B chunk of
+// one vector, block / transposed layouts, P x P LDS transpose) with the
+// decoder's steps (leopard.go reconstruct, as leo16_decode_kernel above):
+//   work = shard * errLocs (0 where missing) -> ifftDITDecoder (skew index
+//   iend - 1) -> formal derivative -> fftDIT -> erased shards = work *
+//   (65535 - errLocs).
+// Runtime multiplies (errLocs are per element, wave-uniform) build their
+// 16-dword product table on the fly: lane 4g + e2 computes (e2 << 2g) * exp(lm)
+// from the log/exp tables, a quad DPP OR packs the four bytes, v_readlane
+// moves the 16 dwords to SGPRs.
+// The formal derivative D(x)_e = x_e ^ XOR_{s: bit s of e == 0} x_{e | 2^s}
+// runs in the transposed layout (element bits 3-5 = wave): slot bits are
+// applied in place in ascending slot order (a read of slot e | 2^t > e sees
+// an original value), the wave bits from the partner waves' originals, which
+// are staged through LDS 16 slots at a time.
+// ---------------------------------------------------------------------------
+constexpr int kDecN = 512;
+
+__device__ __forceinline__ void mul16_table(uint32_t lm, uint32_t (&t)[16]) {
+  const int lane = threadIdx.x & 63;
+  const int g = (lane >> 2) & 7, e2 = lane & 3;
+  const uint32_t x = (uint32_t)e2 << (2 * g);
+  uint32_t prod = 0;
+  if (x) {
+    uint32_t sidx = (uint32_t)g_log16[x] + lm;
+    sidx = (sidx + (sidx >> 16)) & 0xFFFFu;
+    prod = g_exp16[sidx];
+  }
+  uint32_t vlo = (prod & 0xFFu) << (8 * e2), vhi = ((prod >> 8) & 0xFFu) << (8 * e2);
+  vlo |= (uint32_t)__builtin_amdgcn_mov_dpp((int)vlo, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  vhi |= (uint32_t)__builtin_amdgcn_mov_dpp((int)vhi, 0xB1, 0xF, 0xF, false);
+  vlo |= (uint32_t)__builtin_amdgcn_mov_dpp((int)vlo, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  vhi |= (uint32_t)__builtin_amdgcn_mov_dpp((int)vhi, 0x4E, 0xF, 0xF, false);
+#pragma unroll
+  for (int gg = 0; gg < 8; gg++) {
+    t[gg] = __builtin_amdgcn_readlane(vlo, 4 * gg);
+    t[8 + gg] = __builtin_amdgcn_readlane(vhi, 4 * gg);
+  }
+}
+
+// (xlo, xhi) = (xlo, xhi) * exp(lm) with the table of mul16_table
+__device__ __forceinline__ void mul16_by(uint32_t& xlo, uint32_t& xhi, const uint32_t (&t)[16]) {
+  uint32_t pl[8], ph[8];
+#pragma unroll
+  for (int g = 0; g < 4; g++) {
+    const uint32_t sl = (xlo >> (2 * g)) & 0x03030303u;
+    const uint32_t sh = (xhi >> (2 * g)) & 0x03030303u;
+    pl[g] = __builtin_amdgcn_perm(t[g], t[g], sl);
+    ph[g] = __builtin_amdgcn_perm(t[8 + g], t[8 + g], sl);
+    pl[4 + g] = __builtin_amdgcn_perm(t[4 + g], t[4 + g], sh);
+    ph[4 + g] = __builtin_amdgcn_perm(t[12 + g], t[12 + g], sh);
+  }
+  xlo = xor3(xor3(xor3(pl[0], pl[1], pl[2]), pl[3], pl[4]), xor3(pl[5], pl[6], pl[7]), 0u);
+  xhi = xor3(xor3(xor3(ph[0], ph[1], ph[2]), ph[3], ph[4]), xor3(ph[5], ph[6], ph[7]), 0u);
+}
+
+// Formal derivative in the transposed layout (wave c: element bits 3-5 = c,
+// slot 8h + b: h = element bits 6-8, b = bits 0-2).
+__device__ __forceinline__ void derivative16_xposed(W16& w, uint32_t* lds, int c, int lane) {
+  constexpr int B = 16;  // slots per LDS round; lds[(wave * B + u) * 2 + lohi][64]
+#pragma unroll
+  for (int s0 = 0; s0 < 64; s0 += B) {
+#pragma unroll
+    for (int u = 0; u < B; u++) {
+      lds[((c * B + u) * 2) * 64 + lane] = w.lo[s0 + u];
+      lds[((c * B + u) * 2 + 1) * 64 + lane] = w.hi[s0 + u];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < B; u++) {
+      const int sl = s0 + u;
+      uint32_t alo = w.lo[sl], ahi = w.hi[sl];
+#pragma unroll
+      for (int bit = 1; bit < 64; bit <<= 1)  // slot bits (element bits 0-2, 6-8)
+        if ((sl & bit) == 0) {
+          alo ^= w.lo[sl | bit];
+          ahi ^= w.hi[sl | bit];
+        }
+#pragma unroll
+      for (int wb = 1; wb < 8; wb <<= 1)  // wave bits (element bits 3-5): partners' originals
+        if ((c & wb) == 0) {
+          alo ^= lds[(((c | wb) * B + u) * 2) * 64 + lane];
+          ahi ^= lds[(((c | wb) * B + u) * 2 + 1) * 64 + lane];
+        }
+      w.lo[sl] = alo;
+      w.hi[sl] = ahi;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kDecN) __attribute__((amdgpu_waves_per_eu(2, 2))) void leo16_decode_reg_kernel(
+    DecodeArgs a) {
+  constexpr int M = kDecN, P = 8, S = 1, K = M / 2;
+  __shared__ uint32_t lds[P * 16 * 2 * 64];  // derivative staging (64 KiB) >= transpose (32 KiB)
+  const long blk = blockIdx.x;
+  const int chunk = (int)(blk % a.nchunk);
+  const long v = blk / a.nchunk;
+  if (a.flags[v] == 0) return;  // uniform: vector not decodable / complete this pass
+  const long sq = v / a.nvec, vec = v % a.nvec;
+  const int lane = threadIdx.x & 63;
+  const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t col = (uint32_t)chunk * 512u + (uint32_t)(lane >> 3) * 64u + (uint32_t)(lane & 7) * 4u;
+  const bool active = col < (uint32_t)a.shard_bytes;
+  const uint32_t cl = active ? col : 0u;
+  const auto rsrc = make_rsrc(a.data + sq * a.sq_stride + vec * a.vec_stride);
+  const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
+  const uint16_t* err = (const uint16_t*)(a.err + v * rs_err_bytes(K));
+  // work element i = 64 q + j: layout [parity k][data k]
+  const int my_i = 64 * q + lane;
+  const int my_shard = my_i < K ? K + my_i : my_i - K;
+  const uint64_t pm = __builtin_amdgcn_ballot_w64(pres[(long)my_shard * a.p_shard_stride] != 0);
+  const uint32_t my_err = err[my_i];
+  W16 w;
+#pragma unroll
+  for (int j = 0; j < 64; j++) {
+    const int i = 64 * q + j;
+    const int shard = i < K ? K + i : i - K;
+    const uint32_t so = (uint32_t)shard * (uint32_t)a.shard_stride;
+    const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(rsrc, cl, so, 0);
+    const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rsrc, cl + 32u, so, 0);
+    const bool p = (pm >> j) & 1;
+    w.lo[j] = p ? lo : 0u;
+    w.hi[j] = p ? hi : 0u;
+  }
+  // work *= errLocs (one product table per element)
+#pragma unroll
+  for (int j = 0; j < 64; j++) {
+    uint32_t t[16];
+    mul16_table(__builtin_amdgcn_readlane(my_err, j), t);
+    uint32_t xl = w.lo[j], xh = w.hi[j];
+    mul16_by(xl, xh, t);
+    w.lo[j] = xl;
+    w.hi[j] = xh;
+    __builtin_amdgcn_sched_barrier(0);  // one table live at a time
+  }
+  // ---- IFFT (ifftDITDecoder, skew index iend - 1) ----
+  ifft16_block<1>(w, -1 + 64 * q);  // bits 0-5
+  xpose16<P, S>(w, lds, q, lane);
+#pragma unroll
+  for (int hr = 0; hr < 8; hr += 4) {  // radix-4 dist 64 (bits 6, 7)
+    const int p01 = 64 * hr + 63, p02 = p01 + 64, p23 = p01 + 128;
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+      const int s0 = hr * 8 + b;
+      ifft2_16(w, s0, s0 + 8, p01);
+      ifft2_16(w, s0 + 16, s0 + 24, p23);
+      ifft2_16(w, s0, s0 + 16, p02);
+      ifft2_16(w, s0 + 8, s0 + 24, p02);
+    }
+  }
+#pragma unroll
+  for (int s0 = 0; s0 < 32; s0++) ifft2_16(w, s0, s0 + 32, 255);  // last layer, dist 256
+  derivative16_xposed(w, lds, q, lane);
+  // ---- FFT (fftDIT, skew index iend - 1), as the M = 512 encoder ----
+#pragma unroll
+  for (int s0 = 0; s0 < 16; s0++) {  // dist4 = 512, dist = 128 (bits 8, 7)
+    fft2_16(w, s0, s0 + 32, 255);
+    fft2_16(w, s0 + 16, s0 + 48, 255);
+    fft2_16(w, s0, s0 + 16, 127);
+    fft2_16(w, s0 + 32, s0 + 48, 383);
+  }
+#pragma unroll
+  for (int g2 = 0; g2 < 4; g2++)  // dist4 = 128 step, first sub-layer (bit 6)
+#pragma unroll
+    for (int b = 0; b < 8; b++) fft2_16(w, 16 * g2 + b, 16 * g2 + b + 8, 128 * g2 + 63);
+  xpose16<P, S>(w, lds, q, lane);
+#pragma unroll
+  for (int j = 0; j < 32; j++) fft2_16(w, j, j + 32, 64 * q + 31);  // second sub-layer (bit 5)
+  fft16_block<8>(w, 64 * q);                                         // bits 4 .. 0
+  // erased shards = work * (65535 - errLocs); every lane builds the tables
+  // (mul16_table reads lanes 0..31), only active lanes store
+#pragma unroll
+  for (int j = 0; j < 64; j++) {
+    if ((pm >> j) & 1) continue;  // uniform
+    const int i = 64 * q + j;
+    const int shard = i < K ? K + i : i - K;
+    uint32_t t[16];
+    mul16_table(kMod16 - __builtin_amdgcn_readlane(my_err, j), t);
+    uint32_t xl = w.lo[j], xh = w.hi[j];
+    mul16_by(xl, xh, t);
+    const uint32_t so = (uint32_t)shard * (uint32_t)a.shard_stride;
+    if (active) {
+      __builtin_amdgcn_raw_buffer_store_b32(xl, rsrc, col, so, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(xh, rsrc, col + 32u, so, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // Tables are module globals: upload once per device.
 std::mutex g_tab_mu;
 bool g_tab_done[64];
@@ -668,9 +860,18 @@ hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mar
   if (e != hipSuccess) return e;
   const long nv = a.nsq * a.nvec;
   if (nv <= 0) return hipSuccess;
-  const long blocks = nv * (a.shard_bytes / 64);
-  hipLaunchKernelGGL(leo16_decode_kernel, dim3((unsigned)blocks), dim3(kThreads16),
-                     (size_t)a.k * 2 * 64 * 2, s, a);
+#ifndef DAGPU_GF16_LDS_DECODE
+  if (a.k == kDecN / 2) {  // register-resident decoder; nchunk = 512-B chunks of the shard
+    DecodeArgs b = a;
+    b.nchunk = (a.shard_bytes + 511) / 512;
+    hipLaunchKernelGGL(leo16_decode_reg_kernel, dim3((unsigned)(nv * b.nchunk)), dim3(kDecN), 0, s, b);
+  } else
+#endif
+  {
+    const long blocks = nv * (a.shard_bytes / 64);
+    hipLaunchKernelGGL(leo16_decode_kernel, dim3((unsigned)blocks), dim3(kThreads16),
+                       (size_t)a.k * 2 * 64 * 2, s, a);
+  }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (mark_present) {
     hipLaunchKernelGGL(mark_present16_kernel, dim3((unsigned)nv), dim3(256), 0, s, a);
