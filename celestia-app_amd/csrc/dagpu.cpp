@@ -498,7 +498,7 @@ int dagpu_decode(dagpu_ctx* ctx, uint32_t k, size_t nvec, size_t shard_size, uin
   HIP_TRY(ctx, ctx->eds.ensure(bytes));
   HIP_TRY(ctx, ctx->ods.ensure(n * nvec));
   const size_t errb = (size_t)rs_err_bytes((int)k) * nvec;
-  HIP_TRY(ctx, ctx->ws.ensure(errb + nvec * sizeof(int32_t) + 256));
+  HIP_TRY(ctx, ctx->ws.ensure(errb + 3 * nvec * sizeof(int32_t) + 256));
   HIP_TRY(ctx, ctx->status.ensure(sizeof(int32_t)));
   HIP_TRY(ctx, hipMemcpyAsync(ctx->eds.p, shards, bytes, hipMemcpyHostToDevice, s));
   HIP_TRY(ctx, hipMemcpyAsync(ctx->ods.p, present, n * nvec, hipMemcpyHostToDevice, s));
@@ -514,6 +514,8 @@ int dagpu_decode(dagpu_ctx* ctx, uint32_t k, size_t nvec, size_t shard_size, uin
   da.p_shard_stride = 1;
   da.err = (uint8_t*)ctx->ws.p;
   da.flags = (int32_t*)((uint8_t*)ctx->ws.p + errb);
+  da.err_same = da.flags + nvec;
+  da.err_head = da.flags + 2 * nvec;
   da.too_few = (int32_t*)ctx->status.p;
   da.nsq = 1;
   da.nvec = (long)nvec;
@@ -543,6 +545,7 @@ struct RepairWs {
   uint8_t* err_cols;
   int32_t* flags_rows;
   int32_t* flags_cols;
+  int32_t* err_share[2][2];  // [axis][same, head]
   int32_t* bits;
   int32_t* counters;    // [0] decodable rows, [1] decodable cols
 };
@@ -556,6 +559,7 @@ size_t repair_ws_bytes(uint32_t k, size_t n) {
   t += a256(n * w * w);                                           // p0
   t += 2 * a256(n * 2 * w * 4);                                   // complete before/now
   t += 2 * a256(n * w * rs_err_bytes((int)k)) + 2 * a256(n * w * 4);  // err, flags
+  t += 4 * a256(n * w * 4);                                             // err_same, err_head per axis
   t += a256(n * 4) + 256;                                         // bits, counters
   return t;
 }
@@ -579,6 +583,11 @@ RepairWs carve_repair(uint32_t k, size_t n, void* base) {
   r.err_cols = p; p += a256(n * w * rs_err_bytes((int)k));
   r.flags_rows = (int32_t*)p; p += a256(n * w * 4);
   r.flags_cols = (int32_t*)p; p += a256(n * w * 4);
+  for (int ax = 0; ax < 2; ax++)
+    for (int j = 0; j < 2; j++) {
+      r.err_share[ax][j] = (int32_t*)p;
+      p += a256(n * w * 4);
+    }
   r.bits = (int32_t*)p; p += a256(n * 4);
   r.counters = (int32_t*)p;
   return r;
@@ -601,6 +610,8 @@ DecodeArgs axis_decode_args(uint32_t k, size_t n, uint8_t* eds, uint8_t* present
     d.p_vec_stride = 1; d.p_shard_stride = w;
     d.err = r.err_cols; d.flags = r.flags_cols; d.ndecodable = r.counters + 1;
   }
+  d.err_same = r.err_share[axis][0];
+  d.err_head = r.err_share[axis][1];
   d.nsq = (long)n;
   d.nvec = w;
   d.nchunk = 1;

@@ -53,9 +53,19 @@ struct DecodeArgs {
   int32_t* too_few;    // optional: set to 1 if any vector has < k shards
   int32_t* progress;   // optional: += number of vectors rebuilt (mark pass)
   int32_t* ndecodable; // optional: += number of decodable vectors (errlocs pass)
+  // Optional error-locator sharing: the locators depend only on the erasure
+  // pattern, and neighbouring vectors of a repair pass usually share it (every
+  // row of a square kept by the same column set).  err_same[v] = pattern of v
+  // equals that of v - 1; err_head[v] = first vector of v's run, whose locators
+  // v uses.  Both nsq * nvec int32 of workspace; NULL = one computation per vector.
+  int32_t* err_same;
+  int32_t* err_head;
   long nsq, nvec, nchunk, shard_bytes;
   int k;
 };
+
+// vector whose error locators vector v uses
+__device__ __forceinline__ long err_vec(const DecodeArgs& a, long v) { return a.err_head ? a.err_head[v] : v; }
 
 hipError_t launch_leo8_decode(const DecodeArgs& a, hipStream_t s, bool mark_present);
 hipError_t launch_leo8_errlocs(const DecodeArgs& a, hipStream_t s);

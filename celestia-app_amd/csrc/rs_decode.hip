@@ -86,6 +86,7 @@ __global__ __launch_bounds__(64) void leo8_errlocs_kernel(DecodeArgs a) {
     if (decode && a.ndecodable) atomicAdd(a.ndecodable, 1);
   }
   if (!decode) return;  // uniform
+  if (err_vec(a, v) != v) return;  // same erasure pattern as an earlier vector: share its locators
   fwht256_lds(e, n);
   for (int i = threadIdx.x; i < 256; i += 64) e[i] = (e[i] * kGf8.walsh[i]) % 255u;
   __syncthreads();
@@ -180,7 +181,7 @@ __device__ __forceinline__ void decode_small(const DecodeArgs& a, long v, int la
   uint8_t* base = a.data + sq * a.sq_stride + vec * a.vec_stride;
   const auto rsrc = make_rsrc(base);
   const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
-  const uint8_t* err = a.err + v * 256;
+  const uint8_t* err = a.err + err_vec(a, v) * 256;
   const uint32_t ss = (uint32_t)a.shard_stride;
   uint64_t pm[NB];
   uint32_t e8[NB];
@@ -291,7 +292,7 @@ __device__ __forceinline__ void decode128_part(const DecodeArgs& a, long v, int 
   uint8_t* base = a.data + sq * a.sq_stride + vec * a.vec_stride;
   const auto rsrc = make_rsrc(base);
   const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
-  const uint8_t* err = a.err + v * 256;
+  const uint8_t* err = a.err + err_vec(a, v) * 256;
   const uint32_t ss = (uint32_t)a.shard_stride;
   // presence of the shard behind work index i: bit (i & 63) of pm[i >> 6]
   // (wave-uniform ballots); this part's error locators, one per lane

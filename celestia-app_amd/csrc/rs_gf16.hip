@@ -254,6 +254,7 @@ __global__ __launch_bounds__(kErrThreads) void leo16_errlocs_kernel(DecodeArgs a
     if (decode && a.ndecodable) atomicAdd(a.ndecodable, 1);
   }
   if (!decode) return;  // uniform
+  if (err_vec(a, v) != v) return;  // shares an earlier vector's locators
   fwht65536(e16);
   for (int i = threadIdx.x; i < 65536; i += kErrThreads)
     e16[i] = (uint16_t)(((uint32_t)e16[i] * (uint32_t)g_walsh16[i]) % kMod16);
@@ -277,7 +278,7 @@ __global__ __launch_bounds__(kThreads16) void leo16_decode_kernel(DecodeArgs a) 
   const long sq = v / a.nvec, vec = v % a.nvec;
   uint8_t* base = a.data + sq * a.sq_stride + vec * a.vec_stride + blk * 64;
   const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
-  const uint16_t* err = (const uint16_t*)(a.err + v * (long)rs_err_bytes(k));
+  const uint16_t* err = (const uint16_t*)(a.err + err_vec(a, v) * (long)rs_err_bytes(k));
   uint16_t* work = w16;
   uint16_t* der = w16 + n * 32;
   // work[i] = shard(pos(i)) * errLocs[i], zero if missing; layout [parity k][data k]
@@ -586,8 +587,8 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(3, 8))) void 
 //   (65535 - errLocs).
 // Runtime multiplies (errLocs are per element, wave-uniform) build their
 // 16-dword product table on the fly: lane 4g + e2 computes (e2 << 2g) * exp(lm)
-// from the log/exp tables, a quad DPP OR packs the four bytes, v_readlane
-// moves the 16 dwords to SGPRs.
+// from the log/exp tables (16 elements' gathers in flight), a quad DPP OR
+// packs the four bytes, v_readlane moves the 16 dwords to SGPRs.
 // The formal derivative D(x)_e = x_e ^ XOR_{s: bit s of e == 0} x_{e | 2^s}
 // runs in the transposed layout (element bits 3-5 = wave): slot bits are
 // applied in place in ascending slot order (a read of slot e | 2^t > e sees
@@ -596,16 +597,20 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(3, 8))) void 
 // ---------------------------------------------------------------------------
 constexpr int kDecN = 512;
 
-__device__ __forceinline__ void mul16_table(uint32_t lm, uint32_t (&t)[16]) {
+// Lane 4g + e2 (lanes 32..63 repeat 0..31) owns the product (e2 << 2g) * exp(lm):
+// log(e2 << 2g) is per lane (mul16_logx, hoisted), exp() is one gather per
+// table; mul16_pack turns the 32 products into 16 wave-uniform dwords.
+__device__ __forceinline__ uint32_t mul16_x() {
   const int lane = threadIdx.x & 63;
-  const int g = (lane >> 2) & 7, e2 = lane & 3;
-  const uint32_t x = (uint32_t)e2 << (2 * g);
-  uint32_t prod = 0;
-  if (x) {
-    uint32_t sidx = (uint32_t)g_log16[x] + lm;
-    sidx = (sidx + (sidx >> 16)) & 0xFFFFu;
-    prod = g_exp16[sidx];
-  }
+  return (uint32_t)(lane & 3) << (2 * ((lane >> 2) & 7));
+}
+__device__ __forceinline__ uint32_t mul16_prod(uint32_t x, uint32_t logx, uint32_t lm) {
+  uint32_t sidx = logx + lm;
+  sidx = (sidx + (sidx >> 16)) & 0xFFFFu;
+  return x ? (uint32_t)g_exp16[sidx] : 0u;
+}
+__device__ __forceinline__ void mul16_pack(uint32_t prod, uint32_t (&t)[16]) {
+  const int e2 = threadIdx.x & 3;
   uint32_t vlo = (prod & 0xFFu) << (8 * e2), vhi = ((prod >> 8) & 0xFFu) << (8 * e2);
   vlo |= (uint32_t)__builtin_amdgcn_mov_dpp((int)vlo, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
   vhi |= (uint32_t)__builtin_amdgcn_mov_dpp((int)vhi, 0xB1, 0xF, 0xF, false);
@@ -618,7 +623,7 @@ __device__ __forceinline__ void mul16_table(uint32_t lm, uint32_t (&t)[16]) {
   }
 }
 
-// (xlo, xhi) = (xlo, xhi) * exp(lm) with the table of mul16_table
+// (xlo, xhi) = (xlo, xhi) * exp(lm) with the table of mul16_pack
 __device__ __forceinline__ void mul16_by(uint32_t& xlo, uint32_t& xhi, const uint32_t (&t)[16]) {
   uint32_t pl[8], ph[8];
 #pragma unroll
@@ -685,7 +690,7 @@ __global__ __launch_bounds__(kDecN) __attribute__((amdgpu_waves_per_eu(2, 2))) v
   const uint32_t cl = active ? col : 0u;
   const auto rsrc = make_rsrc(a.data + sq * a.sq_stride + vec * a.vec_stride);
   const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
-  const uint16_t* err = (const uint16_t*)(a.err + v * rs_err_bytes(K));
+  const uint16_t* err = (const uint16_t*)(a.err + err_vec(a, v) * rs_err_bytes(K));
   // work element i = 64 q + j: layout [parity k][data k]
   const int my_i = 64 * q + lane;
   const int my_shard = my_i < K ? K + my_i : my_i - K;
@@ -703,16 +708,25 @@ __global__ __launch_bounds__(kDecN) __attribute__((amdgpu_waves_per_eu(2, 2))) v
     w.lo[j] = p ? lo : 0u;
     w.hi[j] = p ? hi : 0u;
   }
-  // work *= errLocs (one product table per element)
+  // work *= errLocs: one product table per element, the exp() gathers of 16
+  // elements in flight at a time
+  const uint32_t mx = mul16_x();
+  const uint32_t mlogx = mx ? (uint32_t)g_log16[mx] : 0u;
 #pragma unroll
-  for (int j = 0; j < 64; j++) {
-    uint32_t t[16];
-    mul16_table(__builtin_amdgcn_readlane(my_err, j), t);
-    uint32_t xl = w.lo[j], xh = w.hi[j];
-    mul16_by(xl, xh, t);
-    w.lo[j] = xl;
-    w.hi[j] = xh;
-    __builtin_amdgcn_sched_barrier(0);  // one table live at a time
+  for (int j0 = 0; j0 < 64; j0 += 16) {
+    uint32_t prod[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) prod[u] = mul16_prod(mx, mlogx, __builtin_amdgcn_readlane(my_err, j0 + u));
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      uint32_t t[16];
+      mul16_pack(prod[u], t);
+      uint32_t xl = w.lo[j0 + u], xh = w.hi[j0 + u];
+      mul16_by(xl, xh, t);
+      w.lo[j0 + u] = xl;
+      w.hi[j0 + u] = xh;
+    }
+    __builtin_amdgcn_sched_barrier(0);
   }
   // ---- IFFT (ifftDITDecoder, skew index iend - 1) ----
   ifft16_block<1>(w, -1 + 64 * q);  // bits 0-5
@@ -751,18 +765,27 @@ __global__ __launch_bounds__(kDecN) __attribute__((amdgpu_waves_per_eu(2, 2))) v
   // erased shards = work * (65535 - errLocs); every lane builds the tables
   // (mul16_table reads lanes 0..31), only active lanes store
 #pragma unroll
-  for (int j = 0; j < 64; j++) {
+  for (int j0 = 0; j0 < 64; j0 += 16) {
+    if (((pm >> j0) & 0xFFFFull) == 0xFFFFull) continue;  // uniform: no erasure among these 16
+    uint32_t prod[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++)
+      prod[u] = mul16_prod(mx, mlogx, kMod16 - __builtin_amdgcn_readlane(my_err, j0 + u));
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+    const int j = j0 + u;
     if ((pm >> j) & 1) continue;  // uniform
     const int i = 64 * q + j;
     const int shard = i < K ? K + i : i - K;
     uint32_t t[16];
-    mul16_table(kMod16 - __builtin_amdgcn_readlane(my_err, j), t);
+    mul16_pack(prod[u], t);
     uint32_t xl = w.lo[j], xh = w.hi[j];
     mul16_by(xl, xh, t);
     const uint32_t so = (uint32_t)shard * (uint32_t)a.shard_stride;
     if (active) {
       __builtin_amdgcn_raw_buffer_store_b32(xl, rsrc, col, so, 0);
       __builtin_amdgcn_raw_buffer_store_b32(xh, rsrc, col + 32u, so, 0);
+    }
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -880,11 +903,64 @@ hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mar
   return e;
 }
 
+// Error-locator sharing (DecodeArgs.err_same / err_head): a wave per vector
+// compares its 2k presence flags with vector v - 1's; then a scan per square
+// finds the head of each run of equal patterns.
+__global__ __launch_bounds__(64) void errloc_same_kernel(DecodeArgs a) {
+  const long v = blockIdx.x;
+  if (v == 0) {
+    if (threadIdx.x == 0) a.err_same[0] = 0;
+    return;
+  }
+  const long u = v - 1;
+  const uint8_t* pv = a.present + (v / a.nvec) * a.p_sq_stride + (v % a.nvec) * a.p_vec_stride;
+  const uint8_t* pu = a.present + (u / a.nvec) * a.p_sq_stride + (u % a.nvec) * a.p_vec_stride;
+  bool diff = false;
+  for (int i = threadIdx.x; i < 2 * a.k; i += 64)
+    diff |= (pv[(long)i * a.p_shard_stride] != 0) != (pu[(long)i * a.p_shard_stride] != 0);
+  const bool any = __builtin_amdgcn_ballot_w64(diff) != 0;
+  if (threadIdx.x == 0) a.err_same[v] = any ? 0 : 1;
+}
+
+// head[v] = last u <= v of v's square whose pattern differs from u - 1 (a
+// run never crosses a square): prefix max of (same ? -1 : index) per square,
+// one workgroup per square, Hillis-Steele in LDS (nvec <= 1024).
+__global__ __launch_bounds__(1024) void errloc_head_kernel(DecodeArgs a) {
+  __shared__ int32_t h[1024];
+  const long sq = blockIdx.x;
+  const int t = threadIdx.x;
+  const int nvec = (int)a.nvec;
+  const long v0 = sq * a.nvec;
+  if (t < nvec) h[t] = (t == 0 || !a.err_same[v0 + t]) ? t : -1;
+  __syncthreads();
+  for (int off = 1; off < nvec; off <<= 1) {
+    const int x = (t < nvec && t >= off) ? h[t - off] : -1;
+    __syncthreads();
+    if (t < nvec && x > h[t]) h[t] = x;
+    __syncthreads();
+  }
+  if (t < nvec) a.err_head[v0 + t] = (int32_t)(v0 + h[t]);
+}
+
+hipError_t launch_errloc_heads(const DecodeArgs& a, hipStream_t s) {
+  if (!a.err_same || !a.err_head) return hipSuccess;
+  const long nv = a.nsq * a.nvec;
+  if (nv <= 0) return hipSuccess;
+  hipLaunchKernelGGL(errloc_same_kernel, dim3((unsigned)nv), dim3(64), 0, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if (a.nvec > 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(errloc_head_kernel, dim3((unsigned)a.nsq), dim3(1024), 0, s, a);
+  return hipGetLastError();
+}
+
 // Field dispatch used by the host runtime: GF(2^8) for 2k <= 256, else GF(2^16).
 hipError_t launch_rs_encode(int k, const EncodeArgs& a, hipStream_t s) {
   return k <= 128 ? launch_leo8_encode(k, a, s) : launch_leo16_encode(k, a, s);
 }
 hipError_t launch_rs_errlocs(const DecodeArgs& a, hipStream_t s) {
+  hipError_t e = launch_errloc_heads(a, s);
+  if (e != hipSuccess) return e;
   return a.k <= 128 ? launch_leo8_errlocs(a, s) : launch_leo16_errlocs(a, s);
 }
 hipError_t launch_rs_decode_only(const DecodeArgs& a, hipStream_t s, bool mark_present) {
