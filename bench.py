@@ -51,16 +51,27 @@ def rs_bytes(k: int) -> int:
 
 
 def dist_init():
+    """One process per GPU over RCCL (torch.distributed "nccl").  With
+    DAGPU_BENCH_SHARED_GPU=1 every rank uses GPU 0 and the collectives run over
+    gloo, host-staged: a rehearsal of the N>1 code path on a one-GPU box (the
+    numbers it prints are not scaling numbers)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
         import datetime
+        if os.environ.get("DAGPU_BENCH_SHARED_GPU") == "1":
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
+            return dist, rank, world, 0
         dist.init_process_group("nccl", device_id=torch.device("cuda", local),
                                 timeout=datetime.timedelta(seconds=300))
         return dist, rank, world, local
     return None, 0, 1, 0
+
+
+def _host_staged(dist) -> bool:
+    return dist is not None and dist.get_backend() == "gloo"
 
 
 def barrier(dist):
@@ -71,9 +82,25 @@ def barrier(dist):
 def max_over_ranks(dist, v: float, local: int) -> float:
     if dist is None:
         return v
-    t = torch.tensor([v], dtype=torch.float64, device=torch.device("cuda", local))
+    dev = torch.device("cpu") if _host_staged(dist) else torch.device("cuda", local)
+    t = torch.tensor([v], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def all_gather_rows(dist, world, t):
+    """All-gather of equal-shaped per-rank tensors along dim 0 (RCCL on device;
+    gloo through host memory)."""
+    if dist is None:
+        return t
+    if _host_staged(dist):
+        h = t.cpu()
+        parts = [torch.empty_like(h) for _ in range(world)]
+        dist.all_gather(parts, h)
+        return torch.cat(parts).to(t.device)
+    allg = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(allg, t)
+    return allg
 
 
 def cpu_baseline(k: int, seconds: float, threads: int):
@@ -310,7 +337,7 @@ def bench_e2e(ctx, local, k, host_ods, steps, total=256):
 def bench_replay(dist, rank, world, local, ctx, ds, n_blocks):
     """configs[4] block replay: n_blocks consecutive k x k squares, contiguous
     shards per rank (celestia_da.replay.shard_range), processed in batches of
-    the resident `ds` (its 64 distinct squares stand for the blocks, cycled), every
+    the resident `ds` (its batch of squares stands for the blocks, cycled), every
     DAH gathered to all ranks and checked against the batch's own DAHs.  Timed
     from the first batch to the gathered DAHs, max over ranks."""
     from celestia_da import replay
@@ -331,11 +358,7 @@ def bench_replay(dist, rank, world, local, ctx, ds, n_blocks):
         ds.extend()
         out[done:done + m].copy_(ds.dah[:m], non_blocking=True)
         done += m
-    if dist is not None:
-        allg = torch.empty((world * per_rank, 32), dtype=torch.uint8, device=out.device)
-        dist.all_gather_into_tensor(allg, out)
-    else:
-        allg = out
+    allg = all_gather_rows(dist, world, out)
     torch.cuda.synchronize()
     barrier(dist)
     el = max_over_ranks(dist, time.perf_counter() - t0, local)
