@@ -39,6 +39,10 @@ struct EncodeArgs {
 };
 
 hipError_t launch_leo8_encode(int k, const EncodeArgs& a, hipStream_t s);
+// bit-sliced GF(2^8) encode (rs_gf8_sliced.hip); launch_leo8_encode uses it
+// whenever leo8_sliced_applicable() holds
+bool leo8_sliced_applicable(int k, const EncodeArgs& a);
+hipError_t launch_leo8_encode_sliced(int k, const EncodeArgs& a, hipStream_t s);
 
 // Decode addressing: shard i of vector (s, v) at
 //   data + s*sq_stride + v*vec_stride + i*shard_stride   (2k shards)

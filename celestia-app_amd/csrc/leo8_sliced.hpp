@@ -1,0 +1,272 @@
+// leo8_sliced.hpp -- bit-sliced Leopard GF(2^8) encode transform (the per-lane
+// part of rs_gf8_sliced.hip), shared with the host emulation that checks it on
+// the CPU (tools/sliced_emu.hip, tests/test_sliced_emu.py).
+//
+// Restates the same transform as rs_gf8.hip -- klauspost/reedsolomon v1.11.8
+// leopardFF8.encode (ifftDITEncoder8 then fftDIT8 with m = k) -- in a
+// different data layout.
+//
+// Bit-sliced data.  A lane owns 32 byte columns of an element (shard).  It
+// keeps them as 8 "planes": plane p is one dword whose 32 bits are bit p of
+// each of the 32 bytes.  Adding field elements is still XOR.  Multiplying by a
+// field constant c is GF(2)-linear in the bits, so it is an 8x8 bit matrix:
+//   out plane i = XOR over j with M_c[i][j] = 1 of plane j,
+// where column j of M_c is c * 2^j.  Only full-rate VALU ops are used: v_xor
+// and v_bitop3 (xor3, and-xor).  The packed-byte kernel needs v_perm, and any
+// v_perm in the stream drops it to half issue rate (profiles/issue_bench_r01.log).
+//
+// Compile-time skews.  The FFT skew of layer m (butterfly distance D = 2^m) for
+// the block starting at element b is fftSkew8[D - 1 + off], with off = b (FFT)
+// or k + b (IFFT).  As field elements these skews are GF(2)-linear in off
+// (initFFTSkew8 builds them as skew[j + s] = skew[j] ^ temp[i]), so
+//   skew(off1 ^ off2) = skew(off1) ^ skew(off2)
+// and the multiply matrix splits the same way: M_(a ^ b) = M_a ^ M_b.
+//
+// Two layouts of the k = 2^n elements over NW = k/16 waves, 16 registers each:
+//   A: wave = e >> 4,        register = e & 15   (pair bits 0..3 local)
+//   B: wave = e & (NW - 1),  register = e >> (n - 4)  (pair bits n-4..n-1 local)
+// In B every bit above a layer's pair bit is a register bit, so every skew is
+// a compile-time constant (the matrix folds into a chain of xor3 ops: about 24
+// ops per 32-byte butterfly, against 13 v_perm-class ops per 4 bytes before).
+// In A the layers below n-4 have skews that also depend on the wave bits:
+// skew = C (register bits, compile-time) ^ W (wave bits, one value per layer
+// per wave).  W's matrix is loaded into 64 SGPR masks and each matrix entry
+// costs one v_bitop3: x_i ^= y_j & (C_ij ? ~W_ij : W_ij).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <utility>
+
+#include "gf_const.hpp"
+
+namespace dagpu {
+namespace sliced {
+
+constexpr uint8_t gmul(uint8_t a, uint8_t c) {
+  if (a == 0 || c == 0) return 0;
+  return kGf8.exp[gf8_add_mod(kGf8.log[a], kGf8.log[c])];
+}
+
+// skew of table index idx as a field element (log kGf8Mod = element 0)
+constexpr uint8_t skew_elem(int idx) {
+  const int l = kGf8.skew[idx];
+  return l == kGf8Mod ? 0 : kGf8.exp[l];
+}
+
+// row[c][i] bit j = bit i of c * 2^j
+struct Gf8Mat {
+  uint8_t row[256][8];
+};
+constexpr Gf8Mat make_mat() {
+  Gf8Mat m{};
+  for (int c = 0; c < 256; c++)
+    for (int j = 0; j < 8; j++) {
+      const uint8_t col = gmul((uint8_t)(1u << j), (uint8_t)c);
+      for (int i = 0; i < 8; i++)
+        if ((col >> i) & 1) m.row[c][i] |= (uint8_t)(1u << j);
+    }
+  return m;
+}
+inline constexpr Gf8Mat kMat = make_mat();
+
+// Runtime part of the layout-A skews: W(m, w) = skew(D - 1 + 16 w), the same
+// for the IFFT and the FFT.  Masks: [m][w][8 i + j] = ~0 if bit i of W * 2^j.
+constexpr int kMaxAL = 3;   // layers below n - 4 for k = 128
+constexpr int kMaxWav = 8;  // waves for k = 128
+struct WMasks {
+  uint32_t m[kMaxAL][kMaxWav][64];
+};
+constexpr WMasks make_wmasks() {
+  WMasks t{};
+  for (int m = 0; m < kMaxAL; m++)
+    for (int w = 0; w < kMaxWav; w++) {
+      const uint8_t W = skew_elem((1 << m) - 1 + 16 * w);
+      for (int i = 0; i < 8; i++)
+        for (int j = 0; j < 8; j++) t.m[m][w][8 * i + j] = ((kMat.row[W][i] >> j) & 1) ? 0xFFFFFFFFu : 0u;
+    }
+  return t;
+}
+inline constexpr WMasks kWMasksHost = make_wmasks();
+
+// v_bitop3_b32 truth tables (S0 = 0xF0, S1 = 0xCC, S2 = 0xAA)
+constexpr uint8_t kXor3 = 0x96;    // a ^ b ^ c
+constexpr uint8_t kXorAnd = 0x78;  // a ^ (b & c)
+constexpr uint8_t kXorAndN = 0xB4; // a ^ (b & ~c)
+constexpr uint8_t kXorThenAnd = 0x28;  // (a ^ b) & c
+
+#if defined(__HIP_DEVICE_COMPILE__)
+#define SL_BOP3(a, b, c, tt) __builtin_amdgcn_bitop3_b32((a), (b), (c), (tt))
+// keeps the scheduler from hoisting the next layer's 64 mask loads (SGPR spills)
+#define SL_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define SL_FENCE() ((void)0)
+__host__ inline uint32_t sl_bop3_host(uint32_t a, uint32_t b, uint32_t c, uint8_t tt) {
+  uint32_t r = 0;
+  for (int k = 0; k < 8; k++)
+    if ((tt >> k) & 1) r |= ((k & 4) ? a : ~a) & ((k & 2) ? b : ~b) & ((k & 1) ? c : ~c);
+  return r;
+}
+#define SL_BOP3(a, b, c, tt) sl_bop3_host((a), (b), (c), (tt))
+#endif
+
+// 8x8 bit transpose of the bytes of 8 dwords, 4 byte positions at once:
+// afterwards d[p] byte q bit w = old d[w] byte q bit p.  Its own inverse.
+__host__ __device__ __forceinline__ void transpose8(uint32_t (&d)[8]) {
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    const uint32_t t = SL_BOP3(d[w] >> 4, d[w + 4], 0x0F0F0F0Fu, kXorThenAnd);
+    d[w + 4] ^= t;
+    d[w] ^= t << 4;
+  }
+#pragma unroll
+  for (int w0 = 0; w0 < 8; w0 += 4)
+#pragma unroll
+    for (int w = w0; w < w0 + 2; w++) {
+      const uint32_t t = SL_BOP3(d[w] >> 2, d[w + 2], 0x33333333u, kXorThenAnd);
+      d[w + 2] ^= t;
+      d[w] ^= t << 2;
+    }
+#pragma unroll
+  for (int w = 0; w < 8; w += 2) {
+    const uint32_t t = SL_BOP3(d[w] >> 1, d[w + 1], 0x55555555u, kXorThenAnd);
+    d[w + 1] ^= t;
+    d[w] ^= t << 1;
+  }
+}
+
+// Compile-time loop: f(std::integral_constant<int, I>{}) for I = 0 .. N-1, so
+// every index, skew and matrix row is a constant expression (a #pragma unroll
+// of these nests exceeds the unroller's budget and leaves the register arrays
+// dynamically indexed, i.e. in scratch).
+template <typename F, int... I>
+__host__ __device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__host__ __device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+__host__ __device__ __forceinline__ void xor8(uint32_t (&y)[8], const uint32_t (&x)[8]) {
+  static_for<8>([&](auto p) { y[p] ^= x[p]; });
+}
+
+// x ^= C * y for a compile-time element C: per output plane, its set matrix
+// bits are consumed two at a time by xor3.
+template <int R, int J>
+__host__ __device__ __forceinline__ uint32_t xor_row(uint32_t acc, const uint32_t (&y)[8]) {
+  if constexpr (J >= 8) {
+    return acc;
+  } else if constexpr (!((R >> J) & 1)) {
+    return xor_row<R, J + 1>(acc, y);
+  } else {
+    constexpr int rest = R & ~((2 << J) - 1);  // set bits above J
+    if constexpr (rest == 0) {
+      return acc ^ y[J];
+    } else {
+      constexpr int J2 = __builtin_ctz(rest);
+      return xor_row<R & ~((2 << J2) - 1), J2 + 1>(SL_BOP3(acc, y[J], y[J2], kXor3), y);
+    }
+  }
+}
+template <int C>
+__host__ __device__ __forceinline__ void muladd_ct(uint32_t (&x)[8], const uint32_t (&y)[8]) {
+  static_for<8>([&](auto i) { x[i] = xor_row<kMat.row[C][i], 0>(x[i], y); });
+}
+
+// x ^= (C ^ W) * y: C compile-time, W given by its 64 masks (wave-uniform)
+template <int C>
+__host__ __device__ __forceinline__ void muladd_rt(uint32_t (&x)[8], const uint32_t (&y)[8], const uint32_t* wm) {
+  static_for<8>([&](auto i) {
+    uint32_t acc = x[i];
+    static_for<8>([&](auto j) {
+      if constexpr ((kMat.row[C][i] >> j) & 1)
+        acc = SL_BOP3(acc, y[j], wm[8 * i + j], kXorAndN);
+      else
+        acc = SL_BOP3(acc, y[j], wm[8 * i + j], kXorAnd);
+    });
+    x[i] = acc;
+  });
+}
+
+template <int K>
+struct Geo {
+  static constexpr int n = __builtin_ctz(K);
+  static constexpr int NB = n - 4;      // wave bits
+  static constexpr int NW = K / 16;     // waves
+  static_assert(K >= 16 && K <= 128 && (K & (K - 1)) == 0, "sliced encode: k = 16..128");
+};
+
+// IFFT layers m = 0 .. n-5 in layout A (wave wa), distance D = 2^m:
+// ifftDIT28 y ^= x; x ^= skew * y.  Compile-time part of the skew: element
+// k + (register block start); runtime part: W(m, wa) from wm_base[m * wstride].
+template <int K>
+__host__ __device__ __forceinline__ void ifft_A(uint32_t (&v)[16][8], const uint32_t* wm_base, int wstride) {
+  static_for<Geo<K>::NB>([&](auto m) {
+    constexpr int D = 1 << m;
+    SL_FENCE();
+    const uint32_t* wm = wm_base + m * wstride;
+    static_for<16>([&](auto j) {
+      if constexpr (!(j & D)) {
+        constexpr int c = skew_elem(D - 1 + K + (j & ~(2 * D - 1)));
+        xor8(v[j + D], v[j]);
+        muladd_rt<c>(v[j], v[j + D], wm);
+      }
+    });
+  });
+}
+
+// FFT layers m = n-5 .. 0 in layout A: fftDIT28 x ^= skew * y; y ^= x.
+template <int K>
+__host__ __device__ __forceinline__ void fft_A(uint32_t (&v)[16][8], const uint32_t* wm_base, int wstride) {
+  static_for<Geo<K>::NB>([&](auto mm) {
+    constexpr int m = Geo<K>::NB - 1 - mm;
+    constexpr int D = 1 << m;
+    SL_FENCE();
+    const uint32_t* wm = wm_base + m * wstride;
+    static_for<16>([&](auto j) {
+      if constexpr (!(j & D)) {
+        constexpr int c = skew_elem(D - 1 + (j & ~(2 * D - 1)));
+        muladd_rt<c>(v[j], v[j + D], wm);
+        xor8(v[j + D], v[j]);
+      }
+    });
+  });
+}
+
+// IFFT layers m = n-4 .. n-1 in layout B: element e = wb + NW * i, the block
+// start b = NW * (i with register bits <= m - NB cleared) -- compile-time.
+template <int K>
+__host__ __device__ __forceinline__ void ifft_B(uint32_t (&v)[16][8]) {
+  constexpr int NB = Geo<K>::NB, NW = Geo<K>::NW;
+  static_for<4>([&](auto rb) {
+    constexpr int D = 1 << (rb + NB), R = 1 << rb;
+    static_for<16>([&](auto i) {
+      if constexpr (!(i & R)) {
+        constexpr int c = skew_elem(D - 1 + K + NW * (i & ~(2 * R - 1)));
+        xor8(v[i + R], v[i]);
+        muladd_ct<c>(v[i], v[i + R]);
+      }
+    });
+  });
+}
+
+template <int K>
+__host__ __device__ __forceinline__ void fft_B(uint32_t (&v)[16][8]) {
+  constexpr int NB = Geo<K>::NB, NW = Geo<K>::NW;
+  static_for<4>([&](auto rr) {
+    constexpr int rb = 3 - rr;
+    constexpr int D = 1 << (rb + NB), R = 1 << rb;
+    static_for<16>([&](auto i) {
+      if constexpr (!(i & R)) {
+        constexpr int c = skew_elem(D - 1 + NW * (i & ~(2 * R - 1)));
+        muladd_ct<c>(v[i], v[i + R]);
+        xor8(v[i + R], v[i]);
+      }
+    });
+  });
+}
+
+}  // namespace sliced
+}  // namespace dagpu

@@ -226,6 +226,7 @@ static hipError_t launch_k(const EncodeArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_leo8_encode(int k, const EncodeArgs& a, hipStream_t s) {
+  if (leo8_sliced_applicable(k, a)) return launch_leo8_encode_sliced(k, a, s);
   switch (k) {
     case 1: return launch_k<1>(a, s);
     case 2: return launch_k<2>(a, s);

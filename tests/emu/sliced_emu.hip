@@ -1,0 +1,83 @@
+// sliced_emu.hip -- host emulation of the bit-sliced GF(2^8) encode
+// (csrc/rs_gf8_sliced.hip): the SAME per-lane transform code
+// (csrc/leo8_sliced.hpp, compiled for the host), with the kernel's loads, LDS
+// layout exchanges and stores replaced by plain loops over the NW waves of a
+// workgroup.  Test infrastructure: tests/test_sliced_emu.py compares it with
+// the oracle on the CPU, so the algorithm (layouts, skew split, matrices,
+// transposes) is checked without a GPU.
+#include <stdint.h>
+#include <string.h>
+
+#include <vector>
+
+#include "../../celestia-app_amd/csrc/leo8_sliced.hpp"
+
+using namespace dagpu::sliced;
+
+namespace {
+
+template <int K>
+void encode_chunk_lane(const uint8_t* data, uint8_t* parity, long shard, long col0) {
+  constexpr int NW = Geo<K>::NW;
+  static uint32_t st[NW][16][8], tmp[NW][16][8];
+  for (int wa = 0; wa < NW; wa++)
+    for (int j = 0; j < 16; j++) {
+      const uint8_t* src = data + (long)(16 * wa + j) * shard;
+      uint32_t d[8];
+      memcpy(d, src + col0, 16);
+      memcpy(d + 4, src + col0 + 256, 16);
+      transpose8(d);
+      memcpy(st[wa][j], d, 32);
+    }
+  for (int wa = 0; wa < NW; wa++) ifft_A<K>(st[wa], &kWMasksHost.m[0][wa][0], kMaxWav * 64);
+  for (int wb = 0; wb < NW; wb++)  // A -> B
+    for (int i = 0; i < 16; i++) {
+      const int e = wb + NW * i;
+      memcpy(tmp[wb][i], st[e >> 4][e & 15], 32);
+    }
+  for (int wb = 0; wb < NW; wb++) {
+    ifft_B<K>(tmp[wb]);
+    fft_B<K>(tmp[wb]);
+  }
+  for (int wb = 0; wb < NW; wb++)  // B -> A
+    for (int i = 0; i < 16; i++) {
+      const int e = wb + NW * i;
+      memcpy(st[e >> 4][e & 15], tmp[wb][i], 32);
+    }
+  for (int wa = 0; wa < NW; wa++) fft_A<K>(st[wa], &kWMasksHost.m[0][wa][0], kMaxWav * 64);
+  for (int wa = 0; wa < NW; wa++)
+    for (int j = 0; j < 16; j++) {
+      uint32_t d[8];
+      memcpy(d, st[wa][j], 32);
+      transpose8(d);
+      uint8_t* dst = parity + (long)(16 * wa + j) * shard;
+      memcpy(dst + col0, d, 16);
+      memcpy(dst + col0 + 256, d + 4, 16);
+    }
+}
+
+template <int K>
+int encode(long shard, const uint8_t* data, uint8_t* parity) {
+  for (long c = 0; c < shard; c += 512)
+    for (int t = 0; t < 16; t++) encode_chunk_lane<K>(data, parity, shard, c + 16 * t);
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int sliced_emu_encode(int k, long shard, const uint8_t* data, uint8_t* parity) {
+  if (shard <= 0 || shard % 512) return -1;
+  switch (k) {
+    case 16: return encode<16>(shard, data, parity);
+    case 32: return encode<32>(shard, data, parity);
+    case 64: return encode<64>(shard, data, parity);
+    case 128: return encode<128>(shard, data, parity);
+    default: return -1;
+  }
+}
+
+// bitop3 emulation and matrices, for a direct unit check
+extern "C" uint32_t sliced_emu_bop3(uint32_t a, uint32_t b, uint32_t c, int tt) {
+  return sl_bop3_host(a, b, c, (uint8_t)tt);
+}
+extern "C" int sliced_emu_gmul(int a, int c) { return gmul((uint8_t)a, (uint8_t)c); }

@@ -11,7 +11,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "celestia-app_a
 from celestia_da import da, synth  # noqa: E402
 from celestia_da.device import DeviceSquares  # noqa: E402
 
-k, B = 128, 64
+k = 128
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 ctx = da.Context(0)
 host = np.stack([synth.random_blob_square(k, i).reshape(-1) for i in range(8)])
 for S in (1, 2, 4, 8):
