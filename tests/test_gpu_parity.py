@@ -183,6 +183,49 @@ def test_codec_encode_matches_oracle(ctx, k, shard):
         assert (par[v] == oracle.encode(data[v])).all()
 
 
+@pytest.mark.parametrize("k", [16, 32, 64, 128])
+@pytest.mark.parametrize("shard", [512, 1024])
+def test_codec_encode_sliced_shapes(ctx, k, shard):
+    """Vector counts that are multiples of 4 and whole 512-B chunks take the
+    bit-sliced kernel (rs_gf8_sliced.hip) through the codec entry too."""
+    rng = np.random.default_rng(k + shard)
+    data = rng.integers(0, 256, (8, k, shard), dtype=np.uint8)
+    par = da.LeoRSCodec(ctx).encode_batch(data)
+    for v in range(8):
+        assert (par[v] == oracle.encode(data[v])).all()
+
+
+_PACKED_CHILD = r"""
+import hashlib, sys
+sys.path[:0] = sys.argv[1:3]
+from celestia_da import da, synth
+ctx = da.Context(0)
+for k in (16, 32, 64, 128):
+    eds = da.extend_shares(synth.random_blob_square(k, 100 + k), ctx)
+    print(k, hashlib.sha256(eds.data.tobytes()).hexdigest())
+ctx.close()
+"""
+
+
+def test_packed_and_sliced_encoders_agree(ctx):
+    """The packed-byte encoder (DAGPU_ENC_SLICED=0, read once per process, so
+    in a child process) and the default bit-sliced encoder give the same EDS."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DAGPU_ENC_SLICED="0")
+    out = subprocess.run([sys.executable, "-c", _PACKED_CHILD, os.path.join(root, "celestia-app_amd"),
+                          os.path.join(root, "oracle")], env=env, capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    packed = dict(line.split() for line in out.stdout.split("\n") if line.strip() and line.split()[0].isdigit())
+    assert len(packed) == 4
+    for k in (16, 32, 64, 128):
+        eds = da.extend_shares(synth.random_blob_square(k, 100 + k), ctx)
+        assert sha(eds.data.tobytes()) == packed[str(k)], k
+
+
 def test_codec_fixture(ctx):
     rng = np.random.default_rng(7)
     codec = da.LeoRSCodec(ctx)
