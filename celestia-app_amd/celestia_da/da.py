@@ -97,6 +97,34 @@ class Context:
             raise cls(rc, self.last_error())
 
 
+class PinnedBuffer:
+    """Page-locked host memory from dagpu_host_alloc (include/dagpu.h), viewed
+    as a flat numpy uint8 array: the input buffer a block-replay caller hands
+    to dagpu_extend_batch so its chunked host->device copies run at PCIe speed."""
+
+    def __init__(self, nbytes: int):
+        self._L = _abi.lib()
+        self.nbytes = int(nbytes)
+        p = self._L.dagpu_host_alloc(max(self.nbytes, 1))
+        if not p:
+            raise MemoryError(f"dagpu_host_alloc({self.nbytes}) failed")
+        self.ptr = p
+        raw = (ctypes.c_uint8 * max(self.nbytes, 1)).from_address(p)
+        self.array = np.frombuffer(raw, dtype=np.uint8)[:self.nbytes]
+
+    def close(self) -> None:
+        if self.ptr:
+            self.array = None
+            self._L.dagpu_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 _default_ctx: Optional[Context] = None
 _default_lock = threading.Lock()
 

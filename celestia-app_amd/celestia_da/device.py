@@ -55,6 +55,21 @@ class DeviceSquares:
             _abi.addr(self.row_roots), _abi.addr(self.col_roots), _abi.addr(self.dah),
             _abi.addr(self.status), _abi.addr(self.workspace), _stream_handle(stream)))
 
+    def extend_from(self, ods: torch.Tensor, stream: Optional[torch.cuda.Stream] = None) -> int:
+        """Extend the first m = ods.shape[0] (<= n) squares taking their ODS
+        from `ods` ((m, k*k*512) uint8 on this device, e.g. a window of a
+        resident block-replay shard) instead of self.ods.  Returns m."""
+        m = int(ods.shape[0])
+        if m > self.n or ods.dtype != torch.uint8 or ods.device != self.eds.device \
+                or not ods.is_contiguous() or ods.numel() != m * self.k * self.k * 512:
+            raise ValueError("ods must be a contiguous (m <= n, k*k*512) uint8 tensor on this device")
+        L = self.ctx._L
+        self._ck(L.dagpu_extend_batch_device(
+            self.ctx.handle, self.k, m, _abi.addr(ods), _abi.addr(self.eds),
+            _abi.addr(self.row_roots), _abi.addr(self.col_roots), _abi.addr(self.dah),
+            _abi.addr(self.status), _abi.addr(self.workspace), _stream_handle(stream)))
+        return m
+
     def extend_rs(self, stream: Optional[torch.cuda.Stream] = None) -> None:
         self._ck(self.ctx._L.dagpu_extend_rs_device(
             self.ctx.handle, self.k, self.n, _abi.addr(self.ods), _abi.addr(self.eds),

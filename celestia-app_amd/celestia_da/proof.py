@@ -26,6 +26,7 @@ re-derive every row root and the data root from the proofs).
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import math
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Tuple
@@ -35,6 +36,10 @@ import numpy as np
 from . import _abi
 from .da import Context, DAError, default_context, extend_shares, new_data_availability_header
 from .inclusion import EDSSubTreeRootCacher
+
+
+# crypto/merkle MaxAunts (celestia-core v0.34 crypto/merkle/proof.go)
+MAX_AUNTS = 100
 
 
 @dataclass
@@ -54,6 +59,13 @@ class MerkleProof:
             raise DAError(_abi.ERR_PROOF, "proof total must be positive")
         if self.index < 0:
             raise DAError(_abi.ERR_PROOF, "proof index cannot be negative")
+        # Proof.ValidateBasic's MaxAunts bound, and Verify's LeafHash check
+        if len(self.aunts) > MAX_AUNTS:
+            raise DAError(_abi.ERR_PROOF, f"expected no more than {MAX_AUNTS} aunts, got {len(self.aunts)}")
+        want_leaf = hashlib.sha256(b"\x00" + bytes(leaf)).digest()
+        if bytes(self.leaf_hash) != want_leaf:
+            raise DAError(_abi.ERR_PROOF, f"invalid leaf hash: wanted {want_leaf.hex().upper()} "
+                                          f"got {bytes(self.leaf_hash).hex().upper()}")
         # keep every buffer referenced until the call returns (addr() is a raw pointer)
         r, lf, au = _bytes(root), _bytes(leaf), _bytes(b"".join(self.aunts))
         rc = _abi.lib().dagpu_merkle_verify(_abi.addr(r), _abi.addr(lf), len(leaf), self.index, self.total,

@@ -8,7 +8,7 @@ pkg/square:
   inclusion.BlobMinSquareSize                            pkg/inclusion/blob_share_commitment_rules.go:76
 
 The square this produces is the ODS the GPU path extends: `square_bytes()`
-feeds `da.extend_shares` / `device.DeviceBatch`, and blob commitments can be
+feeds `da.extend_shares` / `device.DeviceSquares`, and blob commitments can be
 read back from the GPU-built EDS with `inclusion.get_commitment`.
 
 `Deconstruct` needs the blob sizes of each PFB; the reference decodes the

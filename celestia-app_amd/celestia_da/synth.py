@@ -42,6 +42,44 @@ def sort_shares(s: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(s[order])
 
 
+_FAST = None
+
+
+def _fast_lib():
+    """libdasynth.so (csrc/synth.cpp): the multithreaded generator for large
+    runs of distinct squares (block replay, the 4096-square mixed batch)."""
+    global _FAST
+    if _FAST is None:
+        import ctypes
+        import os
+        path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "libdasynth.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run `make -C celestia-app_amd` (or __graft_entry__.build())")
+        lib = ctypes.CDLL(path)
+        lib.dasynth_blob_squares.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
+                                             ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int]
+        lib.dasynth_blob_squares.restype = ctypes.c_int
+        _FAST = lib
+    return _FAST
+
+
+def blob_squares(k: int, seed: int, first: int, count: int, out: np.ndarray = None,
+                 threads: int = 0) -> np.ndarray:
+    """Squares first..first+count-1 of the seeded run `seed` (random blob
+    shares, sorted; see csrc/synth.cpp), as (count, k*k*512) uint8.  Square i
+    is the same bytes whichever (first, count) window produces it.  `out` may
+    be a caller buffer (e.g. page-locked) of at least that many bytes."""
+    n = count * k * k * SHARE
+    if out is None:
+        out = np.empty((count, k * k * SHARE), np.uint8)
+    if out.nbytes < n or not out.flags["C_CONTIGUOUS"]:
+        raise ValueError("out must be a contiguous buffer of count*k*k*512 bytes")
+    rc = _fast_lib().dasynth_blob_squares(k, seed, first, count, out.ctypes.data, threads)
+    if rc != 0:
+        raise ValueError("dasynth_blob_squares: bad argument")
+    return out.reshape(-1)[:n].reshape(count, k * k * SHARE)
+
+
 def constant_square(k: int) -> np.ndarray:
     ns = bytes([0]) + bytes(18) + bytes([1] * 10)
     share = ns + b"\xff" * (SHARE - len(ns))

@@ -34,8 +34,10 @@ size_t eds_bytes(uint64_t k) { return 4ull * k * k * kSS; }
 size_t ods_bytes(uint64_t k) { return 1ull * k * k * kSS; }
 
 // RS extension of n squares (uniform k), device pointers.
+// ev_rows (optional) is recorded between the row and the column pass: rows
+// 0..k-1 of every EDS ([Q0|Q1]) are final from that point on.
 int enqueue_rs(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_ods, uint8_t* d_eds,
-               hipStream_t s) {
+               hipStream_t s, hipEvent_t ev_rows = nullptr) {
   const long w = 2L * k;
   const long esq = (long)eds_bytes(k);
   EncodeArgs ra{};
@@ -68,6 +70,7 @@ int enqueue_rs(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_ods, uint8
     ProfScope p(ctx, 0, s);
     HIP_TRY(ctx, launch_rs_encode((int)k, ra, s));
   }
+  if (ev_rows) HIP_TRY(ctx, hipEventRecord(ev_rows, s));
   // Column pass: vector c = column c of [Q0|Q1] -> [Q2|Q3].
   EncodeArgs ca{};
   ca.in = d_eds;
@@ -233,14 +236,27 @@ int run_group_host(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* ods, uin
   HIP_TRY(ctx, ctx->status.ensure(sizeof(int32_t) * n));
   HIP_TRY(ctx, ctx->ws.ensure(dagpu_workspace_size(k, n)));
   HIP_TRY(ctx, hipMemcpyAsync(ctx->ods.p, ods, ods_bytes(k) * n, hipMemcpyHostToDevice, s));
-  rc = enqueue_rs(ctx, k, n, (const uint8_t*)ctx->ods.p, (uint8_t*)ctx->eds.p, s);
+  // An EDS requested back goes down on the copy stream while the kernels run:
+  // the top halves ([Q0|Q1], final after the row pass) during the column pass
+  // and the NMT kernels, the bottom halves ([Q2|Q3]) during the NMT kernels.
+  rc = enqueue_rs(ctx, k, n, (const uint8_t*)ctx->ods.p, (uint8_t*)ctx->eds.p, s,
+                  eds_out ? ctx->ev_loaded[0] : nullptr);
   if (rc) return rc;
+  hipStream_t cs = ctx->copy_stream;
+  const size_t eb = eds_bytes(k), half = eb / 2;
+  if (eds_out) {
+    HIP_TRY(ctx, hipEventRecord(ctx->ev_loaded[1], s));
+    HIP_TRY(ctx, hipStreamWaitEvent(cs, ctx->ev_loaded[0], 0));
+    HIP_TRY(ctx, hipMemcpy2DAsync(eds_out, eb, ctx->eds.p, eb, half, n, hipMemcpyDeviceToHost, cs));
+    HIP_TRY(ctx, hipStreamWaitEvent(cs, ctx->ev_loaded[1], 0));
+    HIP_TRY(ctx, hipMemcpy2DAsync(eds_out + half, eb, (const uint8_t*)ctx->eds.p + half, eb, half, n,
+                                  hipMemcpyDeviceToHost, cs));
+  }
   rc = enqueue_roots(ctx, k, n, (const uint8_t*)ctx->eds.p, (uint8_t*)ctx->rr.p,
                      (uint8_t*)ctx->cr.p, (uint8_t*)ctx->dah.p, (int32_t*)ctx->status.p,
                      ctx->ws.p, s);
   if (rc) return rc;
-  if (eds_out)
-    HIP_TRY(ctx, hipMemcpyAsync(eds_out, ctx->eds.p, eds_bytes(k) * n, hipMemcpyDeviceToHost, s));
+  if (eds_out) HIP_TRY(ctx, hipStreamSynchronize(cs));
   HIP_TRY(ctx, hipMemcpyAsync(rr, ctx->rr.p, w * kNodeSize * n, hipMemcpyDeviceToHost, s));
   HIP_TRY(ctx, hipMemcpyAsync(cr, ctx->cr.p, w * kNodeSize * n, hipMemcpyDeviceToHost, s));
   HIP_TRY(ctx, hipMemcpyAsync(dah, ctx->dah.p, 32 * n, hipMemcpyDeviceToHost, s));
@@ -281,6 +297,7 @@ int dagpu_init(int device, dagpu_ctx** out) {
 
 void dagpu_destroy(dagpu_ctx* c) {
   if (!c) return;
+  if (thread_err().ctx == c) thread_err() = ThreadErr{};
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
@@ -319,7 +336,19 @@ int dagpu_host_unregister(void* p) {
   return hipHostUnregister(p) == hipSuccess ? DAGPU_OK : DAGPU_ERR_DEVICE;
 }
 
-const char* dagpu_last_error(dagpu_ctx* c) { return c ? c->err.c_str() : "null context"; }
+// The message of this thread's last failure on `c`; if this thread has not
+// failed on `c`, a snapshot of the context's most recent message.  The pointer
+// stays valid until this thread's next call into the library.
+const char* dagpu_last_error(dagpu_ctx* c) {
+  if (!c) return "null context";
+  ThreadErr& t = thread_err();
+  if (t.ctx == c && t.own) return t.msg.c_str();
+  std::lock_guard<std::mutex> g(c->err_mu);
+  t.ctx = c;
+  t.own = false;
+  t.msg = c->err;
+  return t.msg.c_str();
+}
 
 size_t dagpu_workspace_size(uint32_t k, size_t n) {
   if (k == 0 || n == 0) return 256;

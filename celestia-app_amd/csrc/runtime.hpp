@@ -63,6 +63,10 @@ struct dagpu_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::mutex mu;
+  // Last error message.  Device-resident entry points run without `mu`
+  // (several host threads may enqueue on one context, each on its own
+  // stream), so the message has its own lock; see set_err / dagpu_last_error.
+  std::mutex err_mu;
   std::string err;
   DevBuf ods, eds, rr, cr, dah, status, ws;
   // host-mode pipeline (dagpu.cpp run_group_pipelined): H2D on copy_stream,
@@ -85,8 +89,29 @@ constexpr size_t kSS = dagpu::kShareSize;
 
 inline bool is_pow2(uint64_t v) { return v != 0 && (v & (v - 1)) == 0; }
 
+// The calling thread's own last failure (errno-like), so that a thread that
+// just failed reads its own message even while another thread fails on the
+// same context.
+struct ThreadErr {
+  const dagpu_ctx* ctx = nullptr;
+  bool own = false;  // msg is this thread's own failure (not a snapshot)
+  std::string msg;
+};
+inline ThreadErr& thread_err() {
+  static thread_local ThreadErr t;
+  return t;
+}
+
 inline int set_err(dagpu_ctx* c, int code, const std::string& msg) {
-  if (c) c->err = msg;
+  if (!c) return code;
+  {
+    std::lock_guard<std::mutex> g(c->err_mu);
+    c->err = msg;
+  }
+  ThreadErr& t = thread_err();
+  t.ctx = c;
+  t.own = true;
+  t.msg = msg;
   return code;
 }
 

@@ -19,8 +19,12 @@
  *
  * Errors: functions return 0 or a negative dagpu_status; batch calls also
  * fill a per-square status array.  dagpu_last_error() gives the message of the
- * last failure on that context (same wording as the reference where one
- * exists).  A context is thread-safe: host-memory calls are serialised on it.
+ * calling thread's last failure on that context (errno-like; a thread that has
+ * not failed on it gets the context's most recent message), same wording as
+ * the reference where one exists.
+ * Threading: a context is thread-safe.  Host-memory calls are serialised on
+ * it; device-resident (*_device) calls take no lock and may be issued from
+ * several threads at once, each on its own stream with its own buffers.
  */
 #ifndef DAGPU_H
 #define DAGPU_H

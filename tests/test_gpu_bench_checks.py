@@ -1,0 +1,173 @@
+"""GPU tests of the configs[2] and configs[4] workloads at full size and of the
+bench's cross-rank checks:
+
+* the seeded 4096-square mixed batch (k = 2^u, u in 0..7, every square
+  distinct) through the device-resident path, per k group: every DAH equals
+  the host API's, two sampled squares per k bit-exact against the oracle;
+* the block-replay rehearsal: bench.py under torch.distributed.run with 2
+  ranks sharing GPU 0 (DAGPU_BENCH_SHARED_GPU=1, gloo collectives) replays
+  distinct squares host-streamed and device-resident, and the sampled DAHs it
+  reports match the oracle;
+* a deliberately wrong DAH (DAGPU_BENCH_CORRUPT) after the gather, inside a
+  rank's own results, or in the split square makes bench.py exit non-zero;
+* two host threads issuing device-resident calls on ONE context, one of them
+  failing on purpose: both results intact, the failing thread reads its own
+  error message (include/dagpu.h threading contract).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from celestia_da import _abi, da, synth
+from celestia_da.device import DeviceSquares
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = da.Context(0)
+    yield c
+    c.close()
+
+
+def test_mixed_batch_full_size(ctx):
+    """configs[2]: 4096 distinct squares, the bench's own input (bench.mixed_batch)."""
+    import bench
+
+    ks, groups, hosts = bench.mixed_batch(ctx)
+    assert len(ks) == 4096 and set(ks) == {1, 2, 4, 8, 16, 32, 64, 128}
+    for ds in groups.values():
+        ds.extend()
+    torch.cuda.synchronize()
+    for k, ds in groups.items():
+        st = ds.status.cpu().numpy()
+        dah = ds.dah.cpu().numpy()
+        assert (st == 0).all(), k
+        assert len({d.tobytes() for d in dah}) == ds.n, k  # distinct squares
+        _, _, _, hdah, hst = da.extend_batch(hosts[k].reshape(-1), [k] * ds.n, ctx)
+        assert (hst == 0).all() and (hdah == dah).all(), k
+        for i in (0, ds.n - 1):
+            _, orr, ocr, odah = oracle.extend_and_dah(hosts[k][i].reshape(k * k, 512), k, nthreads=16,
+                                                      want_eds=False)
+            assert dah[i].tobytes() == odah, (k, i)
+            assert (ds.row_roots[i].cpu().numpy() == orr).all() and (ds.col_roots[i].cpu().numpy() == ocr).all()
+    del groups
+    torch.cuda.empty_cache()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run_bench(args, corrupt=None, timeout=110):
+    env = dict(os.environ, DAGPU_BENCH_SHARED_GPU="1", MASTER_ADDR="127.0.0.1")
+    if corrupt:
+        env["DAGPU_BENCH_CORRUPT"] = corrupt
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2"] + args
+    return subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+
+
+_REPLAY = ["--steps", "2", "--warmup", "1", "--batch", "8", "--replay-blocks", "40", "--no-cpu",
+           "--no-split"]
+
+
+def test_replay_rehearsal_two_ranks(tmp_path):
+    dump = str(tmp_path / "replay.json")
+    out = _run_bench(_REPLAY + ["--replay-dump", dump])
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
+    rep = line["block_replay"]
+    assert rep["bit_exact"] is True and rep["distinct_squares"] == 40 and rep["per_rank"] == 20
+    assert rep["host_streamed"]["squares_per_s"] > 0 and rep["device_resident"]["squares_per_s"] > 0
+    d = json.load(open(dump))
+    k, seed = d["k"], d["seed"]
+    assert sorted(int(b) for b in d["sampled_dah"]) == [0, 19, 20, 39]
+    for b, hexdah in d["sampled_dah"].items():
+        sq = synth.blob_squares(k, seed, int(b), 1)[0].reshape(k * k, 512)
+        _, _, _, odah = oracle.extend_and_dah(sq, k, nthreads=16, want_eds=False)
+        assert odah.hex() == hexdah, b
+
+
+@pytest.mark.parametrize("corrupt", ["replay-gather", "replay-compute"])
+def test_replay_corruption_is_fatal(corrupt):
+    out = _run_bench(_REPLAY, corrupt=corrupt)
+    assert out.returncode != 0
+    assert "FATAL: block replay DAH check failed" in out.stderr
+    assert not [x for x in out.stdout.splitlines() if x.startswith("{")]
+
+
+def test_split_corruption_is_fatal():
+    out = _run_bench(["--mode", "split", "--split-k", "16", "--steps", "1", "--warmup", "1"],
+                     corrupt="split")
+    assert out.returncode != 0
+    assert "FATAL: split square k=16" in out.stderr
+
+
+def test_two_threads_one_context(ctx):
+    """Device-resident calls from two host threads on one context, each on its
+    own stream; thread B fails on purpose (k = 3, then k = 4096) on every
+    iteration while thread A extends squares."""
+    L = ctx._L
+    k, n = 32, 6
+    ods = synth.blob_squares(k, 31337, 0, n)
+    _, _, _, want, _ = da.extend_batch(ods.reshape(-1), [k] * n, ctx)
+    ds = DeviceSquares(k, n, ctx=ctx)
+    ds.ods.copy_(torch.from_numpy(ods))
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    errors = []
+    iters = 200
+    results = {}
+
+    def worker_a():
+        try:
+            for _ in range(iters // 10):
+                ds.extend(sa)
+            sa.synchronize()
+            results["a"] = ds.dah.cpu().numpy().copy()
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(("a", repr(e)))
+
+    def worker_b():
+        try:
+            for i in range(iters):
+                bad_k = 3 if i % 2 == 0 else 4096
+                rc = L.dagpu_extend_batch_device(ctx.handle, bad_k, 1, _abi.addr(ds.ods), _abi.addr(ds.eds),
+                                                 _abi.addr(ds.row_roots), _abi.addr(ds.col_roots),
+                                                 _abi.addr(ds.dah), _abi.addr(ds.status),
+                                                 _abi.addr(ds.workspace), int(sb.cuda_stream))
+                msg = L.dagpu_last_error(ctx.handle).decode()
+                if bad_k == 3:
+                    ok = rc == _abi.ERR_ARG and msg == "square width must be a power of two"
+                else:
+                    ok = rc == _abi.ERR_UNSUPPORTED and msg.startswith("square width k > ")
+                if not ok:
+                    errors.append(("b", i, rc, msg))
+                    return
+        except Exception as e:  # pragma: no cover
+            errors.append(("b", repr(e)))
+
+    ta, tb = threading.Thread(target=worker_a), threading.Thread(target=worker_b)
+    ta.start()
+    tb.start()
+    ta.join(timeout=100)
+    tb.join(timeout=100)
+    assert not errors, errors
+    assert (results["a"] == want).all()
+    assert (ds.status.cpu().numpy() == 0).all()

@@ -271,37 +271,6 @@ def test_device_batch_full_size(ctx):
 
 # --- decode / Repair (rsmt2d Repair, klauspost Reconstruct) -------------------
 
-def test_extend_batch_pipelined(ctx, monkeypatch):
-    """Host mode splits a large uniform batch into chunks: H2D of chunk c on the
-    copy stream while chunk c-1 is extended (dagpu.cpp run_group_pipelined).
-    Many small chunks (chunk override) and the default 16-square chunks at
-    k=128 must give what the single-shot path gives; a push-order violation in
-    a middle chunk is reported for that square only."""
-    k, n = 8, 37
-    ods = np.stack([synth.random_blob_square(k, 900 + i).reshape(-1) for i in range(n)])
-    ods[20].reshape(k * k, 512)[[0, 1]] = ods[20].reshape(k * k, 512)[[1, 0]]
-    monkeypatch.setenv("DAGPU_PIPELINE_CHUNK", "100000")
-    ref = da.extend_batch(ods.reshape(-1), [k] * n, ctx, want_eds=True)
-    monkeypatch.setenv("DAGPU_PIPELINE_CHUNK", "5")
-    got = da.extend_batch(ods.reshape(-1), [k] * n, ctx, want_eds=True)
-    got2 = da.extend_batch(ods.reshape(-1), [k] * n, ctx, want_eds=False)
-    assert (got[0] == ref[0]).all()
-    for a, b in ((got[1], ref[1]), (got[2], ref[2]), (got2[1], ref[1])):
-        assert all((x == y).all() for x, y in zip(a, b))
-    assert (got[3] == ref[3]).all() and (got2[3] == ref[3]).all()
-    assert list(np.nonzero(got[4])[0]) == [20] and (got[4] == ref[4]).all()
-    _, orr, ocr, odah = oracle.extend_and_dah(ods[36], k)
-    assert got[3][36].tobytes() == odah
-    monkeypatch.delenv("DAGPU_PIPELINE_CHUNK")
-    k, n = 128, 40  # default chunk: 16 squares (128 MiB) -> 3 chunks
-    host = np.stack([synth.random_blob_square(k, 8000 + (i % 5)).reshape(-1) for i in range(n)])
-    _, _, _, hdah, st = da.extend_batch(host.reshape(-1), [k] * n, ctx)
-    assert (st == 0).all()
-    for i in range(5):
-        _, _, _, odah = oracle.extend_and_dah(host[i], k, nthreads=8, want_eds=False)
-        assert all(hdah[j].tobytes() == odah for j in range(i, n, 5))
-
-
 @pytest.mark.parametrize("k", [1, 2, 4, 8, 16, 32, 64, 128])
 @pytest.mark.parametrize("shard", [64, 512, 1536])
 def test_codec_decode_matches_oracle(ctx, k, shard):

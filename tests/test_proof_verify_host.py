@@ -101,6 +101,17 @@ def test_merkle_verify(n):
             proof.MerkleProof(n, i, p.leaf_hash, aunts).verify(root, items[i])
         with pytest.raises(da.DAError):
             proof.MerkleProof(n, -1, p.leaf_hash, p.aunts).verify(root, items[i])
+        # Proof.Verify compares the proof's own LeafHash with leafHash(leaf)
+        with pytest.raises(da.DAError, match="invalid leaf hash"):
+            proof.MerkleProof(n, i, bytes(32), p.aunts).verify(root, items[i])
+
+
+def test_merkle_verify_max_aunts():
+    import hashlib
+    leaf = b"x"
+    p = proof.MerkleProof(2, 0, hashlib.sha256(b"\x00" + leaf).digest(), [bytes(32)] * 101)
+    with pytest.raises(da.DAError, match="no more than 100 aunts"):
+        p.verify(bytes(32), leaf)
 
 
 def test_parse_namespace():

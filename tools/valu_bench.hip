@@ -29,8 +29,10 @@ __global__ __launch_bounds__(256) void op_kernel(uint32_t* out, int iters, uint3
 #pragma unroll
       for (int i = 0; i < 16; i++) {
         uint32_t x = v[i];
-        if constexpr (OP == XOR) x = x ^ v[(i + 3) & 15];
-        if constexpr (OP == ADD) x = x + v[(i + 3) & 15];
+        // xor/add chains go through inline asm: plain C lets the compiler fold
+        // the 8 rounds algebraically (r01 reported v_xor_b32 above the issue peak)
+        if constexpr (OP == XOR) asm volatile("v_xor_b32 %0, %1, %2" : "=v"(x) : "v"(x), "v"(v[(i + 3) & 15]));
+        if constexpr (OP == ADD) asm volatile("v_add_u32 %0, %1, %2" : "=v"(x) : "v"(x), "v"(v[(i + 3) & 15]));
         if constexpr (OP == ALIGNBIT) x = __builtin_amdgcn_alignbit(x, v[(i + 3) & 15], 7);
         if constexpr (OP == BITOP3) x = __builtin_amdgcn_bitop3_b32(x, v[(i + 3) & 15], v[(i + 7) & 15], 0x96);
         if constexpr (OP == ADD3) x = x + v[(i + 3) & 15] + v[(i + 7) & 15];
