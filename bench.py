@@ -103,29 +103,59 @@ def all_gather_rows(dist, world, t):
     return allg
 
 
-def cpu_baseline(k: int, seconds: float, threads: int):
-    """CPU oracle (oracle/da_oracle.c, OpenSSL SHA-256) on host cores: a bounded
-    sample of the same workload (random-blob k x k squares, ExtendShares + DAH)."""
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(seconds: float, threads: int):
+    """CPU baseline on the host cores (BASELINE.md fallback for the Go path
+    pkg/da/data_availability_header.go:44-75, which cannot be built here):
+    oracle/da_simd.c -- GFNI/AVX-512 (or AVX2 PSHUFB) GF(2^8) mul-add with
+    per-constant tables built once, x86 SHA extensions, the reference's work
+    (each leaf hashed in its row and its column tree), rows/columns/trees over
+    `threads` OpenMP threads.  Timed on configs[1] (k=128, the headline's unit)
+    and configs[0] (k=64) random-blob squares, `seconds` each; the EDS is
+    written to host memory as ExtendShares returns it."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     from celestia_da import synth
 
-    ods = [synth.random_blob_square(k, 90000 + i) for i in range(4)]
-    oracle.extend_and_dah(ods[0], k, nthreads=threads, want_eds=False)  # warm
-    n, t0 = 0, time.perf_counter()
-    while True:
-        oracle.extend_and_dah(ods[n % len(ods)], k, nthreads=threads, want_eds=False)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or n >= 200:
-            break
+    res = {}
+    for k in (128, 64):
+        ods = synth.blob_squares(k, 90000 + k, 0, 4, threads=threads)
+        sq = oracle.SimdSquare(k)
+        sq.run(ods[0], threads)  # warm
+        n, t0 = 0, time.perf_counter()
+        while True:
+            sq.run(ods[n % len(ods)], threads)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+        res[k] = (n, el)
+    n, el = res[128]
+    n64, el64 = res[64]
     return {
         "value": n / el,
         "unit": "squares/s",
         "cores": threads,
-        "kind": "port",
-        "sample": f"{n} random-blob {k}x{k} squares, ExtendShares+NewDataAvailabilityHeader "
-                  f"(C restatement, {threads} pthreads, {el:.1f} s wall)",
+        "kind": "simd-port",
+        "k": 128,
+        "cpu_model": cpu_model(),
+        "host_cpus_visible": os.cpu_count(),
+        "isa": oracle.simd_isa(),
+        "sample": f"{n} random-blob 128x128 squares, ExtendShares+NewDataAvailabilityHeader "
+                  f"(oracle/da_simd.c, {threads} threads, {el:.1f} s wall; leaves hashed per row and "
+                  f"column tree as the reference does)",
+        "configs0_k64": {"squares_per_s": n64 / el64, "ms_per_square": el64 / n64 * 1e3,
+                         "sample": f"{n64} random-blob 64x64 squares, {el64:.1f} s wall"},
+        "note": "C restatement of the Go path (no Go toolchain here), not the Go reference itself",
     }
 
 
@@ -149,8 +179,8 @@ def main():
     ap.add_argument("--batch", type=int, default=256,
                     help="squares per GPU per step (SURVEY.md §8d: C2 batches of >= 256 squares)")
     ap.add_argument("--distinct", type=int, default=256, help="distinct generated squares per GPU")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time per k (64 and 128)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = all usable host cores)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--mode", choices=["extend", "mixed", "repair", "split"], default="extend",
                     help="extend: configs[1] (headline); mixed: configs[2]; repair: configs[3]; "
@@ -294,7 +324,7 @@ def main():
                                       max(3, args.steps // 4))
         out["end_to_end"]["single_square"] = bench_single(ctx)
     if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(k, args.cpu_seconds, args.cpu_threads)
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.cpu_threads or host_threads())
         out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
     if world > 1 and not args.no_split:
         # configs[4] stress: one oversized square split over all ranks (RCCL all-to-all)

@@ -247,9 +247,12 @@ int run_group_host(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* ods, uin
   if (eds_out) {
     HIP_TRY(ctx, hipEventRecord(ctx->ev_loaded[1], s));
     HIP_TRY(ctx, hipStreamWaitEvent(cs, ctx->ev_loaded[0], 0));
-    HIP_TRY(ctx, hipMemcpy2DAsync(eds_out, eb, ctx->eds.p, eb, half, n, hipMemcpyDeviceToHost, cs));
+    const uint8_t* d = (const uint8_t*)ctx->eds.p;
+    for (size_t i = 0; i < n; i++)  // plain 1D copies: the DMA engines' fast path
+      HIP_TRY(ctx, hipMemcpyAsync(eds_out + i * eb, d + i * eb, half, hipMemcpyDeviceToHost, cs));
     HIP_TRY(ctx, hipStreamWaitEvent(cs, ctx->ev_loaded[1], 0));
-    HIP_TRY(ctx, hipMemcpy2DAsync(eds_out + half, eb, (const uint8_t*)ctx->eds.p + half, eb, half, n,
+    for (size_t i = 0; i < n; i++)
+      HIP_TRY(ctx, hipMemcpyAsync(eds_out + i * eb + half, d + i * eb + half, half,
                                   hipMemcpyDeviceToHost, cs));
   }
   rc = enqueue_roots(ctx, k, n, (const uint8_t*)ctx->eds.p, (uint8_t*)ctx->rr.p,

@@ -204,3 +204,40 @@ def nmt_root(leaf_nodes) -> bytes:
         a = _u8(b"".join(leaf_nodes))
         lib().orc_nmt_root_from_leaves(_p(a), len(leaf_nodes), _p(out))
     return out.tobytes()
+
+
+# --- SIMD CPU baseline (da_simd.c; bench.py cpu_baseline "simd-port") ---------
+
+def simd_lib() -> ctypes.CDLL:
+    if "simd" not in _libs:
+        path = os.path.join(_BUILD, "libda_simd.so")
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        L.simd_isa.restype = ctypes.c_char_p
+        L.simd_extend_and_dah.argtypes = [ctypes.c_int, u8p, u8p, u8p, u8p, u8p, ctypes.c_int]
+        _libs["simd"] = L
+    return _libs["simd"]
+
+
+def simd_isa() -> str:
+    return simd_lib().simd_isa().decode()
+
+
+class SimdSquare:
+    """Reusable buffers for simd_extend_and_dah (the EDS the Go path returns)."""
+
+    def __init__(self, k: int):
+        w = 2 * k
+        self.k = k
+        self.eds = np.empty((w, w, SHARE_SIZE), np.uint8)
+        self.rr = np.empty((w, NODE_SIZE), np.uint8)
+        self.cr = np.empty((w, NODE_SIZE), np.uint8)
+        self.dah = np.empty(32, np.uint8)
+
+    def run(self, ods: np.ndarray, nthreads: int):
+        o = _u8(ods)
+        _check(simd_lib().simd_extend_and_dah(self.k, _p(o), _p(self.eds), _p(self.rr), _p(self.cr),
+                                              _p(self.dah), nthreads))
+        return self.eds, self.rr, self.cr, self.dah.tobytes()

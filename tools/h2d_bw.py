@@ -36,6 +36,10 @@ def main():
                     dev[i * step:(i + 1) * step].copy_(host[i * step:(i + 1) * step], non_blocking=True)
         t = timed(go)
         print(json.dumps({"variant": f"h2d_{chunks}_streams", "GBps": n / t / 1e9}), flush=True)
+    for mib in (8, 32, 256):  # one EDS (k=64: 8 MiB, k=128: 32 MiB) back to pinned memory
+        m = mib << 20
+        t = timed(lambda: host[:m].copy_(dev[:m], non_blocking=True))
+        print(json.dumps({"variant": f"d2h_{mib}MiB_pinned", "GBps": m / t / 1e9, "ms": t * 1e3}), flush=True)
     t = timed(lambda: back.copy_(dev[:back.numel()], non_blocking=True))
     print(json.dumps({"variant": "d2h_roots_batch", "GBps": back.numel() / t / 1e9, "ms": t * 1e3}), flush=True)
 
