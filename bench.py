@@ -182,6 +182,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time per k (64 and 128)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = all usable host cores)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--in-place", action="store_true",
+                    help="ODS resident in Q0 of the EDS buffer (dagpu_extend_batch_device with d_ods = NULL)")
     ap.add_argument("--mode", choices=["extend", "mixed", "repair", "split"], default="extend",
                     help="extend: configs[1] (headline); mixed: configs[2]; repair: configs[3]; "
                          "split: configs[4] oversized square over all ranks")
@@ -209,13 +211,12 @@ def main():
 
     k, B = args.k, args.batch
     ctx = da.Context(local)
-    ds = DeviceSquares(k, B, device=local, ctx=ctx)
+    ds = DeviceSquares(k, B, device=local, ctx=ctx, in_place=args.in_place)
     # distinct synthetic squares (seeded run, rank r takes squares r*B ..), replicated
     # up to the batch size if --distinct is smaller
     nd = min(args.distinct, B)
     host = synth.blob_squares(k, HEADLINE_SEED, rank * B, nd, threads=host_threads())
-    for i in range(B):
-        ds.ods[i].copy_(torch.from_numpy(host[i % nd]), non_blocking=False)
+    ds.load_ods(np.stack([host[i % nd] for i in range(B)]))
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream()
@@ -306,6 +307,7 @@ def main():
             "squares_per_gpu_per_step": B,
             "global_batch": B * world,
             "parallelism": f"squares sharded over {world} GPU(s), no collective",
+            "ods_layout": "in place (Q0 of the EDS buffer)" if args.in_place else "separate ODS buffer",
         },
         "rs_gbs": rs_gbs,
         "nmt_sha256_compressions_per_s": comp_per_s,

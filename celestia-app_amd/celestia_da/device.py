@@ -29,12 +29,16 @@ class DeviceSquares:
     """
 
     def __init__(self, k: int, n: int, device: int = 0, ctx: Optional[Context] = None,
-                 with_ods: bool = True):
+                 with_ods: bool = True, in_place: bool = False):
         self.k, self.n = int(k), int(n)
         self.ctx = ctx or default_context()
         dev = torch.device("cuda", device)
         w = 2 * self.k
-        self.ods = torch.empty((n, self.k * self.k * 512), dtype=torch.uint8, device=dev) if with_ods else None
+        # in_place: the ODS lives in Q0 of the EDS buffer itself (rows at the EDS
+        # row pitch), the zero-copy input of dagpu_extend_batch_device (d_ods = NULL)
+        self.in_place = bool(in_place)
+        self.ods = (torch.empty((n, self.k * self.k * 512), dtype=torch.uint8, device=dev)
+                    if with_ods and not in_place else None)
         self.eds = torch.empty((n, w * w * 512), dtype=torch.uint8, device=dev)
         self.row_roots = torch.empty((n, w, ROOT), dtype=torch.uint8, device=dev)
         self.col_roots = torch.empty((n, w, ROOT), dtype=torch.uint8, device=dev)
@@ -42,6 +46,21 @@ class DeviceSquares:
         self.status = torch.zeros((n,), dtype=torch.int32, device=dev)
         ws = self.ctx._L.dagpu_workspace_size(self.k, self.n)
         self.workspace = torch.empty((ws,), dtype=torch.uint8, device=dev)
+
+    def q0(self) -> torch.Tensor:
+        """(n, k, k*512) view of Q0 inside the EDS buffer."""
+        w = 2 * self.k
+        return self.eds.view(self.n, w, w * 512)[:, :self.k, :self.k * 512]
+
+    def load_ods(self, ods) -> None:
+        """Copy n ODS (anything viewable as (n, k*k*512) uint8) to where extend()
+        reads them: self.ods, or Q0 of the EDS when in_place."""
+        src = ods if isinstance(ods, torch.Tensor) else torch.from_numpy(ods)
+        src = src.reshape(self.n, self.k, self.k * 512)
+        if self.in_place:
+            self.q0().copy_(src)
+        else:
+            self.ods.view(self.n, self.k, self.k * 512).copy_(src)
 
     def _ck(self, rc: int) -> None:
         if rc != 0:

@@ -268,5 +268,105 @@ __host__ __device__ __forceinline__ void fft_B(uint32_t (&v)[16][8]) {
   });
 }
 
+// ---------------------------------------------------------------------------
+// Two-vector layout for k = 128 (rs_gf8_sliced.hip leo8_encode_sliced2_kernel).
+// A 4-wave workgroup holds 2 vectors (128 KB) instead of 4 (256 KB), so two
+// workgroups fit a CU and one loads / stores while the other transforms (the
+// 4-vector kernel runs one 8-wave workgroup per CU with its phases serialised).
+// Lane l = eb * 32 + vv * 16 + t: t = column block, vv = vector, eb = one
+// ELEMENT bit carried by the lane.
+//   A: e = j + 16 eb + 32 w   (j = register, w = wave)   -- IFFT/FFT layers 0..2
+//   B: e = eb + 2 w + 8 i     (i = register)             -- layers 3..6, the same
+//      register stride as Geo<128>'s layout B, so ifft_B/fft_B<128> apply as is.
+// In A the skew of layer m for element e splits, by the GF(2)-linearity of the
+// FFT skews in the block offset (checked by skew_split_ok below), into
+//   C(register bits, with the IFFT's +k) ^ eb S16 ^ w0 S32 ^ w1 S64,
+// S_b = skew(2^m - 1 + b): C is folded at compile time, the wave bits are
+// wave-uniform branches around compile-time matrices, the lane bit multiplies
+// a lane-masked copy of y by a compile-time matrix.
+// ---------------------------------------------------------------------------
+constexpr bool skew_split_ok() {
+  for (int m = 0; m < 7; m++) {
+    const int D = 1 << m;
+    for (int b = 0; b < 256; b += 2 * D) {
+      if (D - 1 + b >= 255) continue;
+      uint8_t want = 0;
+      for (int bit = m + 1; bit < 8; bit++)
+        if ((b >> bit) & 1) want ^= skew_elem(D - 1 + (1 << bit));
+      if (skew_elem(D - 1 + b) != want) return false;
+    }
+  }
+  return true;
+}
+static_assert(skew_split_ok(), "FFT skews must be GF(2)-linear in the block offset");
+
+// x ^= C * (y & mask): the lane-bit part of a layout-A skew
+template <int C>
+__host__ __device__ __forceinline__ void muladd_ct_masked(uint32_t (&x)[8], const uint32_t (&y)[8], uint32_t mask) {
+  uint32_t ym[8];
+  static_for<8>([&](auto p) { ym[p] = y[p] & mask; });
+  muladd_ct<C>(x, ym);
+}
+
+// IFFT layers 0..2 in the two-vector layout A (K = 128), wave w, lane mask of eb.
+template <int K>
+__host__ __device__ __forceinline__ void ifft_A2(uint32_t (&v)[16][8], int w, uint32_t ebmask) {
+  static_assert(K == 128, "two-vector layout: k = 128");
+  static_for<3>([&](auto m) {
+    constexpr int D = 1 << m;
+    SL_FENCE();
+    static_for<16>([&](auto j) {
+      if constexpr (!(j & D)) {
+        constexpr int c = skew_elem(D - 1 + K + (j & ~(2 * D - 1)));
+        xor8(v[j + D], v[j]);
+        muladd_ct<c>(v[j], v[j + D]);
+      }
+    });
+    if (w & 1) {
+      static_for<16>([&](auto j) {
+        if constexpr (!(j & D)) muladd_ct<skew_elem(D - 1 + 32)>(v[j], v[j + D]);
+      });
+    }
+    if (w & 2) {
+      static_for<16>([&](auto j) {
+        if constexpr (!(j & D)) muladd_ct<skew_elem(D - 1 + 64)>(v[j], v[j + D]);
+      });
+    }
+    static_for<16>([&](auto j) {
+      if constexpr (!(j & D)) muladd_ct_masked<skew_elem(D - 1 + 16)>(v[j], v[j + D], ebmask);
+    });
+  });
+}
+
+// FFT layers 2..0 in the two-vector layout A.
+template <int K>
+__host__ __device__ __forceinline__ void fft_A2(uint32_t (&v)[16][8], int w, uint32_t ebmask) {
+  static_assert(K == 128, "two-vector layout: k = 128");
+  static_for<3>([&](auto mm) {
+    constexpr int m = 2 - mm;
+    constexpr int D = 1 << m;
+    SL_FENCE();
+    static_for<16>([&](auto j) {
+      if constexpr (!(j & D)) muladd_ct<skew_elem(D - 1 + (j & ~(2 * D - 1)))>(v[j], v[j + D]);
+    });
+    if (w & 1) {
+      static_for<16>([&](auto j) {
+        if constexpr (!(j & D)) muladd_ct<skew_elem(D - 1 + 32)>(v[j], v[j + D]);
+      });
+    }
+    if (w & 2) {
+      static_for<16>([&](auto j) {
+        if constexpr (!(j & D)) muladd_ct<skew_elem(D - 1 + 64)>(v[j], v[j + D]);
+      });
+    }
+    static_for<16>([&](auto j) {
+      if constexpr (!(j & D)) muladd_ct_masked<skew_elem(D - 1 + 16)>(v[j], v[j + D], ebmask);
+    });
+    static_for<16>([&](auto j) {
+      if constexpr (!(j & D)) xor8(v[j + D], v[j]);
+    });
+  });
+}
+
 }  // namespace sliced
 }  // namespace dagpu

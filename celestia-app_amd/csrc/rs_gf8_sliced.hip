@@ -143,6 +143,110 @@ void leo8_encode_sliced_kernel(EncodeArgs a) {
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// k = 128, two vectors per 4-wave workgroup (leo8_sliced.hpp "two-vector
+// layout"): 128 KB of state per workgroup instead of 256 KB, so two workgroups
+// share a CU (VGPRs 2 x 1 wave/SIMD, LDS 2 x 64 KB) and one workgroup's loads
+// and stores overlap the other's transform.  Lane l: t = l & 15 (column block),
+// vv = (l >> 4) & 1 (vector), eb = l >> 5 (element bit).  LDS slot of element e
+// for lane (vv, t): e * 32 + vv * 16 + t, 4 planes per pass, two passes.
+// ---------------------------------------------------------------------------
+template <bool A_TO_B>
+__device__ __forceinline__ void exchange2(uint32_t (&v)[16][8], u32x4* lds, int w, int eb, int col) {
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    if (h) __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      const int e = A_TO_B ? r + 16 * eb + 32 * w : eb + 2 * w + 8 * r;
+      lds[e * 32 + col] = (u32x4){v[r][4 * h], v[r][4 * h + 1], v[r][4 * h + 2], v[r][4 * h + 3]};
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      const int e = A_TO_B ? eb + 2 * w + 8 * r : r + 16 * eb + 32 * w;
+      const u32x4 q = lds[e * 32 + col];
+      v[r][4 * h] = q.x;
+      v[r][4 * h + 1] = q.y;
+      v[r][4 * h + 2] = q.z;
+      v[r][4 * h + 3] = q.w;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void leo8_encode_sliced2_kernel(EncodeArgs a) {
+  constexpr int K = 128;
+  __shared__ u32x4 lds[K * 32];  // 64 KB
+  const long ngrp = a.nvec >> 1;
+  const long nblk = a.nsq * ngrp * a.nchunk;
+  long blk = blockIdx.x;
+  if ((nblk & 7) == 0) blk = (blk & 7) * (nblk >> 3) + (blk >> 3);  // one eighth per XCD
+  const long chunk = blk % a.nchunk;
+  const long sg = blk / a.nchunk;
+  const long grp = sg % ngrp;
+  const long sq = sg / ngrp;
+  constexpr int st_aux = 2;  // non-temporal stores
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int t = lane & 15, vv = (lane >> 4) & 1, eb = lane >> 5;
+  const uint32_t ebmask = eb ? 0xFFFFFFFFu : 0u;
+
+  // layout A: register j holds element j + 16 eb + 32 w; the lane part of the
+  // element offset (16 eb) goes into voffset, the wave part into soffset
+  uint32_t v[16][8];
+  {
+    const auto rsrc = make_rsrc(a.in + sq * a.in_sq_stride + grp * 2 * a.in_vec_stride + chunk * 512);
+    const uint32_t sstride = (uint32_t)a.in_shard_stride;
+    const uint32_t voff = (uint32_t)(vv * a.in_vec_stride) + (uint32_t)(16 * eb) * sstride + 16u * t;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint32_t soff = (uint32_t)(j + 32 * w) * sstride;
+      const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, soff, 0);
+      const u32x4 hi = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 256u, soff, 0);
+      v[j][0] = lo.x; v[j][1] = lo.y; v[j][2] = lo.z; v[j][3] = lo.w;
+      v[j][4] = hi.x; v[j][5] = hi.y; v[j][6] = hi.z; v[j][7] = hi.w;
+    }
+  }
+  if (a.copy) {  // row pass: the data shards also go to Q0 of the EDS
+    const auto rsrc = make_rsrc(a.copy + sq * a.copy_sq_stride + grp * 2 * a.copy_vec_stride + chunk * 512);
+    const uint32_t sstride = (uint32_t)a.copy_shard_stride;
+    const uint32_t voff = (uint32_t)(vv * a.copy_vec_stride) + (uint32_t)(16 * eb) * sstride + 16u * t;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint32_t soff = (uint32_t)(j + 32 * w) * sstride;
+      __builtin_amdgcn_raw_buffer_store_b128((u32x4){v[j][0], v[j][1], v[j][2], v[j][3]}, rsrc, voff, soff, st_aux);
+      __builtin_amdgcn_raw_buffer_store_b128((u32x4){v[j][4], v[j][5], v[j][6], v[j][7]}, rsrc, voff + 256u, soff,
+                                             st_aux);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 16; j++) transpose8(v[j]);
+
+  const int col = vv * 16 + t;
+  ifft_A2<K>(v, w, ebmask);
+  exchange2<true>(v, lds, w, eb, col);
+  ifft_B<K>(v);
+  fft_B<K>(v);
+  __syncthreads();
+  exchange2<false>(v, lds, w, eb, col);
+  fft_A2<K>(v, w, ebmask);
+
+#pragma unroll
+  for (int j = 0; j < 16; j++) transpose8(v[j]);
+  const auto rsrc = make_rsrc(a.out + sq * a.out_sq_stride + grp * 2 * a.out_vec_stride + chunk * 512);
+  const uint32_t sstride = (uint32_t)a.out_shard_stride;
+  const uint32_t voff = (uint32_t)(vv * a.out_vec_stride) + (uint32_t)(16 * eb) * sstride + 16u * t;
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    const uint32_t soff = (uint32_t)(j + 32 * w) * sstride;
+    __builtin_amdgcn_raw_buffer_store_b128((u32x4){v[j][0], v[j][1], v[j][2], v[j][3]}, rsrc, voff, soff, st_aux);
+    __builtin_amdgcn_raw_buffer_store_b128((u32x4){v[j][4], v[j][5], v[j][6], v[j][7]}, rsrc, voff + 256u, soff,
+                                           st_aux);
+  }
+}
+
 template <int K>
 static hipError_t launch_sliced_k(const EncodeArgs& a, hipStream_t s) {
   const long blocks = a.nsq * (a.nvec / 4) * a.nchunk;
@@ -179,7 +283,23 @@ bool leo8_sliced_applicable(int k, const EncodeArgs& a) {
   return true;
 }
 
+// DAGPU_ENC_SLICED2=0 keeps k = 128 on the 4-vector kernel (A/B runs).
+static bool sliced2_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("DAGPU_ENC_SLICED2");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 hipError_t launch_leo8_encode_sliced(int k, const EncodeArgs& a, hipStream_t s) {
+  // (leo8_sliced_applicable has checked the shapes: nvec % 4 == 0, offsets < 2^31)
+  if (k == 128 && sliced2_enabled()) {
+    const long blocks = a.nsq * (a.nvec / 2) * a.nchunk;
+    if (blocks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(leo8_encode_sliced2_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
   switch (k) {
     case 16: return launch_sliced_k<16>(a, s);
     case 32: return launch_sliced_k<32>(a, s);

@@ -56,6 +56,56 @@ void encode_chunk_lane(const uint8_t* data, uint8_t* parity, long shard, long co
     }
 }
 
+
+// Two-vector layout of leo8_encode_sliced2_kernel (k = 128): one vector's
+// column block t, the 8 (wave w, lane element bit eb) "lanes" of layout A
+// (e = j + 16 eb + 32 w) and layout B (e = eb + 2 w + 8 i).
+void encode2_chunk_lane(const uint8_t* data, uint8_t* parity, long shard, long col0) {
+  constexpr int K = 128;
+  static uint32_t st[4][2][16][8], tmp[4][2][16][8];
+  for (int w = 0; w < 4; w++)
+    for (int eb = 0; eb < 2; eb++)
+      for (int j = 0; j < 16; j++) {
+        const uint8_t* src = data + (long)(j + 16 * eb + 32 * w) * shard;
+        uint32_t d[8];
+        memcpy(d, src + col0, 16);
+        memcpy(d + 4, src + col0 + 256, 16);
+        transpose8(d);
+        memcpy(st[w][eb][j], d, 32);
+      }
+  for (int w = 0; w < 4; w++)
+    for (int eb = 0; eb < 2; eb++) ifft_A2<K>(st[w][eb], w, eb ? 0xFFFFFFFFu : 0u);
+  for (int w = 0; w < 4; w++)  // A -> B
+    for (int eb = 0; eb < 2; eb++)
+      for (int i = 0; i < 16; i++) {
+        const int e = eb + 2 * w + 8 * i;
+        memcpy(tmp[w][eb][i], st[e >> 5][(e >> 4) & 1][e & 15], 32);
+      }
+  for (int w = 0; w < 4; w++)
+    for (int eb = 0; eb < 2; eb++) {
+      ifft_B<K>(tmp[w][eb]);
+      fft_B<K>(tmp[w][eb]);
+    }
+  for (int w = 0; w < 4; w++)  // B -> A
+    for (int eb = 0; eb < 2; eb++)
+      for (int i = 0; i < 16; i++) {
+        const int e = eb + 2 * w + 8 * i;
+        memcpy(st[e >> 5][(e >> 4) & 1][e & 15], tmp[w][eb][i], 32);
+      }
+  for (int w = 0; w < 4; w++)
+    for (int eb = 0; eb < 2; eb++) fft_A2<K>(st[w][eb], w, eb ? 0xFFFFFFFFu : 0u);
+  for (int w = 0; w < 4; w++)
+    for (int eb = 0; eb < 2; eb++)
+      for (int j = 0; j < 16; j++) {
+        uint32_t d[8];
+        memcpy(d, st[w][eb][j], 32);
+        transpose8(d);
+        uint8_t* dst = parity + (long)(j + 16 * eb + 32 * w) * shard;
+        memcpy(dst + col0, d, 16);
+        memcpy(dst + col0 + 256, d + 4, 16);
+      }
+}
+
 template <int K>
 int encode(long shard, const uint8_t* data, uint8_t* parity) {
   for (long c = 0; c < shard; c += 512)
@@ -64,6 +114,13 @@ int encode(long shard, const uint8_t* data, uint8_t* parity) {
 }
 
 }  // namespace
+
+extern "C" int sliced2_emu_encode(long shard, const uint8_t* data, uint8_t* parity) {
+  if (shard <= 0 || shard % 512) return -1;
+  for (long c = 0; c < shard; c += 512)
+    for (int t = 0; t < 16; t++) encode2_chunk_lane(data, parity, shard, c + 16 * t);
+  return 0;
+}
 
 extern "C" int sliced_emu_encode(int k, long shard, const uint8_t* data, uint8_t* parity) {
   if (shard <= 0 || shard % 512) return -1;

@@ -171,3 +171,22 @@ def test_two_threads_one_context(ctx):
     assert not errors, errors
     assert (results["a"] == want).all()
     assert (ds.status.cpu().numpy() == 0).all()
+
+
+def test_device_batch_in_place_matches(ctx):
+    """ODS resident in Q0 of the EDS buffer (d_ods = NULL) gives the same EDS,
+    roots and DAHs as a separate ODS buffer, over repeated steps."""
+    k, n = 128, 6
+    ods = synth.blob_squares(k, 4242, 0, n)
+    a = DeviceSquares(k, n, ctx=ctx)
+    b = DeviceSquares(k, n, ctx=ctx, in_place=True)
+    a.load_ods(ods)
+    b.load_ods(ods)
+    for _ in range(2):
+        a.extend()
+        b.extend()
+    torch.cuda.synchronize()
+    assert torch.equal(a.eds, b.eds) and torch.equal(a.dah, b.dah)
+    assert torch.equal(a.row_roots, b.row_roots) and torch.equal(a.col_roots, b.col_roots)
+    _, _, _, hdah, _ = da.extend_batch(ods.reshape(-1), [k] * n, ctx)
+    assert (b.dah.cpu().numpy() == hdah).all()

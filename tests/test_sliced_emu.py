@@ -22,6 +22,7 @@ def emu():
         pytest.skip("emulator not built (make -C celestia-app_amd emu)")
     L = ctypes.CDLL(EMU)
     L.sliced_emu_encode.argtypes = [ctypes.c_int, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p]
+    L.sliced2_emu_encode.argtypes = [ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p]
     L.sliced_emu_bop3.restype = ctypes.c_uint32
     L.sliced_emu_bop3.argtypes = [ctypes.c_uint32] * 3 + [ctypes.c_int]
     return L
@@ -63,3 +64,21 @@ def test_sliced_rejects_unsupported(emu):
     buf = np.zeros((8, 512), np.uint8)
     assert emu.sliced_emu_encode(8, 512, buf.ctypes.data, buf.ctypes.data) == -1
     assert emu.sliced_emu_encode(16, 100, buf.ctypes.data, buf.ctypes.data) == -1
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_sliced2_encode_matches_oracle(emu, seed):
+    """The two-vector k = 128 layout (lane element bit, wave-bit branches;
+    leo8_encode_sliced2_kernel) on random and structured data."""
+    k, shard = 128, 512 * (1 + seed % 2)
+    rng = np.random.default_rng(900 + seed)
+    cases = [rng.integers(0, 256, (k, shard), dtype=np.uint8)]
+    if seed == 0:
+        one = np.zeros((k, shard), np.uint8)
+        for e in range(k):
+            one[e, (e * 5) % shard] = 1 << (e % 8)
+        cases += [one, np.full((k, shard), 0xFF, np.uint8)]
+    for data in cases:
+        parity = np.zeros_like(data)
+        assert emu.sliced2_emu_encode(shard, data.ctypes.data, parity.ctypes.data) == 0
+        assert np.array_equal(parity, oracle.encode(data))
