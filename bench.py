@@ -182,8 +182,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time per k (64 and 128)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = all usable host cores)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--in-place", action="store_true",
-                    help="ODS resident in Q0 of the EDS buffer (dagpu_extend_batch_device with d_ods = NULL)")
+    ap.add_argument("--separate-ods", dest="in_place", action="store_false",
+                    help="keep the ODS in its own buffer (the row pass then also copies Q0 into the EDS); "
+                         "default: ODS resident in Q0 of the EDS buffer (dagpu_extend_batch_device, d_ods = NULL)")
     ap.add_argument("--mode", choices=["extend", "mixed", "repair", "split"], default="extend",
                     help="extend: configs[1] (headline); mixed: configs[2]; repair: configs[3]; "
                          "split: configs[4] oversized square over all ranks")

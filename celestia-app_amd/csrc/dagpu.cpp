@@ -286,7 +286,8 @@ int dagpu_init(int device, dagpu_ctx** out) {
   dagpu_ctx* c = new dagpu_ctx();
   c->device = device;
   bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
-            hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) == hipSuccess;
+            hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->rs_stream, hipStreamNonBlocking) == hipSuccess;
   for (int i = 0; ok && i < 2; i++)
     ok = hipEventCreateWithFlags(&c->ev_loaded[i], hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&c->ev_done[i], hipEventDisableTiming) == hipSuccess;
@@ -315,6 +316,9 @@ void dagpu_destroy(dagpu_ctx* c) {
     if (c->ev_loaded[i]) (void)hipEventDestroy(c->ev_loaded[i]);
     if (c->ev_done[i]) (void)hipEventDestroy(c->ev_done[i]);
   }
+  if (c->rs_stream) (void)hipStreamSynchronize(c->rs_stream);
+  for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+  if (c->rs_stream) (void)hipStreamDestroy(c->rs_stream);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -439,14 +443,91 @@ int dagpu_roots_device(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_ed
                        (hipStream_t)stream);
 }
 
+namespace {
+
+hipEvent_t ev_take(dagpu_ctx* c) {
+  std::lock_guard<std::mutex> g(c->ev_mu);
+  if (!c->ev_pool.empty()) {
+    hipEvent_t e = c->ev_pool.back();
+    c->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+  return e;
+}
+
+void ev_give(dagpu_ctx* c, hipEvent_t e) {
+  if (!e) return;
+  std::lock_guard<std::mutex> g(c->ev_mu);
+  c->ev_pool.push_back(e);
+}
+
+// Slices of a device batch for the RS/NMT pipeline: RS of slice i+1.. runs on
+// ctx->rs_stream while the NMT kernels of slice i run on the caller's stream
+// (bench: 256 squares at k = 128, 4 slices 11.98 -> 11.63 ms; tools/pipe_exp.py).
+// DAGPU_PIPE_SLICES overrides (1 = off).  Off while profiling, so that every
+// kernel's event bracket times that kernel alone.
+size_t pipe_slices(dagpu_ctx* ctx, uint32_t k, size_t n) {
+  static const long env = [] {
+    const char* e = getenv("DAGPU_PIPE_SLICES");
+    return e ? atol(e) : 0L;
+  }();
+  if (ctx->prof) return 1;
+  size_t s = env > 0 ? (size_t)env : (k >= 128 && n >= 64 ? 4 : 1);
+  while (s > 1 && n / s < 8) s >>= 1;
+  return s < 1 ? 1 : s;
+}
+
+}  // namespace
+
 int dagpu_extend_batch_device(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_ods,
                               uint8_t* d_eds, uint8_t* d_row_roots, uint8_t* d_col_roots,
                               uint8_t* d_dah, int32_t* d_status, void* d_workspace,
                               void* stream) {
-  int rc = dagpu_extend_rs_device(ctx, k, n, d_ods, d_eds, stream);
+  if (!ctx || !d_eds || !d_row_roots || !d_col_roots || !d_dah || !d_status || !d_workspace)
+    return DAGPU_ERR_ARG;
+  int rc = check_k(ctx, k);
   if (rc) return rc;
-  return dagpu_roots_device(ctx, k, n, d_eds, d_row_roots, d_col_roots, d_dah, d_status,
-                            d_workspace, stream);
+  const size_t S = pipe_slices(ctx, k, n);
+  hipStream_t s = (hipStream_t)stream;
+  if (S <= 1) {
+    rc = enqueue_rs(ctx, k, n, d_ods, d_eds, s);
+    if (rc) return rc;
+    return enqueue_roots(ctx, k, n, d_eds, d_row_roots, d_col_roots, d_dah, d_status, d_workspace, s);
+  }
+  // fork: rs_stream starts after the work already queued on the caller's stream
+  std::vector<hipEvent_t> ev(S + 1, nullptr);
+  for (auto& e : ev)
+    if (!(e = ev_take(ctx))) {
+      for (auto x : ev) ev_give(ctx, x);
+      return set_err(ctx, DAGPU_ERR_DEVICE, "hipEventCreate failed");
+    }
+  auto done = [&](int r) {
+    for (auto x : ev) ev_give(ctx, x);
+    return r;
+  };
+  hipStream_t rs = ctx->rs_stream;
+  const size_t w = 2 * (size_t)k;
+  if (hipEventRecord(ev[S], s) != hipSuccess || hipStreamWaitEvent(rs, ev[S], 0) != hipSuccess)
+    return done(set_err(ctx, DAGPU_ERR_DEVICE, "pipeline fork failed"));
+  for (size_t i = 0; i < S; i++) {
+    const size_t a = n * i / S, b = n * (i + 1) / S;
+    rc = enqueue_rs(ctx, k, b - a, d_ods ? d_ods + a * ods_bytes(k) : nullptr, d_eds + a * eds_bytes(k), rs);
+    if (rc) return done(rc);
+    if (hipEventRecord(ev[i], rs) != hipSuccess) return done(set_err(ctx, DAGPU_ERR_DEVICE, "hipEventRecord failed"));
+  }
+  // the slices' NMT work runs in order on the caller's stream and shares the
+  // front of the workspace; waiting on the last slice's event also joins rs_stream
+  for (size_t i = 0; i < S; i++) {
+    const size_t a = n * i / S, b = n * (i + 1) / S;
+    if (hipStreamWaitEvent(s, ev[i], 0) != hipSuccess)
+      return done(set_err(ctx, DAGPU_ERR_DEVICE, "hipStreamWaitEvent failed"));
+    rc = enqueue_roots(ctx, k, b - a, d_eds + a * eds_bytes(k), d_row_roots + a * w * kNodeSize,
+                       d_col_roots + a * w * kNodeSize, d_dah + a * 32, d_status + a, d_workspace, s);
+    if (rc) return done(rc);
+  }
+  return done(DAGPU_OK);
 }
 
 int dagpu_roots(dagpu_ctx* ctx, uint32_t k, const uint8_t* eds, uint8_t* row_roots,

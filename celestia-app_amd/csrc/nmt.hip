@@ -28,6 +28,7 @@
 // Kernel 3 (DAH): one workgroup per square, RFC-6962 over 4k roots.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "kernels.hpp"
 #include "nmt_node.hpp"
@@ -308,11 +309,22 @@ __global__ __launch_bounds__(kDahThreads) void dah_kernel(SquareArgs a) {
   }
 }
 
+// DAGPU_LEAF_LDS_KB (experiments): dynamic LDS requested per leaf workgroup,
+// which caps the leaf kernel's occupancy (it uses no LDS) to leave room on a
+// CU for RS workgroups of a pipelined batch.
+static size_t leaf_lds_bytes() {
+  static const size_t v = [] {
+    const char* e = getenv("DAGPU_LEAF_LDS_KB");
+    return e ? (size_t)atol(e) * 1024 : (size_t)0;
+  }();
+  return v;
+}
+
 hipError_t launch_nmt_leaves(const SquareArgs& a, hipStream_t s) {
   const long w = 2L * a.k;
   const long total = w * w * a.nsq;
   const long blocks = (total + kLeafWave - 1) / kLeafWave;
-  hipLaunchKernelGGL(nmt_leaf_kernel, dim3((unsigned)blocks), dim3(kLeafWave), 0, s, a);
+  hipLaunchKernelGGL(nmt_leaf_kernel, dim3((unsigned)blocks), dim3(kLeafWave), leaf_lds_bytes(), s, a);
   return hipGetLastError();
 }
 

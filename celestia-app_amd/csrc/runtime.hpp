@@ -72,6 +72,11 @@ struct dagpu_ctx {
   // host-mode pipeline (dagpu.cpp run_group_pipelined): H2D on copy_stream,
   // kernels + D2H on stream, two slots handed over with events
   hipStream_t copy_stream = nullptr;
+  // device-resident pipeline (dagpu.cpp dagpu_extend_batch_device): RS of later slices
+  // on rs_stream beside the NMT work of earlier slices on the caller's stream
+  hipStream_t rs_stream = nullptr;
+  std::mutex ev_mu;
+  std::vector<hipEvent_t> ev_pool;  // timing-disabled events, recycled per call
   hipEvent_t ev_loaded[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
   HostBuf h_out;
   // generic forests / commitments / split square (trees.cpp, split.cpp)
