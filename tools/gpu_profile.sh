@@ -15,5 +15,8 @@ for P in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_WAV
   echo "pmc $P ok"
 done
 find $OUT -name "*.csv" | head -50
-timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/calib_$TAG -o run -- "$GRAFT_REPO_ROOT/tools/fetch_calib" > $OUT/calib_$TAG.log 2>&1 || { echo "calib failed"; exit 1; }
-echo "calib ok"
+# clock check of the 4-vector encoder run (leaf kernel time after each encoder)
+DAGPU_ENC_SLICED2=0 timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d $OUT/pmc_${TAG}s1_GRBM -o run -- python3 $BENCH > $OUT/pmc_${TAG}s1_GRBM.log 2>&1 || { echo "pmc s1 failed"; exit 1; }
+echo "pmc s1 ok"
+DAGPU_ENC_SLICED2=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_${TAG}s1 -o run -- python3 $BENCH > $OUT/trace_${TAG}s1.log 2>&1 || { echo "trace s1 failed"; exit 1; }
+echo "trace s1 ok"

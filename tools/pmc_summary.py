@@ -17,6 +17,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SHORT = {
+    "leo8_encode_sliced2_kernel": "rs_encode_sliced2",
     "leo8_encode_sliced_kernel": "rs_encode_sliced",
     "leo8_encode_kernel": "rs_encode",
     "leo8_decode_kernel": "decode",
