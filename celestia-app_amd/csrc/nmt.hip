@@ -161,11 +161,20 @@ __global__ __launch_bounds__(256) void nmt_level1_kernel(SquareArgs a, uint8_t* 
     if (bad) atomicOr(&a.status[sq], kStatusPushOrder);
   }
   uint32_t st[8];
-  auto get = [&](int P, int i) -> uint32_t {
-    return P == 0 || P == 1 ? nl[i] : P == 2 ? dl[i] : P == 3 || P == 4 ? nr[i] : dr[i];
-  };
-  sha_node_msg(get, st);
   const bool lpar = ns_is_parity(nl), rpar = ns_is_parity(nr);
+  if (__all(lpar)) {
+    // every left leaf of this wave carries the parity namespace: the message's
+    // first 56 bytes (0x01 | 0xFF*58) are constant and rounds 0..13 of block 0 fold
+    auto get = [&](int P, int i) -> uint32_t {
+      return P == 0 || P == 1 ? (i == 7 ? 0xFFu : 0xFFFFFFFFu) : P == 2 ? dl[i] : P == 3 || P == 4 ? nr[i] : dr[i];
+    };
+    sha_node_msg(get, st);
+  } else {
+    auto get = [&](int P, int i) -> uint32_t {
+      return P == 0 || P == 1 ? nl[i] : P == 2 ? dl[i] : P == 3 || P == 4 ? nr[i] : dr[i];
+    };
+    sha_node_msg(get, st);
+  }
   uint32_t dg[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) dg[i] = bswap32(st[i]);
@@ -206,10 +215,19 @@ __global__ __launch_bounds__(256) void nmt_level_kernel(SquareArgs a, const uint
   ns_by_ref(ns_sq, r2.x, rmn);
   ns_by_ref(ns_sq, r2.y, rmx);
   uint32_t st[8];
-  auto get = [&](int P, int i) -> uint32_t {
-    return P == 0 ? lmn[i] : P == 1 ? lmx[i] : P == 2 ? dl[i] : P == 3 ? rmn[i] : P == 4 ? rmx[i] : dr[i];
-  };
-  sha_node_msg(get, st);
+  if (__all(l2.x == kParityRef)) {
+    // all-parity left children (min PARITY implies max PARITY): constant
+    // 0x01 | 0xFF*58 prefix, rounds 0..13 of block 0 fold
+    auto get = [&](int P, int i) -> uint32_t {
+      return P <= 1 ? (i == 7 ? 0xFFu : 0xFFFFFFFFu) : P == 2 ? dl[i] : P == 3 ? rmn[i] : P == 4 ? rmx[i] : dr[i];
+    };
+    sha_node_msg(get, st);
+  } else {
+    auto get = [&](int P, int i) -> uint32_t {
+      return P == 0 ? lmn[i] : P == 1 ? lmx[i] : P == 2 ? dl[i] : P == 3 ? rmn[i] : P == 4 ? rmx[i] : dr[i];
+    };
+    sha_node_msg(get, st);
+  }
   uint32_t dg[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) dg[i] = bswap32(st[i]);

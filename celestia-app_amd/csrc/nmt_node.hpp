@@ -151,24 +151,27 @@ __device__ __forceinline__ void share_leaf_sha256(const uint4* src, bool q0, uin
     const uint4 q0v = cur[0], q1v = cur[1], q2v = cur[2];
     const uint32_t d[12] = {q0v.x, q0v.y, q0v.z, q0v.w, q1v.x, q1v.y,
                             q1v.z, q1v.w, q2v.x, q2v.y, q2v.z, q2v.w};
-    if (q0) {
-      m[0] = __builtin_amdgcn_perm(d[0], d[0], (PZ << 24) | 0x000102u);
-#pragma unroll
-      for (int j = 1; j <= 6; j++) m[j] = __builtin_amdgcn_perm(d[j - 1], d[j], 0x07000102u);
-      m[7] = __builtin_amdgcn_perm(d[6], d[7], (0x0700u << 16) | (PZ << 8) | PZ);
-    } else {
-      m[0] = 0x00FFFFFFu;
-#pragma unroll
-      for (int j = 1; j <= 6; j++) m[j] = 0xFFFFFFFFu;
-      m[7] = 0xFFFF0000u;
-    }
-    m[7] |= __builtin_amdgcn_perm(d[0], d[0], (PZ << 24) | (PZ << 16) | 0x0001u);
 #pragma unroll
     for (int j = 0; j < 7; j++) ns[j] = d[j];
     ns[7] = d[7] & 0xFFu;
 #pragma unroll
     for (int j = 8; j < 16; j++) m[j] = __builtin_amdgcn_perm(d[j - 8], d[j - 7], 0x06070001u);
-    sha256_compress(st, m);
+    const uint32_t m7lo = __builtin_amdgcn_perm(d[0], d[0], (PZ << 24) | (PZ << 16) | 0x0001u);
+    if (q0) {
+      m[0] = __builtin_amdgcn_perm(d[0], d[0], (PZ << 24) | 0x000102u);
+#pragma unroll
+      for (int j = 1; j <= 6; j++) m[j] = __builtin_amdgcn_perm(d[j - 1], d[j], 0x07000102u);
+      m[7] = __builtin_amdgcn_perm(d[6], d[7], (0x0700u << 16) | (PZ << 8) | PZ) | m7lo;
+      sha256_compress(st, m);
+    } else {
+      // parity leaf (wave-uniform): words 0..6 are the constant prefix
+      // 0x00 | 0xFF*27, so rounds 0..6 fold at compile time (own call site)
+      m[0] = 0x00FFFFFFu;
+#pragma unroll
+      for (int j = 1; j <= 6; j++) m[j] = 0xFFFFFFFFu;
+      m[7] = 0xFFFF0000u | m7lo;
+      sha256_compress(st, m);
+    }
   }
   mid_block(cur[2], cur[3], cur[4], cur[5], cur[6]);  // block 1
   uint4 prev0 = cur[6], prev1 = cur[7];

@@ -14,17 +14,26 @@
 
 namespace dagpu {
 
+// Each helper falls back to plain C when its operands are compile-time
+// constants, so rounds whose inputs are all constant (the parity-namespace
+// prefix of a parity leaf, the 0xFF prefix of a node whose left child is all
+// parity) fold away entirely instead of being issued with literal operands.
+#define DAGPU_CONST3(a, b, c) (__builtin_constant_p(a) && __builtin_constant_p(b) && __builtin_constant_p(c))
 __device__ __forceinline__ uint32_t rotr32(uint32_t x, int n) {
+  if (__builtin_constant_p(x)) return (x >> n) | (x << (32 - n));
   return __builtin_amdgcn_alignbit(x, x, n);
 }
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  if (DAGPU_CONST3(a, b, c)) return a ^ b ^ c;
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 // bitop3 truth-table index = (src0 << 2) | (src1 << 1) | src2
 __device__ __forceinline__ uint32_t sha_ch(uint32_t e, uint32_t f, uint32_t g) {
+  if (DAGPU_CONST3(e, f, g)) return (e & f) ^ (~e & g);
   return __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);
 }
 __device__ __forceinline__ uint32_t sha_maj(uint32_t a, uint32_t b, uint32_t c) {
+  if (DAGPU_CONST3(a, b, c)) return (a & b) ^ (a & c) ^ (b & c);
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
 }
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) {

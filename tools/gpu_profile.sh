@@ -6,6 +6,7 @@ OUT=gpurun_out/prof; mkdir -p $OUT
 TAG=${1:-r01}
 timeout -k 10 120 "$GRAFT_REPO_ROOT/tools/valu_bench" > $OUT/valu_bench_$TAG.log 2>&1 || { echo "valu_bench failed"; cat $OUT/valu_bench_$TAG.log; exit 1; }
 cat $OUT/valu_bench_$TAG.log
+export DAGPU_PIPE_SLICES=1  # one launch per kernel per step: clean per-launch counters
 BENCH="bench.py --steps 5 --warmup 1 --no-cpu --no-e2e --no-replay --distinct 16"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_$TAG -o run -- python3 $BENCH > $OUT/trace_$TAG.log 2>&1 || { echo "trace failed"; tail -20 $OUT/trace_$TAG.log; exit 1; }
 echo "trace ok"
