@@ -511,8 +511,22 @@ int dagpu_extend_batch_device(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_
   const size_t w = 2 * (size_t)k;
   if (hipEventRecord(ev[S], s) != hipSuccess || hipStreamWaitEvent(rs, ev[S], 0) != hipSuccess)
     return done(set_err(ctx, DAGPU_ERR_DEVICE, "pipeline fork failed"));
+  // slice boundaries: a smaller first slice shortens the RS run nothing overlaps
+  std::vector<size_t> cut(S + 1);
+  {
+    static const long first_env = [] {
+      const char* e = getenv("DAGPU_PIPE_FIRST");
+      return e ? atol(e) : 0L;
+    }();
+    size_t f = first_env > 0 ? (size_t)first_env : n / S;
+    if (f < 1) f = 1;
+    if (f > n - (S - 1)) f = n - (S - 1);
+    cut[0] = 0;
+    cut[1] = f;
+    for (size_t i = 2; i <= S; i++) cut[i] = f + (n - f) * (i - 1) / (S - 1);
+  }
   for (size_t i = 0; i < S; i++) {
-    const size_t a = n * i / S, b = n * (i + 1) / S;
+    const size_t a = cut[i], b = cut[i + 1];
     rc = enqueue_rs(ctx, k, b - a, d_ods ? d_ods + a * ods_bytes(k) : nullptr, d_eds + a * eds_bytes(k), rs);
     if (rc) return done(rc);
     if (hipEventRecord(ev[i], rs) != hipSuccess) return done(set_err(ctx, DAGPU_ERR_DEVICE, "hipEventRecord failed"));
@@ -520,7 +534,7 @@ int dagpu_extend_batch_device(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_
   // the slices' NMT work runs in order on the caller's stream and shares the
   // front of the workspace; waiting on the last slice's event also joins rs_stream
   for (size_t i = 0; i < S; i++) {
-    const size_t a = n * i / S, b = n * (i + 1) / S;
+    const size_t a = cut[i], b = cut[i + 1];
     if (hipStreamWaitEvent(s, ev[i], 0) != hipSuccess)
       return done(set_err(ctx, DAGPU_ERR_DEVICE, "hipStreamWaitEvent failed"));
     rc = enqueue_roots(ctx, k, b - a, d_eds + a * eds_bytes(k), d_row_roots + a * w * kNodeSize,
