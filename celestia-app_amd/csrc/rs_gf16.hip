@@ -791,6 +791,245 @@ __global__ __launch_bounds__(kDecN) __attribute__((amdgpu_waves_per_eu(2, 2))) v
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Register-resident GF(2^16) decode for k = 512 (n = 2k = 1024 work elements).
+// 1024 elements do not fit 16 waves at 2 VGPRs per element (4 symbols per
+// lane, the k = 256 layout), so here a lane holds 2 symbols in ONE dword,
+// packed [lo(2s) lo(2s+1) hi(2s) hi(2s+1)]: a wave covers 256 B of a shard
+// (lane l: 64-B block l >> 4, symbol pair l & 15), a 1024-thread workgroup of
+// 16 waves x 64 elements (64 data VGPRs) one 256-B half of a 512-B chunk.
+// Steps as leo16_decode_reg_kernel; layouts: block (wave q holds 64 q + j) and
+// transposed through LDS (wave c = element bits 2-5, slot (h << 2) | l, h =
+// bits 6-9, l = bits 0-1); n = 2^10 is radix-4 all the way (dist 1, 4, 16 in
+// block layout, 64 and 256 transposed).  A packed multiply is 8 v_perm (one per
+// 2-bit group of the symbol, selecting the low- and high-byte products of both
+// symbols at once) over the same 16-dword product tables.
+// ---------------------------------------------------------------------------
+constexpr int kDec1k = 1024;
+
+// y * c for a packed dword, t = c's 16-dword product table (t[G] low bytes,
+// t[8 + G] high bytes of (e2 << 2G) * c, e2 = 0..3)
+__device__ __forceinline__ uint32_t mulp_g(uint32_t y, const uint32_t* t, int G) {
+  const uint32_t sg = (y >> (G < 4 ? 2 * G : 16 + 2 * (G - 4))) & 0x0303u;
+  const uint32_t sel = (sg | (sg << 16)) + 0x04040000u;  // bytes 2,3 select from t[8 + G]
+  return __builtin_amdgcn_perm(t[8 + G], t[G], sel);
+}
+__device__ __forceinline__ uint32_t mulp(uint32_t y, const uint32_t* t) {
+  uint32_t acc = xor3(mulp_g(y, t, 0), mulp_g(y, t, 1), mulp_g(y, t, 2));
+  acc = xor3(acc, mulp_g(y, t, 3), mulp_g(y, t, 4));
+  acc = xor3(acc, mulp_g(y, t, 5), mulp_g(y, t, 6));
+  return acc ^ mulp_g(y, t, 7);
+}
+
+struct W1k {
+  uint32_t v[64];
+};
+
+// ifftDIT2: y ^= x; x ^= y * skew[pos]     fftDIT2: x ^= y * skew[pos]; y ^= x
+__device__ __forceinline__ void ifft2_p(W1k& w, int i, int j, int pos) {
+  w.v[j] ^= w.v[i];
+  w.v[i] ^= mulp(w.v[j], g_ptab16 + pos * 16);
+}
+__device__ __forceinline__ void fft2_p(W1k& w, int i, int j, int pos) {
+  w.v[i] ^= mulp(w.v[j], g_ptab16 + pos * 16);
+  w.v[j] ^= w.v[i];
+}
+
+// block layout, decoder IFFT radix-4 steps dist D..16 (skew index iend - 1)
+template <int D>
+__device__ __forceinline__ void ifftp_block(W1k& w, int base) {
+#pragma unroll
+  for (int r = 0; r < 64; r += 4 * D) {
+    const int p01 = base + r + D, p02 = p01 + D, p23 = p01 + 2 * D;
+#pragma unroll
+    for (int i = r; i < r + D; i++) {
+      ifft2_p(w, i, i + D, p01);
+      ifft2_p(w, i + 2 * D, i + 3 * D, p23);
+      ifft2_p(w, i, i + 2 * D, p02);
+      ifft2_p(w, i + D, i + 3 * D, p02);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if constexpr (D * 16 <= 64) ifftp_block<D * 4>(w, base);
+}
+
+template <int DIST>
+__device__ __forceinline__ void fftp_block(W1k& w, int base) {
+#pragma unroll
+  for (int r = 0; r < 64; r += 4 * DIST) {
+    const int iend = r + DIST;
+    const int p01 = base + iend - 1, p02 = base + iend + DIST - 1, p23 = base + iend + 2 * DIST - 1;
+#pragma unroll
+    for (int i = r; i < r + DIST; i++) {
+      fft2_p(w, i, i + 2 * DIST, p02);
+      fft2_p(w, i + DIST, i + 3 * DIST, p02);
+      fft2_p(w, i, i + DIST, p01);
+      fft2_p(w, i + 2 * DIST, i + 3 * DIST, p23);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if constexpr (DIST >= 4) fftp_block<DIST / 4>(w, base);
+}
+
+// 16 x 16 block transpose: element (wave Q, slot (c << 2) | l) <-> (wave c,
+// slot (Q << 2) | l); one slot l per LDS round (64 KiB).
+__device__ __forceinline__ void xposep(W1k& w, uint32_t* lds, int q, int lane) {
+#pragma unroll
+  for (int l = 0; l < 4; l++) {
+#pragma unroll
+    for (int c = 0; c < 16; c++) lds[(c * 16 + q) * 64 + lane] = w.v[(c << 2) | l];
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 16; c++) w.v[(c << 2) | l] = lds[(q * 16 + c) * 64 + lane];
+    __syncthreads();
+  }
+}
+
+// formal derivative in the transposed layout (wave c = element bits 2-5; slot
+// bits = element bits 0-1 and 6-9), partner waves' originals through LDS
+__device__ __forceinline__ void derivativep(W1k& w, uint32_t* lds, int c, int lane) {
+  constexpr int B = 16;
+#pragma unroll
+  for (int s0 = 0; s0 < 64; s0 += B) {
+#pragma unroll
+    for (int u = 0; u < B; u++) lds[(c * B + u) * 64 + lane] = w.v[s0 + u];
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < B; u++) {
+      const int sl = s0 + u;
+      uint32_t acc = w.v[sl];
+#pragma unroll
+      for (int bit = 1; bit < 64; bit <<= 1)
+        if ((sl & bit) == 0) acc ^= w.v[sl | bit];
+#pragma unroll
+      for (int wb = 1; wb < 16; wb <<= 1)
+        if ((c & wb) == 0) acc ^= lds[((c | wb) * B + u) * 64 + lane];
+      w.v[sl] = acc;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kDec1k) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_decode_reg1k_kernel(
+    DecodeArgs a) {
+  constexpr int K = kDec1k / 2;
+  __shared__ uint32_t lds[16 * 16 * 64];  // 64 KiB: transpose rounds and derivative staging
+  const long blk = blockIdx.x;
+  const int half = (int)(blk % a.nchunk);  // nchunk = 256-B pieces of the shard
+  const long v = blk / a.nchunk;
+  if (a.flags[v] == 0) return;  // uniform
+  const long sq = v / a.nvec, vec = v % a.nvec;
+  const int lane = threadIdx.x & 63;
+  const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // lane: 64-B block (lane >> 4) of this 256-B piece, symbols 2 (lane & 15) and +1
+  const uint32_t col = (uint32_t)half * 256u + (uint32_t)(lane >> 4) * 64u + (uint32_t)(lane & 15) * 2u;
+  const auto rsrc = make_rsrc(a.data + sq * a.sq_stride + vec * a.vec_stride);
+  const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
+  const uint16_t* err = (const uint16_t*)(a.err + err_vec(a, v) * rs_err_bytes(K));
+  const int my_i = 64 * q + lane;
+  const int my_shard = my_i < K ? K + my_i : my_i - K;
+  const uint64_t pm = __builtin_amdgcn_ballot_w64(pres[(long)my_shard * a.p_shard_stride] != 0);
+  const uint32_t my_err = err[my_i];
+  W1k w;
+#pragma unroll
+  for (int j = 0; j < 64; j++) {
+    const int i = 64 * q + j;
+    const int shard = i < K ? K + i : i - K;
+    const uint32_t so = (uint32_t)shard * (uint32_t)a.shard_stride;
+    const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b16(rsrc, col, so, 0);
+    const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b16(rsrc, col + 32u, so, 0);
+    w.v[j] = ((pm >> j) & 1) ? (lo | (hi << 16)) : 0u;
+  }
+  // work *= errLocs (per-element tables, 16 elements' gathers in flight)
+  const uint32_t mx = mul16_x();
+  const uint32_t mlogx = mx ? (uint32_t)g_log16[mx] : 0u;
+#pragma unroll
+  for (int j0 = 0; j0 < 64; j0 += 8) {
+    uint32_t prod[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) prod[u] = mul16_prod(mx, mlogx, __builtin_amdgcn_readlane(my_err, j0 + u));
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      uint32_t t[16];
+      mul16_pack(prod[u], t);
+      w.v[j0 + u] = mulp(w.v[j0 + u], t);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // ---- IFFT (ifftDITDecoder, skew index iend - 1) ----
+  ifftp_block<1>(w, -1 + 64 * q);  // bits 0-5
+  xposep(w, lds, q, lane);
+#pragma unroll
+  for (int hr = 0; hr < 4; hr++) {  // radix-4 dist 64 (bits 6, 7), r = 256 hr
+    const int p01 = 256 * hr + 63, p02 = p01 + 64, p23 = p01 + 128;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const int s0 = 16 * hr + b;
+      ifft2_p(w, s0, s0 + 4, p01);
+      ifft2_p(w, s0 + 8, s0 + 12, p23);
+      ifft2_p(w, s0, s0 + 8, p02);
+      ifft2_p(w, s0 + 4, s0 + 12, p02);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int s0 = 0; s0 < 16; s0++) {  // radix-4 dist 256 (bits 8, 9)
+    ifft2_p(w, s0, s0 + 16, 255);
+    ifft2_p(w, s0 + 32, s0 + 48, 767);
+    ifft2_p(w, s0, s0 + 32, 511);
+    ifft2_p(w, s0 + 16, s0 + 48, 511);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  derivativep(w, lds, q, lane);
+  // ---- FFT (fftDIT, skew index iend - 1) ----
+#pragma unroll
+  for (int s0 = 0; s0 < 16; s0++) {  // dist 256
+    fft2_p(w, s0, s0 + 32, 511);
+    fft2_p(w, s0 + 16, s0 + 48, 511);
+    fft2_p(w, s0, s0 + 16, 255);
+    fft2_p(w, s0 + 32, s0 + 48, 767);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int hr = 0; hr < 4; hr++) {  // dist 64
+    const int p01 = 256 * hr + 63, p02 = p01 + 64, p23 = p01 + 128;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const int s0 = 16 * hr + b;
+      fft2_p(w, s0, s0 + 8, p02);
+      fft2_p(w, s0 + 4, s0 + 12, p02);
+      fft2_p(w, s0, s0 + 4, p01);
+      fft2_p(w, s0 + 8, s0 + 12, p23);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  xposep(w, lds, q, lane);
+  fftp_block<16>(w, 64 * q);  // dist 16, 4, 1 (bits 5 .. 0)
+  // erased shards = work * (65535 - errLocs)
+#pragma unroll
+  for (int j0 = 0; j0 < 64; j0 += 8) {
+    if (((pm >> j0) & 0xFFull) == 0xFFull) continue;  // uniform
+    uint32_t prod[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) prod[u] = mul16_prod(mx, mlogx, kMod16 - __builtin_amdgcn_readlane(my_err, j0 + u));
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int j = j0 + u;
+      if ((pm >> j) & 1) continue;  // uniform
+      const int i = 64 * q + j;
+      const int shard = i < K ? K + i : i - K;
+      uint32_t t[16];
+      mul16_pack(prod[u], t);
+      const uint32_t r = mulp(w.v[j], t);
+      const uint32_t so = (uint32_t)shard * (uint32_t)a.shard_stride;
+      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(r & 0xFFFFu), rsrc, col, so, 0);
+      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(r >> 16), rsrc, col + 32u, so, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // Tables are module globals: upload once per device.
 std::mutex g_tab_mu;
 bool g_tab_done[64];
@@ -888,6 +1127,10 @@ hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mar
     DecodeArgs b = a;
     b.nchunk = (a.shard_bytes + 511) / 512;
     hipLaunchKernelGGL(leo16_decode_reg_kernel, dim3((unsigned)(nv * b.nchunk)), dim3(kDecN), 0, s, b);
+  } else if (a.k == kDec1k / 2 && a.shard_bytes % 256 == 0) {  // k = 512: 256-B pieces
+    DecodeArgs b = a;
+    b.nchunk = a.shard_bytes / 256;
+    hipLaunchKernelGGL(leo16_decode_reg1k_kernel, dim3((unsigned)(nv * b.nchunk)), dim3(kDec1k), 0, s, b);
   } else
 #endif
   {

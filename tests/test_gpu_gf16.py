@@ -76,6 +76,27 @@ def test_gf16_decode_matches_oracle(ctx):
     assert b"".join(got) == want.tobytes() == full.tobytes()
 
 
+@pytest.mark.parametrize("shard", [256, 512, 1024])
+def test_gf16_decode_k512_matches_oracle(ctx, shard):
+    """k = 512 (n = 1024): shards that are whole 256-B pieces take the
+    register-resident decoder (leo16_decode_reg1k_kernel); random erasure
+    patterns with k .. 2k-1 survivors, only parity and only data present."""
+    k = 512
+    rng = np.random.default_rng(shard)
+    data = rng.integers(0, 256, (k, shard), dtype=np.uint8)
+    full = np.concatenate([data, oracle.encode(data)])
+    codec = da.LeoRSCodec(ctx)
+    pats = [np.isin(np.arange(2 * k), rng.choice(2 * k, k + extra, replace=False)) for extra in (0, 1, 100, k - 1)]
+    pats += [np.arange(2 * k) >= k, np.arange(2 * k) < k]
+    for present in pats:
+        present = present.astype(np.uint8)
+        damaged = full * present[:, None]
+        if shard == 256:
+            assert (oracle.decode(damaged, present) == full).all()
+        got = codec.decode([damaged[i].tobytes() if present[i] else None for i in range(2 * k)])
+        assert b"".join(got) == full.tobytes()
+
+
 def test_gf16_decode_too_few(ctx):
     k = 256
     shards = [bytes(64)] * (k - 1) + [None] * (k + 1)
@@ -99,8 +120,8 @@ def test_gf16_extend_matches_oracle(ctx, k):
         dah.validate_basic()
 
 
-def test_gf16_repair_max_erasure(ctx):
-    k = 256
+@pytest.mark.parametrize("k", [256, 512])
+def test_gf16_repair_max_erasure(ctx, k):
     ods = synth.random_blob_square(k, 77)
     eds, rr, cr, _ = oracle.extend_and_dah(ods, k, nthreads=8)
     rng = np.random.default_rng(5)
