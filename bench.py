@@ -193,6 +193,8 @@ def main():
     ap.add_argument("--split-steps", type=int, default=3)
     ap.add_argument("--no-split", action="store_true", help="skip the split stress at N > 1")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end measurement")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the configs[2] mixed batch and configs[3] repair lines of the default run")
     ap.add_argument("--replay-blocks", type=int, default=8192, help="configs[4] block replay length")
     ap.add_argument("--no-replay", action="store_true", help="skip the block replay measurement")
     ap.add_argument("--replay-dump", default=None,
@@ -326,6 +328,17 @@ def main():
         out["end_to_end"] = bench_e2e(ctx, local, k, np.stack([host[i % nd] for i in range(B)]),
                                       max(3, args.steps // 4))
         out["end_to_end"]["single_square"] = bench_single(ctx)
+    if world == 1 and not args.no_configs:
+        # configs[2] and configs[3] (and the GF(2^16) stress repair) at bounded
+        # step counts, so that the driver's own run records them too
+        if "ds" in locals():
+            del ds
+            torch.cuda.empty_cache()
+        out["other_configs"] = {
+            "configs[2]_mixed_4096": run_mixed(ctx, 3, 1),
+            "configs[3]_repair_k128": run_repair(ctx, 128, 256, 3, 1),
+            "repair_k512_gf16": run_repair(ctx, 512, 2, 2, 1),
+        }
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.cpu_threads or host_threads())
         out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
@@ -637,15 +650,14 @@ def mixed_batch(ctx, dev=0):
     return ks, groups, hosts
 
 
-def bench_mixed(args):
+def run_mixed(ctx, steps, warmup):
     """configs[2]: a batch of 4096 distinct mixed-size squares (k = 2^u,
-    u ~ U{0..7}, seeded), one launch sequence per distinct k per step.
-    bit_exact: the concurrent run's DAHs equal the one-stream run's and the
-    host API's (dagpu_extend_batch) for every square, every status is 0."""
+    u ~ U{0..7}, seeded), one launch sequence per distinct k per step, each k
+    group on its own stream.  bit_exact (fatal if false): the concurrent run's
+    DAHs equal the one-stream run's and the host API's (dagpu_extend_batch) for
+    every square, every status is 0."""
     from celestia_da import da
 
-    torch.cuda.set_device(0)
-    ctx = da.Context(0)
     ks, groups, hosts = mixed_batch(ctx)
     # Squares of different k are independent: each k group runs on its own
     # stream (forked from and joined back to the current one), so the small-k
@@ -665,11 +677,11 @@ def bench_mixed(args):
                 cur.wait_stream(st)
 
     def timed(concurrent):
-        for _ in range(args.warmup):
+        for _ in range(warmup):
             step(concurrent)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
+        for _ in range(steps):
             step(concurrent)
         torch.cuda.synchronize()
         return time.perf_counter() - t0
@@ -694,35 +706,46 @@ def bench_mixed(args):
         print("FATAL: mixed batch results differ between runs / the host API", file=sys.stderr)
         raise SystemExit(3)
     comp = sum(sum(compressions(k)) for k in ks)
-    out = {"metric": "mixed-batch squares/sec (4096 squares, k=1..128)", "value": 4096 * args.steps / el,
+    del groups
+    torch.cuda.empty_cache()
+    return {"squares_per_s": 4096 * steps / el, "ms_per_step": el / steps * 1e3, "steps": steps,
+            "sha256_compressions_per_s": comp * steps / el, "streams": len(streams),
+            "one_stream_ms_per_step": serial / steps * 1e3, "bit_exact": bool(ok),
+            "squares_per_k": {str(k): ks.count(k) for k in sorted(set(ks))}}
+
+
+def bench_mixed(args):
+    from celestia_da import da
+
+    torch.cuda.set_device(0)
+    r = run_mixed(da.Context(0), args.steps, args.warmup)
+    out = {"metric": "mixed-batch squares/sec (4096 squares, k=1..128)", "value": r["squares_per_s"],
            "unit": "squares/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-           "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "dtype": "u8",
+           "ms_per_step": r["ms_per_step"], "higher_is_better": True, "dtype": "u8",
            "data": "synthetic random-namespace blob shares, 4096 distinct squares",
-           "sha256_compressions_per_s": comp * args.steps / el,
-           "streams": len(streams), "one_stream_ms_per_step": serial / args.steps * 1e3,
-           "bit_exact": bool(ok),
-           "config": {"workload": "configs[2]: 4096 mixed squares per step",
-                      "squares_per_k": {str(k): ks.count(k) for k in sorted(set(ks))}}}
+           "sha256_compressions_per_s": r["sha256_compressions_per_s"], "streams": r["streams"],
+           "one_stream_ms_per_step": r["one_stream_ms_per_step"], "bit_exact": r["bit_exact"],
+           "config": {"workload": "configs[2]: 4096 mixed squares per step", "squares_per_k": r["squares_per_k"]}}
     print(json.dumps(out), flush=True)
 
 
-def bench_repair(args):
-    """configs[3]: rsmt2d Repair of k x k squares with the maximal recoverable
-    erasure pattern (a random k x k sub-grid kept, 3k^2 cells erased), every
-    row/column root re-verified.  Timed with HIP events around the repair only
-    (each step first restores the damaged input)."""
-    from celestia_da import da, synth
+REPAIR_SEED = 777
+
+
+def run_repair(ctx, k, B, steps, warmup, distinct=None):
+    """configs[3]: rsmt2d Repair of B distinct k x k squares with the maximal
+    recoverable erasure pattern (a random k x k sub-grid kept, 3k^2 cells
+    erased), every row/column root re-verified.  Timed with HIP events around
+    the repair only (each step first restores the damaged input).  bit_exact
+    (fatal if false): the repaired EDS equals the extended one, status 0."""
+    from celestia_da import synth
     from celestia_da.device import DeviceSquares
 
-    torch.cuda.set_device(0)
-    ctx = da.Context(0)
-    k, B = args.k, args.batch
     w = 2 * k
     ds = DeviceSquares(k, B, ctx=ctx)
-    nd = min(args.distinct, B)
-    host = np.stack([synth.random_blob_square(k, 777 + i).reshape(-1) for i in range(nd)])
-    for i in range(B):
-        ds.ods[i].copy_(torch.from_numpy(host[i % nd]))
+    nd = min(distinct or B, B)
+    host = synth.blob_squares(k, REPAIR_SEED, 0, nd, threads=host_threads())
+    ds.load_ods(np.stack([host[i % nd] for i in range(B)]))
     ds.extend()
     rng = np.random.default_rng(5)
     pres = np.zeros((B, w, w), np.uint8)
@@ -734,23 +757,37 @@ def bench_repair(args):
     present = pres_t.clone()
     status = torch.zeros(B, dtype=torch.int32, device="cuda")
     ws = ds.repair_workspace()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    for i in range(args.warmup + args.steps):
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for i in range(warmup + steps):
         ds.eds.copy_(damaged)
         present.copy_(pres_t)
-        if i >= args.warmup:
-            ev[i - args.warmup][0].record()
+        if i >= warmup:
+            ev[i - warmup][0].record()
         ds.repair(present, status, ws)
-        if i >= args.warmup:
-            ev[i - args.warmup][1].record()
+        if i >= warmup:
+            ev[i - warmup][1].record()
     torch.cuda.synchronize()
     ok = bool(torch.equal(ds.eds, ref)) and int(status.abs().sum()) == 0
-    ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-    out = {"metric": f"Repair squares/sec (k={k}, maximal erasure, roots re-verified)",
-           "value": B / (ms * 1e-3), "unit": "squares/s", "n_gpus": 1, "steps": args.steps,
-           "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "bit_exact": ok,
-           "decode_gbs": rs_bytes(k) * B / (ms * 1e-3) / 1e9,
-           "config": {"workload": f"configs[3]: {B} squares {k}x{k}, 3k^2 cells erased each"}}
+    if not ok:
+        print(f"FATAL: repair k={k} did not restore the extended square", file=sys.stderr)
+        raise SystemExit(3)
+    ms = sum(a.elapsed_time(b) for a, b in ev) / steps
+    del ds, ref, damaged, ws
+    torch.cuda.empty_cache()
+    return {"k": k, "squares": B, "squares_per_s": B / (ms * 1e-3), "ms_per_step": ms, "steps": steps,
+            "bit_exact": ok, "decode_gbs": rs_bytes(k) * B / (ms * 1e-3) / 1e9}
+
+
+def bench_repair(args):
+    from celestia_da import da
+
+    torch.cuda.set_device(0)
+    r = run_repair(da.Context(0), args.k, args.batch, args.steps, args.warmup, args.distinct)
+    out = {"metric": f"Repair squares/sec (k={args.k}, maximal erasure, roots re-verified)",
+           "value": r["squares_per_s"], "unit": "squares/s", "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": r["ms_per_step"], "higher_is_better": True,
+           "bit_exact": r["bit_exact"], "decode_gbs": r["decode_gbs"],
+           "config": {"workload": f"configs[3]: {args.batch} squares {args.k}x{args.k}, 3k^2 cells erased each"}}
     print(json.dumps(out), flush=True)
 
 

@@ -7,7 +7,7 @@ rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/gpu_tests.log
 if [ $rc -ne 0 ]; then grep -E "FAILED|Error|assert" gpurun_out/gpu_tests.log | head -20; exit $rc; fi
 for spec in "$@"; do
   label=${spec%%:*}; rest=${spec#*:}; envs=${rest%%:*}; args=${rest#*:}
-  env $envs timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --no-cpu --no-e2e --no-replay $args > gpurun_out/ab_$label.log 2>&1
+  env $envs timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --no-cpu --no-e2e --no-replay --no-configs $args > gpurun_out/ab_$label.log 2>&1
   rc=$?
   if [ $rc -ne 0 ]; then echo "$label rc=$rc"; tail -5 gpurun_out/ab_$label.log; exit $rc; fi
   python - "$label" gpurun_out/ab_$label.log <<'PY'
