@@ -12,6 +12,8 @@
 //      (k = 128 shards x 512 B), does `ops` fast xor/bitop3 ops per data dword
 //      group, writes 64 KB.
 // Prints ms alone and concurrent (two non-blocking streams).
+// argv: <sha LDS KB> <rs variant> [sha WG size] [sha persistent WGs per CU] [work queue 0/1] [variant 5: rs WGs per CU]
+// rs variant 5 = rs2 as a persistent grid taking groups from a counter
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++20 tools/overlap_probe.hip -o tools/overlap_probe
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -36,8 +38,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
   u32x4 nx[4];
 #pragma unroll
   for (int q = 0; q < 4; q++) nx[q] = p[q];
-#pragma unroll 1
-  for (int b = 0; b < 9; b++) {
+#pragma unroll
+  for (int b = 0; b < 9; b++) {  // unrolled: ~9 compression sites of code, like nmt_leaf_kernel's 27 KB
     uint32_t w[16];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -51,6 +53,71 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
   }
   if (threadIdx.x == 0 && n < 0) cap[0] = st[0];
   out[i] = st[0] ^ st[7];
+}
+
+// persistent form: a fixed grid (wgs_per_cu x CUs) strides over the leaves, so
+// the SHA work holds a bounded number of wave slots without claiming LDS
+__global__ __launch_bounds__(256) void sha_persist_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                          long n) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    uint32_t st[8];
+    sha256_init(st);
+    const u32x4* p = (const u32x4*)(in + i * 144);
+    u32x4 nx[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) nx[q] = p[q];
+#pragma unroll
+    for (int b = 0; b < 9; b++) {
+      uint32_t w[16];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        w[4 * q] = nx[q].x; w[4 * q + 1] = nx[q].y; w[4 * q + 2] = nx[q].z; w[4 * q + 3] = nx[q].w;
+      }
+      if (b + 1 < 9) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) nx[q] = p[(b + 1) * 4 + q];
+      }
+      sha256_compress(st, w);
+    }
+    out[i] = st[0] ^ st[7];
+  }
+}
+
+// work-queue form: a fixed grid, each workgroup grabs 256 leaves at a time from
+// a counter, so workgroups that become resident late simply take less work
+__global__ __launch_bounds__(256) void sha_queue_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                        long n, unsigned long long* counter) {
+  __shared__ long base_s;
+  for (;;) {
+    if (threadIdx.x == 0) base_s = (long)atomicAdd(counter, 256ull);
+    __syncthreads();
+    const long base = base_s;
+    __syncthreads();
+    if (base >= n) return;
+    const long i = base + threadIdx.x;
+    if (i < n) {
+      uint32_t st[8];
+      sha256_init(st);
+      const u32x4* p = (const u32x4*)(in + i * 144);
+      u32x4 nx[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) nx[q] = p[q];
+#pragma unroll
+      for (int b = 0; b < 9; b++) {
+        uint32_t w[16];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          w[4 * q] = nx[q].x; w[4 * q + 1] = nx[q].y; w[4 * q + 2] = nx[q].z; w[4 * q + 3] = nx[q].w;
+        }
+        if (b + 1 < 9) {
+#pragma unroll
+          for (int q = 0; q < 4; q++) nx[q] = p[(b + 1) * 4 + q];
+        }
+        sha256_compress(st, w);
+      }
+      out[i] = st[0] ^ st[7];
+    }
+  }
 }
 
 template <int OPS>
@@ -81,10 +148,31 @@ __global__ __launch_bounds__(256) void rs_kernel(const u32x4* __restrict__ in, u
 // rs2: the L1 shape -- a 4-wave workgroup holds 128 KB (two 64-KB vectors):
 // 128 data dwords per lane (~200 VGPRs), one 64-KB LDS exchange (2 passes).
 template <int OPS>
+__device__ __forceinline__ void rs2_body(const u32x4* __restrict__ in, u32x4* __restrict__ out, long v, u32x4* lds);
+template <int OPS>
 __global__ __launch_bounds__(256) void rs2_kernel(const u32x4* __restrict__ in, u32x4* __restrict__ out, long ngrp) {
   __shared__ u32x4 lds[4096];  // 64 KB
   const long v = blockIdx.x;
   if (v >= ngrp) return;
+  rs2_body<OPS>(in, out, v, lds);
+}
+// persistent rs2: a fixed grid takes groups from a counter
+template <int OPS>
+__global__ __launch_bounds__(256) void rs2_queue_kernel(const u32x4* __restrict__ in, u32x4* __restrict__ out, long ngrp,
+                                                        unsigned long long* counter) {
+  __shared__ u32x4 lds[4096];  // 64 KB
+  __shared__ long v_s;
+  for (;;) {
+    __syncthreads();
+    if (threadIdx.x == 0) v_s = (long)atomicAdd(counter, 1ull);
+    __syncthreads();
+    const long v = v_s;
+    if (v >= ngrp) return;
+    rs2_body<OPS>(in, out, v, lds);
+  }
+}
+template <int OPS>
+__device__ __forceinline__ void rs2_body(const u32x4* __restrict__ in, u32x4* __restrict__ out, long v, u32x4* lds) {
   const u32x4* src = in + v * 8192;  // 128 KB per group
   u32x4* dst = out + v * 8192;
   uint32_t x[128];
@@ -182,6 +270,33 @@ __global__ __launch_bounds__(256) void rs4_kernel(const u32x4* __restrict__ in, 
   for (int j = 0; j < 32; j++) dst[j * 256 + threadIdx.x] = (u32x4){x[4 * j], x[4 * j + 1], x[4 * j + 2], x[4 * j + 3]};
 }
 
+// rs5: variant 0 with the op loop fully unrolled (~60 KB of straight-line code,
+// the size of a real k = 128 encoder) -- does instruction-cache pressure spoil
+// the overlap with the SHA kernel?
+template <int OPS>
+__global__ __launch_bounds__(256) void rs5_kernel(const u32x4* __restrict__ in, u32x4* __restrict__ out, long nvec) {
+  const long v = blockIdx.x;
+  if (v >= nvec) return;
+  const u32x4* src = in + v * 4096;
+  u32x4* dst = out + v * 4096;
+  uint32_t x[64];
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    const u32x4 d = src[j * 256 + threadIdx.x];
+    x[4 * j] = d.x; x[4 * j + 1] = d.y; x[4 * j + 2] = d.z; x[4 * j + 3] = d.w;
+  }
+#pragma unroll
+  for (int r = 0; r < OPS; r++) {
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+      const uint32_t a = x[(j + 1) & 63], b = x[(j + 7) & 63];
+      asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(x[j]) : "v"(a), "v"(b));
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 16; j++) dst[j * 256 + threadIdx.x] = (u32x4){x[4 * j], x[4 * j + 1], x[4 * j + 2], x[4 * j + 3]};
+}
+
 int main(int argc, char** argv) {
   const long ncell = 256L * 65536;  // leaves per 256-square step
   const long nvec = 256L * 384;  // RS vectors per step (k = 128, 64 KB each)
@@ -201,7 +316,23 @@ int main(int argc, char** argv) {
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
   const int shab = argc > 3 ? atoi(argv[3]) : 256;  // sha workgroup size
+  const int persist = argc > 4 ? atoi(argv[4]) : 0;  // SHA workgroups per CU (persistent grid), 0 = off
+  const int queue = argc > 5 ? atoi(argv[5]) : 0;  // 1: the persistent grid takes work from a queue
+  const int rs_wgs = argc > 6 ? atoi(argv[6]) : 1;  // variant 5: persistent rs2 workgroups per CU
+  unsigned long long* counter;
+  unsigned long long* rcounter;
+  (void)hipMalloc(&counter, 8);
+  (void)hipMalloc(&rcounter, 8);
   auto sha = [&](hipStream_t s) {
+    if (persist > 0 && queue) {
+      (void)hipMemsetAsync(counter, 0, 8, s);
+      hipLaunchKernelGGL(sha_queue_kernel, dim3(256 * persist), dim3(256), 0, s, shin, shout, ncell, counter);
+      return;
+    }
+    if (persist > 0) {
+      hipLaunchKernelGGL(sha_persist_kernel, dim3(256 * persist), dim3(256), 0, s, shin, shout, ncell);
+      return;
+    }
     hipLaunchKernelGGL(sha_kernel, dim3((unsigned)((ncell + shab - 1) / shab)), dim3(shab), lds_kb * 1024, s, shin, shout, ncell);
   };
   const int variant = argc > 2 ? atoi(argv[2]) : 0;
@@ -209,7 +340,12 @@ int main(int argc, char** argv) {
     if (variant == 0) hipLaunchKernelGGL(rs_kernel<52>, dim3((unsigned)nvec), dim3(256), 0, s, rin, rout, nvec);
     else if (variant == 1) hipLaunchKernelGGL(rs2_kernel<55>, dim3((unsigned)(nvec / 2)), dim3(256), 0, s, rin, rout, nvec / 2);
     else if (variant == 2) hipLaunchKernelGGL(rs3_kernel<52>, dim3((unsigned)nvec), dim3(256), 0, s, rin, rout, nvec);
-    else hipLaunchKernelGGL(rs4_kernel<55>, dim3((unsigned)(nvec / 2)), dim3(256), 0, s, rin, rout, nvec / 2);
+    else if (variant == 3) hipLaunchKernelGGL(rs4_kernel<55>, dim3((unsigned)(nvec / 2)), dim3(256), 0, s, rin, rout, nvec / 2);
+    else if (variant == 5) {
+      (void)hipMemsetAsync(rcounter, 0, 8, s);
+      hipLaunchKernelGGL(rs2_queue_kernel<55>, dim3((unsigned)(256 * rs_wgs)), dim3(256), 0, s, rin, rout, nvec / 2, rcounter);
+    }
+    else hipLaunchKernelGGL(rs5_kernel<90>, dim3((unsigned)nvec), dim3(256), 0, s, rin, rout, nvec);
   };
   auto timeit = [&](const char* name, auto fn) {
     fn();
@@ -224,7 +360,8 @@ int main(int argc, char** argv) {
       (void)hipEventElapsedTime(&ms, e0, e1);
       if (ms < best) best = ms;
     }
-    printf("{\"probe\":\"%s\",\"variant\":%d,\"sha_wg\":%d,\"lds_kb\":%d,\"ms\":%.3f}\n", name, variant, shab, lds_kb, best);
+    printf("{\"probe\":\"%s\",\"variant\":%d,\"sha_wg\":%d,\"lds_kb\":%d,\"sha_persist_wg_per_cu\":%d,\"queue\":%d,\"ms\":%.3f}\n", name,
+           variant, shab, lds_kb, persist, queue, best);
     fflush(stdout);
   };
   // the default stream (0) is blocking w.r.t. nothing here: sa/sb are non-blocking,
