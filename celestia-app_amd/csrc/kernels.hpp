@@ -74,6 +74,10 @@ __device__ __forceinline__ long err_vec(const DecodeArgs& a, long v) { return a.
 hipError_t launch_leo8_decode(const DecodeArgs& a, hipStream_t s, bool mark_present);
 hipError_t launch_leo8_errlocs(const DecodeArgs& a, hipStream_t s);
 hipError_t launch_leo8_decode_only(const DecodeArgs& a, hipStream_t s, bool mark_present);
+// bit-sliced k = 128 decode (rs_decode_sliced.hip); launch_leo8_decode_only
+// uses it whenever leo8_decode_sliced_applicable() holds
+bool leo8_decode_sliced_applicable(const DecodeArgs& a);
+hipError_t launch_leo8_decode128_sliced(const DecodeArgs& a, hipStream_t s);
 
 // GF(2^16) (rs_gf16.hip) and the field dispatch the host runtime uses:
 // GF(2^8) for k <= 128, GF(2^16) for 256 <= k <= kMaxK.  DecodeArgs.err then

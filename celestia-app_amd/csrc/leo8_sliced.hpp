@@ -368,5 +368,200 @@ __host__ __device__ __forceinline__ void fft_A2(uint32_t (&v)[16][8], int w, uin
   });
 }
 
+
+// ---------------------------------------------------------------------------
+// Bit-sliced decode for k = 128 (rs_decode.hip leo8_decode128_sliced_kernel):
+// leopard8.go reconstruct's IFFT_256 and FFT_256 (decoder skew index b + D - 1,
+// no +k offset) on n = 256 work elements, one vector per 4-wave workgroup.
+// Lane l = t + 16 eb: t = 32-byte column block, eb = TWO element bits; wave w.
+//   A: e = j + 16 eb + 64 w   (j = register)  -- layers 0..3
+//   B: e = eb + 4 w + 16 i    (i = register)  -- layers 4..7, skews compile-time
+// In A the skew of layer m splits (skew_split_ok, bits up to 7) into
+//   C(j) ^ eb0 S16 ^ eb1 S32 ^ w0 S64 ^ w1 S128,  S_x = skew(2^m - 1 + x).
+// ---------------------------------------------------------------------------
+
+// t = C * y from scratch (no accumulator): the first set bit of a row is the
+// plane itself, the rest are consumed two at a time by xor3.
+template <int R>
+__host__ __device__ __forceinline__ uint32_t row_sum(const uint32_t (&y)[8]) {
+  constexpr int J = __builtin_ctz(R);
+  return xor_row<R & ~((2 << J) - 1), J + 1>(y[J], y);
+}
+// x ^= (C * y) & mask: the lane-bit part of a layout-A skew.  One and-xor per
+// output plane on top of the row sums (cheaper than masking the 8 inputs).
+template <int C>
+__host__ __device__ __forceinline__ void muladd_ct_lane(uint32_t (&x)[8], const uint32_t (&y)[8], uint32_t mask) {
+  static_for<8>([&](auto i) {
+    constexpr int R = kMat.row[C][i];
+    if constexpr (R != 0) x[i] = SL_BOP3(x[i], row_sum<R>(y), mask, kXorAnd);
+  });
+}
+
+// Decoder layers 0..3 in layout A (IFFT ascending, FFT descending).
+// IFFT butterfly (ifftDIT8): y ^= x; x ^= skew * y.  FFT (fftDIT8): x ^= skew * y; y ^= x.
+template <bool IFFT>
+__host__ __device__ __forceinline__ void dec_A(uint32_t (&v)[16][8], int w, uint32_t eb0mask, uint32_t eb1mask) {
+  static_for<4>([&](auto mm) {
+    constexpr int m = IFFT ? (int)mm : 3 - (int)mm;
+    constexpr int D = 1 << m;
+    SL_FENCE();
+    if constexpr (IFFT) {
+      static_for<16>([&](auto j) {
+        if constexpr (!(j & D)) xor8(v[j + D], v[j]);
+      });
+    }
+    static_for<16>([&](auto j) {
+      if constexpr (!(j & D)) muladd_ct<skew_elem(D - 1 + (j & ~(2 * D - 1)))>(v[j], v[j + D]);
+    });
+    if (w & 1) {
+      static_for<16>([&](auto j) {
+        if constexpr (!(j & D)) muladd_ct<skew_elem(D - 1 + 64)>(v[j], v[j + D]);
+      });
+    }
+    if (w & 2) {
+      static_for<16>([&](auto j) {
+        if constexpr (!(j & D)) muladd_ct<skew_elem(D - 1 + 128)>(v[j], v[j + D]);
+      });
+    }
+    static_for<16>([&](auto j) {
+      if constexpr (!(j & D)) muladd_ct_lane<skew_elem(D - 1 + 16)>(v[j], v[j + D], eb0mask);
+    });
+    static_for<16>([&](auto j) {
+      if constexpr (!(j & D)) muladd_ct_lane<skew_elem(D - 1 + 32)>(v[j], v[j + D], eb1mask);
+    });
+    if constexpr (!IFFT) {
+      static_for<16>([&](auto j) {
+        if constexpr (!(j & D)) xor8(v[j + D], v[j]);
+      });
+    }
+  });
+}
+
+// Decoder layers 4..7 in layout B: register bit rb of i is element bit 4 + rb,
+// block start b = 16 (i with register bits <= rb cleared) -- compile-time.
+template <bool IFFT>
+__host__ __device__ __forceinline__ void dec_B(uint32_t (&v)[16][8]) {
+  static_for<4>([&](auto rr) {
+    constexpr int rb = IFFT ? (int)rr : 3 - (int)rr;
+    constexpr int D = 16 << rb, R = 1 << rb;
+    SL_FENCE();
+    static_for<16>([&](auto i) {
+      if constexpr (!(i & R)) {
+        constexpr int c = skew_elem(D - 1 + 16 * (i & ~(2 * R - 1)));
+        if constexpr (IFFT) {
+          xor8(v[i + R], v[i]);
+          muladd_ct<c>(v[i], v[i + R]);
+        } else {
+          muladd_ct<c>(v[i], v[i + R]);
+          xor8(v[i + R], v[i]);
+        }
+      }
+    });
+  });
+}
+
+// Formal derivative (leopard8.go: for i in 1..n-1, work[i-lowbit(i), i) ^=
+// work[i, i+lowbit(i))) in closed form: D(x)_e = x_e ^ XOR over bits s with
+// e_s = 0 of x_(e | 2^s), ORIGINAL x.  The register bits of the layout are
+// applied in place in ascending register order (v[j | 2^sb] > j is still
+// original when j is processed); the caller adds the other bits' terms.
+// Planes [P0, P0 + NP).
+template <int P0, int NP>
+__host__ __device__ __forceinline__ void deriv_local(uint32_t (&v)[16][8]) {
+  static_for<16>([&](auto j) {
+    static_for<4>([&](auto sb) {
+      if constexpr (!((j >> sb) & 1)) {
+        static_for<NP>([&](auto p) { v[j][P0 + p] ^= v[j | (1 << sb)][P0 + p]; });
+      }
+    });
+  });
+}
+
+// x * c for a per-lane field element c (the decoder's error-locator
+// multiplies).  c is given in the power basis of G = 94: c = XOR over bits k of
+// cp of G^k (kDecPow below maps a log value to that form), so
+//   x * c = XOR over bits k of cp of (x * G^k),
+// a chain of compile-time multiplies by G -- 8 ops each, the cheapest such G
+// (every row of its matrix has at most 3 set bits) -- and one and-xor per
+// plane and power.  Only full-rate ops (no v_perm table lookups).
+constexpr int kDecG = 94;
+
+struct DecPow {
+  uint8_t cp[256];  // cp[lm]: exp(lm) in the power basis of G (exp(255) = exp(0) = 1)
+};
+constexpr DecPow make_decpow() {
+  // columns G^0..G^7; solve c = P * cp by Gaussian elimination over GF(2)
+  uint8_t pw[8] = {};
+  pw[0] = 1;
+  for (int k = 1; k < 8; k++) pw[k] = gmul(pw[k - 1], (uint8_t)kDecG);
+  DecPow t{};
+  for (int lm = 0; lm < 256; lm++) {
+    const uint8_t c = kGf8.exp[lm];
+    // augmented rows: bit i of each column k, plus the target bit i of c
+    uint16_t row[8] = {};
+    for (int i = 0; i < 8; i++) {
+      uint16_t r = 0;
+      for (int k = 0; k < 8; k++) r |= (uint16_t)(((pw[k] >> i) & 1) << k);
+      r |= (uint16_t)(((c >> i) & 1) << 8);
+      row[i] = r;
+    }
+    int rk = 0;
+    for (int col = 0; col < 8; col++) {
+      int piv = -1;
+      for (int i = rk; i < 8; i++)
+        if ((row[i] >> col) & 1) { piv = i; break; }
+      if (piv < 0) continue;
+      const uint16_t tmp = row[rk]; row[rk] = row[piv]; row[piv] = tmp;
+      for (int i = 0; i < 8; i++)
+        if (i != rk && ((row[i] >> col) & 1)) row[i] ^= row[rk];
+      rk++;
+    }
+    uint8_t cp = 0;
+    for (int i = 0; i < 8; i++)
+      for (int col = 0; col < 8; col++)
+        if (row[i] & (1 << col)) { cp |= (uint8_t)(((row[i] >> 8) & 1) << col); break; }
+    t.cp[lm] = cp;
+  }
+  return t;
+}
+inline constexpr DecPow kDecPow = make_decpow();
+constexpr bool decpow_ok() {
+  uint8_t pw[8] = {};
+  pw[0] = 1;
+  for (int k = 1; k < 8; k++) pw[k] = gmul(pw[k - 1], (uint8_t)kDecG);
+  for (int lm = 0; lm < 256; lm++) {
+    uint8_t c = 0;
+    for (int k = 0; k < 8; k++)
+      if ((kDecPow.cp[lm] >> k) & 1) c ^= pw[k];
+    if (c != kGf8.exp[lm]) return false;
+  }
+  return true;
+}
+static_assert(decpow_ok(), "power-basis table of the decoder's runtime multiplies");
+
+__host__ __device__ __forceinline__ void mul_lane(uint32_t (&x)[8], uint32_t cp) {
+  uint32_t acc[8], cur[8];
+  {
+    const uint32_t m = (uint32_t)(-(int32_t)(cp & 1u));
+    static_for<8>([&](auto p) {
+      cur[p] = x[p];
+      acc[p] = x[p] & m;
+    });
+  }
+  static_for<7>([&](auto kk) {
+    constexpr int k = kk + 1;
+    uint32_t n[8];
+    static_for<8>([&](auto i) {
+      constexpr int R = kMat.row[kDecG][i];
+      n[i] = row_sum<R>(cur);
+    });
+    const uint32_t m = (uint32_t)(-(int32_t)((cp >> k) & 1u));
+    static_for<8>([&](auto p) {
+      cur[p] = n[p];
+      acc[p] = SL_BOP3(acc[p], n[p], m, kXorAnd);
+    });
+  });
+  static_for<8>([&](auto p) { x[p] = acc[p]; });
+}
 }  // namespace sliced
 }  // namespace dagpu

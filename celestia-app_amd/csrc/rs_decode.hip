@@ -440,6 +440,10 @@ hipError_t launch_leo8_decode_only(const DecodeArgs& a, hipStream_t s, bool mark
     case 32: e = launch_dec<32>(a, s); break;
     case 64: e = launch_dec<64>(a, s); break;
     case 128: {
+      if (leo8_decode_sliced_applicable(a)) {
+        e = launch_leo8_decode128_sliced(a, s);
+        break;
+      }
       const long nc = (a.shard_bytes + 255) / 256;
       hipLaunchKernelGGL(leo8_decode128_kernel, dim3((unsigned)(nv * nc)), dim3(kD4Threads), 0, s, a, (int)nc);
       e = hipGetLastError();

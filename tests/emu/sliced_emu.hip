@@ -138,3 +138,116 @@ extern "C" uint32_t sliced_emu_bop3(uint32_t a, uint32_t b, uint32_t c, int tt) 
   return sl_bop3_host(a, b, c, (uint8_t)tt);
 }
 extern "C" int sliced_emu_gmul(int a, int c) { return gmul((uint8_t)a, (uint8_t)c); }
+
+// ---------------------------------------------------------------------------
+// Bit-sliced k = 128 decode (csrc/rs_decode_sliced.hip): the kernel's error
+// locators (leo8_errlocs_kernel), premultiply, dec_A / dec_B, formal
+// derivative and postmultiply, with the 16 (wave w, lane group eb) lanes of a
+// column block as loops and the LDS passes as copies.
+// ---------------------------------------------------------------------------
+namespace {
+
+uint32_t add_mod8(uint32_t a, uint32_t b) { const uint32_t s = a + b; return (s + (s >> 8)) & 0xFFu; }
+uint32_t sub_mod8(uint32_t a, uint32_t b) { const uint32_t d = a - b; return (d + (d >> 8)) & 0xFFu; }
+
+void fwht256(uint32_t* e, int mtrunc) {
+  for (int dist = 1; dist <= 64; dist *= 4) {
+    const int dist4 = dist * 4;
+    for (int g = 0; g < 64; g++) {
+      const int r = (g / dist) * dist4;
+      const int i = r + (g % dist);
+      if (r >= mtrunc) continue;
+      const uint32_t t0 = e[i], t1 = e[i + dist], t2 = e[i + 2 * dist], t3 = e[i + 3 * dist];
+      const uint32_t a0 = add_mod8(t0, t1), a1 = sub_mod8(t0, t1);
+      const uint32_t a2 = add_mod8(t2, t3), a3 = sub_mod8(t2, t3);
+      e[i] = add_mod8(a0, a2);
+      e[i + 2 * dist] = sub_mod8(a0, a2);
+      e[i + dist] = add_mod8(a1, a3);
+      e[i + 3 * dist] = sub_mod8(a1, a3);
+    }
+  }
+}
+
+int elemA(int r, int eb, int w) { return r + 16 * eb + 64 * w; }
+int elemB(int r, int eb, int w) { return eb + 4 * w + 16 * r; }
+
+}  // namespace
+
+// shards: 256 x shard bytes, [data 128][parity 128] (shard order), repaired in
+// place; present: 256 flags in shard order.  Returns -1 on bad arguments.
+extern "C" int sliced_dec_emu(long shard, uint8_t* shards, const uint8_t* present) {
+  constexpr int K = 128, N = 256;
+  if (shard <= 0 || shard % 512) return -1;
+  auto shard_of = [&](int e) { return e < K ? e + K : e - K; };  // work index -> shard
+  uint32_t err[N];
+  for (int i = 0; i < N; i++) err[i] = present[shard_of(i)] ? 0u : 1u;
+  fwht256(err, N);
+  for (int i = 0; i < N; i++) err[i] = (err[i] * dagpu::kGf8.walsh[i]) % 255u;
+  fwht256(err, N);
+  static uint32_t st[4][4][16][8], tmp[4][4][16][8], orig[4][4][16][8];
+  for (long c = 0; c < shard; c += 512)
+    for (int t = 0; t < 16; t++) {
+      const long col0 = c + 16 * t;
+      for (int w = 0; w < 4; w++)
+        for (int eb = 0; eb < 4; eb++)
+          for (int j = 0; j < 16; j++) {
+            const int e = elemA(j, eb, w);
+            const uint8_t* src = shards + (long)shard_of(e) * shard;
+            uint32_t d[8];
+            memcpy(d, src + col0, 16);
+            memcpy(d + 4, src + col0 + 256, 16);
+            transpose8(d);
+            mul_lane(d, present[shard_of(e)] ? kDecPow.cp[err[e] & 0xFF] : 0u);
+            memcpy(st[w][eb][j], d, 32);
+          }
+      for (int w = 0; w < 4; w++)
+        for (int eb = 0; eb < 4; eb++)
+          dec_A<true>(st[w][eb], w, (eb & 1) ? 0xFFFFFFFFu : 0u, (eb & 2) ? 0xFFFFFFFFu : 0u);
+      for (int w = 0; w < 4; w++)  // A -> B
+        for (int eb = 0; eb < 4; eb++)
+          for (int i = 0; i < 16; i++) {
+            const int e = elemB(i, eb, w);
+            memcpy(tmp[w][eb][i], st[e >> 6][(e >> 4) & 3][e & 15], 32);
+          }
+      for (int w = 0; w < 4; w++)
+        for (int eb = 0; eb < 4; eb++) dec_B<true>(tmp[w][eb]);
+      memcpy(orig, tmp, sizeof(orig));
+      for (int w = 0; w < 4; w++)
+        for (int eb = 0; eb < 4; eb++) {
+          deriv_local<0, 8>(tmp[w][eb]);
+          for (int i = 0; i < 16; i++) {
+            const int e = elemB(i, eb, w);
+            for (int s = 0; s < 4; s++) {
+              if ((e >> s) & 1) continue;
+              const int f = e | (1 << s);  // partner in layout B: eb' = f & 3, w' = (f >> 2) & 3, i' = f >> 4
+              for (int p = 0; p < 8; p++) tmp[w][eb][i][p] ^= orig[(f >> 2) & 3][f & 3][f >> 4][p];
+            }
+          }
+        }
+      for (int w = 0; w < 4; w++)
+        for (int eb = 0; eb < 4; eb++) dec_B<false>(tmp[w][eb]);
+      for (int w = 0; w < 4; w++)  // B -> A
+        for (int eb = 0; eb < 4; eb++)
+          for (int i = 0; i < 16; i++) {
+            const int e = elemB(i, eb, w);
+            memcpy(st[e >> 6][(e >> 4) & 3][e & 15], tmp[w][eb][i], 32);
+          }
+      for (int w = 0; w < 4; w++)
+        for (int eb = 0; eb < 4; eb++)
+          dec_A<false>(st[w][eb], w, (eb & 1) ? 0xFFFFFFFFu : 0u, (eb & 2) ? 0xFFFFFFFFu : 0u);
+      for (int w = 0; w < 4; w++)
+        for (int eb = 0; eb < 4; eb++)
+          for (int j = 0; j < 16; j++) {
+            const int e = elemA(j, eb, w);
+            if (present[shard_of(e)]) continue;
+            uint32_t d[8];
+            memcpy(d, st[w][eb][j], 32);
+            mul_lane(d, kDecPow.cp[255u - (err[e] & 0xFF)]);
+            transpose8(d);
+            uint8_t* dst = shards + (long)shard_of(e) * shard;
+            memcpy(dst + col0, d, 16);
+            memcpy(dst + col0 + 256, d + 4, 16);
+          }
+    }
+  return 0;
+}
