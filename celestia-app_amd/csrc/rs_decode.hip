@@ -5,7 +5,7 @@
 // (solveCrosswordRow/Col -> rebuildShares), SURVEY.md §3.5 and §8a row A11.
 //
 // Per vector of n = 2k shards with >= k present:
-//   1. error locator (kernel 1, one wave per vector):
+//   1. error locator (kernel 1, one wave per vector, four per workgroup):
 //        errLocs[i] = 1 for each missing position (work layout: [parity k][data k]),
 //        FWHT(errLocs, mtrunc = n); errLocs[i] = errLocs[i]*logWalsh[i] mod 255;
 //        FWHT(errLocs, 256)
@@ -40,9 +40,16 @@ __device__ __forceinline__ uint32_t sub_mod8(uint32_t a, uint32_t b) {
   return (d + (d >> 8)) & 0xFFu;
 }
 
-// fwht8(data, m = 256, mtrunc): 4 radix-4 passes, 64 groups of 4 each.
-__device__ __forceinline__ void fwht256_lds(uint32_t* e, int mtrunc) {
-  const int g = threadIdx.x;  // 0..63
+// fwht8(data, m = 256, mtrunc) by one wave: 4 radix-4 passes, 64 groups of 4
+// each.  Only this wave touches e, and a wave's LDS operations complete in
+// order, so a wave-scope fence is the barrier between passes.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ void fwht256_wave(uint32_t* e, int mtrunc, int g) {
 #pragma unroll
   for (int dist = 1; dist <= 64; dist *= 4) {
     const int dist4 = dist * 4;
@@ -57,42 +64,56 @@ __device__ __forceinline__ void fwht256_lds(uint32_t* e, int mtrunc) {
       e[i + dist] = add_mod8(a1, a3);
       e[i + 3 * dist] = sub_mod8(a1, a3);
     }
-    __syncthreads();
+    wave_sync();
   }
 }
 
-__global__ __launch_bounds__(64) void leo8_errlocs_kernel(DecodeArgs a) {
-  __shared__ uint32_t e[256];
-  const long v = blockIdx.x;  // flattened (square, vector)
-  const long sq = v / a.nvec, vec = v % a.nvec;
-  const int k = a.k, n = 2 * k;
-  const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
-  int cnt = 0;
-  for (int i = threadIdx.x; i < 256; i += 64) {
-    uint32_t x = 0;
-    if (i < k) x = pres[(long)(k + i) * a.p_shard_stride] ? 0u : 1u;          // parity k+i -> work i
-    else if (i < n) x = pres[(long)(i - k) * a.p_shard_stride] ? 0u : 1u;     // data i-k -> work i
-    e[i] = x;
-    if (i < n) cnt += (x == 0);
-  }
-  // wave-wide count of present shards
+// One wave per vector, four vectors per workgroup; the decodable count goes
+// to the global counter once per workgroup (one atomic per vector on a single
+// address cost 0.27 ms per launch at 65,536 vectors).
+constexpr int kErrVecs = 4;
+__global__ __launch_bounds__(64 * kErrVecs) void leo8_errlocs_kernel(DecodeArgs a) {
+  __shared__ uint32_t e_all[kErrVecs][256];
+  __shared__ int blk_cnt;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (threadIdx.x == 0) blk_cnt = 0;
+  __syncthreads();
+  const long v = (long)blockIdx.x * kErrVecs + wave;  // flattened (square, vector)
+  if (v < a.nsq * a.nvec) {
+    uint32_t* e = e_all[wave];
+    const long sq = v / a.nvec, vec = v % a.nvec;
+    const int k = a.k, n = 2 * k;
+    const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
+    int cnt = 0;
+    for (int i = lane; i < 256; i += 64) {
+      uint32_t x = 0;
+      if (i < k) x = pres[(long)(k + i) * a.p_shard_stride] ? 0u : 1u;          // parity k+i -> work i
+      else if (i < n) x = pres[(long)(i - k) * a.p_shard_stride] ? 0u : 1u;     // data i-k -> work i
+      e[i] = x;
+      if (i < n) cnt += (x == 0);
+    }
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
-  __syncthreads();
-  const bool decode = cnt >= k && cnt < n;
-  if (threadIdx.x == 0) {
-    a.flags[v] = decode ? 1 : 0;
-    if (cnt < k && a.too_few) atomicOr(a.too_few, 1);
-    if (decode && a.ndecodable) atomicAdd(a.ndecodable, 1);
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);  // present shards
+    const bool decode = cnt >= k && cnt < n;
+    if (lane == 0) {
+      a.flags[v] = decode ? 1 : 0;
+      if (cnt < k && a.too_few) atomicOr(a.too_few, 1);
+      if (decode) atomicAdd(&blk_cnt, 1);
+    }
+    // uniform per wave; a vector sharing an earlier vector's erasure pattern
+    // uses that vector's locators
+    if (decode && err_vec(a, v) == v) {
+      wave_sync();
+      fwht256_wave(e, n, lane);
+      for (int i = lane; i < 256; i += 64) e[i] = (e[i] * kGf8.walsh[i]) % 255u;
+      wave_sync();
+      fwht256_wave(e, 256, lane);
+      uint8_t* out = a.err + v * 256;
+      for (int i = lane; i < n; i += 64) out[i] = (uint8_t)e[i];
+    }
   }
-  if (!decode) return;  // uniform
-  if (err_vec(a, v) != v) return;  // same erasure pattern as an earlier vector: share its locators
-  fwht256_lds(e, n);
-  for (int i = threadIdx.x; i < 256; i += 64) e[i] = (e[i] * kGf8.walsh[i]) % 255u;
   __syncthreads();
-  fwht256_lds(e, 256);
-  uint8_t* out = a.err + v * 256;
-  for (int i = threadIdx.x; i < n; i += 64) out[i] = (uint8_t)e[i];
+  if (threadIdx.x == 0 && blk_cnt && a.ndecodable) atomicAdd(a.ndecodable, blk_cnt);
 }
 
 // ---------------------------------------------------------------------------
@@ -423,7 +444,8 @@ static hipError_t launch_dec(const DecodeArgs& a, hipStream_t s) {
 hipError_t launch_leo8_errlocs(const DecodeArgs& a, hipStream_t s) {
   const long nv = a.nsq * a.nvec;
   if (nv <= 0) return hipSuccess;
-  hipLaunchKernelGGL(leo8_errlocs_kernel, dim3((unsigned)nv), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(leo8_errlocs_kernel, dim3((unsigned)((nv + kErrVecs - 1) / kErrVecs)), dim3(64 * kErrVecs), 0,
+                     s, a);
   return hipGetLastError();
 }
 
