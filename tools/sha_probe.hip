@@ -61,6 +61,46 @@ __device__ __forceinline__ uint64_t pair(uint32_t x) {
   return ((uint64_t)x << 32) | x;  // one v_mov of x into the high half
 }
 
+// slow-class (VOP3-only) forms: a ^ b = v_xad_u32(a, b, 0); (a ^ b) + c = v_xad_u32(a, b, c);
+// x >> n = v_alignbit_b32(0, x, n); a + b = v_add3_u32(a, b, 0); Ch = v_bfi_b32(e, f, g)
+__device__ __forceinline__ uint32_t xad(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_xad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ uint32_t xad0(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_xad_u32 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ uint32_t add3s(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ uint32_t add2s(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_add3_u32 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t x, uint32_t y) {
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(x), "v"(y));
+  return r;
+}
+template <int N>
+__device__ __forceinline__ uint32_t rots(uint32_t x) {
+  uint32_t r;
+  asm("v_alignbit_b32 %0, %1, %1, %2" : "=v"(r) : "v"(x), "i"(N));
+  return r;
+}
+template <int N>
+__device__ __forceinline__ uint32_t shrs(uint32_t x) {
+  uint32_t r;
+  asm("v_alignbit_b32 %0, 0, %1, %2" : "=v"(r) : "v"(x), "i"(N));
+  return r;
+}
+
 // Sigma functions in the three forms.
 template <int ROT, int A, int B, int C>
 __device__ __forceinline__ uint32_t big_sigma(uint32_t x) {
@@ -94,6 +134,45 @@ template <int ROT>
 __device__ __forceinline__ uint32_t add3x(uint32_t a, uint32_t b, uint32_t c) {
   if constexpr (ROT == 0) return a + b + c;  // v_add3
   return add2(add2(a, b), c);
+}
+
+// rot 3: slow-class ops only -- 16 per round
+__device__ __forceinline__ void round_slow(uint32_t a, uint32_t b, uint32_t c, uint32_t& d, uint32_t e,
+                                           uint32_t f, uint32_t g, uint32_t& h, uint32_t kw) {
+  const uint32_t u = xad(xad0(rots<6>(e), rots<11>(e)), rots<25>(e), h);  // h + Sigma1(e)
+  const uint32_t t1 = add3s(u, bfi(e, f, g), kw);
+  const uint32_t maj = bfi(xad0(a, b), c, a);
+  const uint32_t t2 = xad(xad0(rots<2>(a), rots<13>(a)), rots<22>(a), maj);  // Sigma0(a) + Maj
+  d = add2s(d, t1);
+  h = add2s(t1, t2);
+}
+__device__ __forceinline__ void compress_slow(uint32_t (&st)[8], uint32_t (&w)[16]) {
+  uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll 1
+  for (int it = 0; it < 64; it += 16) {
+    if (it) {
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const uint32_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+        const uint32_t s0w = xad(xad0(rots<7>(w15), rots<18>(w15)), shrs<3>(w15), w[j]);
+        const uint32_t s1w = xad(xad0(rots<17>(w2), rots<19>(w2)), shrs<10>(w2), w[(j + 9) & 15]);
+        w[j] = add2s(s0w, s1w);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 16; j += 8) {
+      round_slow(a, b, c, d, e, f, g, h, add2s(kK[it + j + 0], w[j + 0]));
+      round_slow(h, a, b, c, d, e, f, g, add2s(kK[it + j + 1], w[j + 1]));
+      round_slow(g, h, a, b, c, d, e, f, add2s(kK[it + j + 2], w[j + 2]));
+      round_slow(f, g, h, a, b, c, d, e, add2s(kK[it + j + 3], w[j + 3]));
+      round_slow(e, f, g, h, a, b, c, d, add2s(kK[it + j + 4], w[j + 4]));
+      round_slow(d, e, f, g, h, a, b, c, add2s(kK[it + j + 5], w[j + 5]));
+      round_slow(c, d, e, f, g, h, a, b, add2s(kK[it + j + 6], w[j + 6]));
+      round_slow(b, c, d, e, f, g, h, a, add2s(kK[it + j + 7], w[j + 7]));
+    }
+  }
+  st[0] = add2s(st[0], a); st[1] = add2s(st[1], b); st[2] = add2s(st[2], c); st[3] = add2s(st[3], d);
+  st[4] = add2s(st[4], e); st[5] = add2s(st[5], f); st[6] = add2s(st[6], g); st[7] = add2s(st[7], h);
 }
 
 template <int ROT>
@@ -144,8 +223,9 @@ __global__ __launch_bounds__(256) void sha_kernel(uint32_t* out, int iters, uint
   for (int it = 0; it < iters; it++) {
     uint32_t w[16];
 #pragma unroll
-    for (int i = 0; i < 16; i++) w[i] = m[i] ^ st[i & 7];
-    compress<ROT>(st, w);
+    for (int i = 0; i < 16; i++) w[i] = ROT == 3 ? xad0(m[i], st[i & 7]) : m[i] ^ st[i & 7];
+    if constexpr (ROT == 3) compress_slow(st, w);
+    else compress<ROT>(st, w);
   }
   const long t = (long)blockIdx.x * 256 + threadIdx.x;
 #pragma unroll
@@ -245,6 +325,46 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 #pragma unroll
     for (int i = 0; i < 8; i++) out[msg * 8 + i] = st[i];
   }
+}
+
+// ---- co-issue: SHA waves (rot 0 mixed or rot 3 slow-only) beside fast-only waves ----
+// 512-thread workgroup: waves 0-3 run `iters` compressions (MODE & 1: SHA on),
+// waves 4-7 run `fiters` x 64 dependent-chain v_bitop3 over 16 chains (MODE & 2: fast on).
+template <int ROT, int MODE>
+__global__ __launch_bounds__(512) void coissue_kernel(uint32_t* out, int iters, int fiters, uint32_t seed) {
+  const int wave = threadIdx.x >> 6;
+  uint32_t acc = 0;
+  if (wave < 4) {
+    if (MODE & 1) {
+      uint32_t st[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                        0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+      uint32_t m[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) m[i] = seed + threadIdx.x * 16 + i + blockIdx.x;
+      for (int it = 0; it < iters; it++) {
+        uint32_t w[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) w[i] = ROT == 3 ? xad0(m[i], st[i & 7]) : m[i] ^ st[i & 7];
+        if constexpr (ROT == 3) compress_slow(st, w);
+        else compress<ROT>(st, w);
+      }
+      acc = st[0] ^ st[5];
+    }
+  } else if (MODE & 2) {
+    uint32_t v[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) v[i] = seed ^ (threadIdx.x * 16 + i);
+    for (int it = 0; it < fiters; it++) {
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+          asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(v[i]) : "v"(v[(i + 3) & 15]), "v"(v[(i + 7) & 15]));
+    }
+#pragma unroll
+    for (int i = 0; i < 16; i++) acc ^= v[i];
+  }
+  if (acc == 0x12345678u) out[blockIdx.x] = acc;
 }
 
 // ---- single-opcode rates ----
@@ -369,6 +489,11 @@ static void launch_sha(uint32_t* out, int iters) {
 static void launch_sha_capped(uint32_t* out, int iters) {  // 48 KB LDS per 256-thread WG: 3 WGs/CU
   hipLaunchKernelGGL(sha_kernel<0>, dim3(g_blocks), dim3(256), 48 * 1024, 0, out, iters, 1u);
 }
+static int g_fiters = 200;
+template <int ROT, int MODE>
+static void launch_co(uint32_t* out, int iters) {
+  hipLaunchKernelGGL((coissue_kernel<ROT, MODE>), dim3(g_blocks / 2), dim3(512), 0, 0, out, iters, g_fiters, 1u);
+}
 template <bool F>
 static void launch_split(uint32_t* out, int iters) {
   hipLaunchKernelGGL(sha_split_kernel<F>, dim3(g_blocks), dim3(512), 0, 0, out, iters, 1u);
@@ -419,15 +544,34 @@ int main() {
     printf("{\"probe\":\"cross_wave_mix\",\"all_slow_ms\":%.3f,\"all_fast_ms\":%.3f,\"half_half_ms\":%.3f,"
            "\"additive_prediction_ms\":%.3f}\n", m0, m1, m2, 0.5 * (m0 + m1));
   }
+  {
+    const int it = 40;
+    for (int fi : {100, 200, 400}) {
+      g_fiters = fi;
+      const float f = time_ms(launch_co<0, 2>, out, it);
+      const float s0 = time_ms(launch_co<0, 1>, out, it), b0 = time_ms(launch_co<0, 3>, out, it);
+      const float s3 = time_ms(launch_co<3, 1>, out, it), b3 = time_ms(launch_co<3, 3>, out, it);
+      printf("{\"coissue\":true,\"fast_iters\":%d,\"fast_alone_ms\":%.3f,\"sha_mixed_alone_ms\":%.3f,"
+             "\"sha_mixed_with_fast_ms\":%.3f,\"sha_slowonly_alone_ms\":%.3f,\"sha_slowonly_with_fast_ms\":%.3f}\n",
+             fi, f, s0, b0, s3, b3);
+    }
+  }
   const int iters = 100;
   const double comp = (double)g_blocks * 256 * iters;
-  float ms[3];
+  float ms[4];
   ms[0] = time_ms(launch_sha<0>, out, iters);
   (void)hipMemcpy(h0.data(), out, h0.size() * 4, hipMemcpyDeviceToHost);
   ms[1] = time_ms(launch_sha<1>, out, iters);
   (void)hipMemcpy(h1.data(), out, h1.size() * 4, hipMemcpyDeviceToHost);
   ms[2] = time_ms(launch_sha<2>, out, iters);
   (void)hipMemcpy(h2.data(), out, h2.size() * 4, hipMemcpyDeviceToHost);
+  ms[3] = time_ms(launch_sha<3>, out, iters);
+  {
+    std::vector<uint32_t> h3(h0.size());
+    (void)hipMemcpy(h3.data(), out, h3.size() * 4, hipMemcpyDeviceToHost);
+    printf("{\"sha_rot\":3,\"ms\":%.3f,\"gcompr_per_s\":%.2f,\"same_digests\":%s}\n", ms[3], comp / ms[3] / 1e6,
+           h3 == h0 ? "true" : "false");
+  }
   bool same = h0 == h1 && h0 == h2;
   {
     const float mss = time_ms(launch_sha_capped, out, iters);
