@@ -300,12 +300,21 @@ constexpr bool skew_split_ok() {
 }
 static_assert(skew_split_ok(), "FFT skews must be GF(2)-linear in the block offset");
 
-// x ^= C * (y & mask): the lane-bit part of a layout-A skew
+// t = C * y from scratch (no accumulator): the first set bit of a row is the
+// plane itself, the rest are consumed two at a time by xor3.
+template <int R>
+__host__ __device__ __forceinline__ uint32_t row_sum(const uint32_t (&y)[8]) {
+  constexpr int J = __builtin_ctz(R);
+  return xor_row<R & ~((2 << J) - 1), J + 1>(y[J], y);
+}
+// x ^= (C * y) & mask: the lane-bit part of a layout-A skew.  One and-xor per
+// output plane on top of the row sums (cheaper than masking the 8 inputs).
 template <int C>
-__host__ __device__ __forceinline__ void muladd_ct_masked(uint32_t (&x)[8], const uint32_t (&y)[8], uint32_t mask) {
-  uint32_t ym[8];
-  static_for<8>([&](auto p) { ym[p] = y[p] & mask; });
-  muladd_ct<C>(x, ym);
+__host__ __device__ __forceinline__ void muladd_ct_lane(uint32_t (&x)[8], const uint32_t (&y)[8], uint32_t mask) {
+  static_for<8>([&](auto i) {
+    constexpr int R = kMat.row[C][i];
+    if constexpr (R != 0) x[i] = SL_BOP3(x[i], row_sum<R>(y), mask, kXorAnd);
+  });
 }
 
 // IFFT layers 0..2 in the two-vector layout A (K = 128), wave w, lane mask of eb.
@@ -333,7 +342,7 @@ __host__ __device__ __forceinline__ void ifft_A2(uint32_t (&v)[16][8], int w, ui
       });
     }
     static_for<16>([&](auto j) {
-      if constexpr (!(j & D)) muladd_ct_masked<skew_elem(D - 1 + 16)>(v[j], v[j + D], ebmask);
+      if constexpr (!(j & D)) muladd_ct_lane<skew_elem(D - 1 + 16)>(v[j], v[j + D], ebmask);
     });
   });
 }
@@ -360,7 +369,7 @@ __host__ __device__ __forceinline__ void fft_A2(uint32_t (&v)[16][8], int w, uin
       });
     }
     static_for<16>([&](auto j) {
-      if constexpr (!(j & D)) muladd_ct_masked<skew_elem(D - 1 + 16)>(v[j], v[j + D], ebmask);
+      if constexpr (!(j & D)) muladd_ct_lane<skew_elem(D - 1 + 16)>(v[j], v[j + D], ebmask);
     });
     static_for<16>([&](auto j) {
       if constexpr (!(j & D)) xor8(v[j + D], v[j]);
@@ -370,39 +379,25 @@ __host__ __device__ __forceinline__ void fft_A2(uint32_t (&v)[16][8], int w, uin
 
 
 // ---------------------------------------------------------------------------
-// Bit-sliced decode for k = 128 (rs_decode.hip leo8_decode128_sliced_kernel):
+// Bit-sliced decode for k = 128 (rs_decode_sliced.hip leo8_decode128_sliced_kernel):
 // leopard8.go reconstruct's IFFT_256 and FFT_256 (decoder skew index b + D - 1,
 // no +k offset) on n = 256 work elements, one vector per 4-wave workgroup.
 // Lane l = t + 16 eb: t = 32-byte column block, eb = TWO element bits; wave w.
-//   A: e = j + 16 eb + 64 w   (j = register)  -- layers 0..3
-//   B: e = eb + 4 w + 16 i    (i = register)  -- layers 4..7, skews compile-time
+//   A:  e = j + 16 eb + 64 w  (j = register)  -- layers 0..1
+//   A*: e = eb + 4 r + 64 w   (r = register)  -- layers 2..3 (wave-local transpose of A)
+//   B:  e = eb + 4 w + 16 i   (i = register)  -- layers 4..7, skews compile-time
 // In A the skew of layer m splits (skew_split_ok, bits up to 7) into
-//   C(j) ^ eb0 S16 ^ eb1 S32 ^ w0 S64 ^ w1 S128,  S_x = skew(2^m - 1 + x).
+//   C(j) ^ eb0 S16 ^ eb1 S32 ^ w0 S64 ^ w1 S128,  S_x = skew(2^m - 1 + x);
+// in A* the lane bits are element bits 0..1, below the pair bit, so only the
+// wave terms remain.
 // ---------------------------------------------------------------------------
 
-// t = C * y from scratch (no accumulator): the first set bit of a row is the
-// plane itself, the rest are consumed two at a time by xor3.
-template <int R>
-__host__ __device__ __forceinline__ uint32_t row_sum(const uint32_t (&y)[8]) {
-  constexpr int J = __builtin_ctz(R);
-  return xor_row<R & ~((2 << J) - 1), J + 1>(y[J], y);
-}
-// x ^= (C * y) & mask: the lane-bit part of a layout-A skew.  One and-xor per
-// output plane on top of the row sums (cheaper than masking the 8 inputs).
-template <int C>
-__host__ __device__ __forceinline__ void muladd_ct_lane(uint32_t (&x)[8], const uint32_t (&y)[8], uint32_t mask) {
-  static_for<8>([&](auto i) {
-    constexpr int R = kMat.row[C][i];
-    if constexpr (R != 0) x[i] = SL_BOP3(x[i], row_sum<R>(y), mask, kXorAnd);
-  });
-}
-
-// Decoder layers 0..3 in layout A (IFFT ascending, FFT descending).
+// Decoder layers 0..NL-1 in layout A (IFFT ascending, FFT descending).
 // IFFT butterfly (ifftDIT8): y ^= x; x ^= skew * y.  FFT (fftDIT8): x ^= skew * y; y ^= x.
-template <bool IFFT>
+template <bool IFFT, int NL>
 __host__ __device__ __forceinline__ void dec_A(uint32_t (&v)[16][8], int w, uint32_t eb0mask, uint32_t eb1mask) {
-  static_for<4>([&](auto mm) {
-    constexpr int m = IFFT ? (int)mm : 3 - (int)mm;
+  static_for<NL>([&](auto mm) {
+    constexpr int m = IFFT ? (int)mm : NL - 1 - (int)mm;
     constexpr int D = 1 << m;
     SL_FENCE();
     if constexpr (IFFT) {
@@ -432,6 +427,40 @@ __host__ __device__ __forceinline__ void dec_A(uint32_t (&v)[16][8], int w, uint
     if constexpr (!IFFT) {
       static_for<16>([&](auto j) {
         if constexpr (!(j & D)) xor8(v[j + D], v[j]);
+      });
+    }
+  });
+}
+
+// Decoder layers 2..3 in layout A*: register bit (m - 2) of r is element bit m,
+// block start b = 4 (r with register bits <= m - 2 cleared) + 64 w.
+template <bool IFFT>
+__host__ __device__ __forceinline__ void dec_Astar(uint32_t (&v)[16][8], int w) {
+  static_for<2>([&](auto mm) {
+    constexpr int rb = IFFT ? (int)mm : 1 - (int)mm;
+    constexpr int D = 4 << rb, R = 1 << rb;
+    SL_FENCE();
+    if constexpr (IFFT) {
+      static_for<16>([&](auto r) {
+        if constexpr (!(r & R)) xor8(v[r + R], v[r]);
+      });
+    }
+    static_for<16>([&](auto r) {
+      if constexpr (!(r & R)) muladd_ct<skew_elem(D - 1 + 4 * (r & ~(2 * R - 1)))>(v[r], v[r + R]);
+    });
+    if (w & 1) {
+      static_for<16>([&](auto r) {
+        if constexpr (!(r & R)) muladd_ct<skew_elem(D - 1 + 64)>(v[r], v[r + R]);
+      });
+    }
+    if (w & 2) {
+      static_for<16>([&](auto r) {
+        if constexpr (!(r & R)) muladd_ct<skew_elem(D - 1 + 128)>(v[r], v[r + R]);
+      });
+    }
+    if constexpr (!IFFT) {
+      static_for<16>([&](auto r) {
+        if constexpr (!(r & R)) xor8(v[r + R], v[r]);
       });
     }
   });

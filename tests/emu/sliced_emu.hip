@@ -169,7 +169,22 @@ void fwht256(uint32_t* e, int mtrunc) {
 }
 
 int elemA(int r, int eb, int w) { return r + 16 * eb + 64 * w; }
+int elemS(int r, int eb, int w) { return eb + 4 * r + 64 * w; }  // A*
 int elemB(int r, int eb, int w) { return eb + 4 * w + 16 * r; }
+
+// wave-local A <-> A* (the kernel's dec_transpose_wave): per wave, element
+// e = j + 16 eb moves to lane group e & 3, register e >> 2
+void a_to_s(uint32_t (&st)[4][4][16][8], bool forward) {
+  static uint32_t tmp[4][4][16][8];
+  for (int w = 0; w < 4; w++)
+    for (int eb = 0; eb < 4; eb++)
+      for (int r = 0; r < 16; r++) {
+        const int e = forward ? elemS(r, eb, 0) : elemA(r, eb, 0);  // destination element
+        const int src_eb = forward ? (e >> 4) : (e & 3), src_r = forward ? (e & 15) : (e >> 2);
+        memcpy(tmp[w][eb][r], st[w][src_eb][src_r], 32);
+      }
+  memcpy(st, tmp, sizeof(tmp));
+}
 
 }  // namespace
 
@@ -202,12 +217,15 @@ extern "C" int sliced_dec_emu(long shard, uint8_t* shards, const uint8_t* presen
           }
       for (int w = 0; w < 4; w++)
         for (int eb = 0; eb < 4; eb++)
-          dec_A<true>(st[w][eb], w, (eb & 1) ? 0xFFFFFFFFu : 0u, (eb & 2) ? 0xFFFFFFFFu : 0u);
-      for (int w = 0; w < 4; w++)  // A -> B
+          dec_A<true, 2>(st[w][eb], w, (eb & 1) ? 0xFFFFFFFFu : 0u, (eb & 2) ? 0xFFFFFFFFu : 0u);
+      a_to_s(st, true);
+      for (int w = 0; w < 4; w++)
+        for (int eb = 0; eb < 4; eb++) dec_Astar<true>(st[w][eb], w);
+      for (int w = 0; w < 4; w++)  // A* -> B
         for (int eb = 0; eb < 4; eb++)
           for (int i = 0; i < 16; i++) {
-            const int e = elemB(i, eb, w);
-            memcpy(tmp[w][eb][i], st[e >> 6][(e >> 4) & 3][e & 15], 32);
+            const int e = elemB(i, eb, w);  // held in A* by wave e >> 6, lane group e & 3, register (e >> 2) & 15
+            memcpy(tmp[w][eb][i], st[e >> 6][e & 3][(e >> 2) & 15], 32);
           }
       for (int w = 0; w < 4; w++)
         for (int eb = 0; eb < 4; eb++) dec_B<true>(tmp[w][eb]);
@@ -226,15 +244,18 @@ extern "C" int sliced_dec_emu(long shard, uint8_t* shards, const uint8_t* presen
         }
       for (int w = 0; w < 4; w++)
         for (int eb = 0; eb < 4; eb++) dec_B<false>(tmp[w][eb]);
-      for (int w = 0; w < 4; w++)  // B -> A
+      for (int w = 0; w < 4; w++)  // B -> A*
         for (int eb = 0; eb < 4; eb++)
           for (int i = 0; i < 16; i++) {
             const int e = elemB(i, eb, w);
-            memcpy(st[e >> 6][(e >> 4) & 3][e & 15], tmp[w][eb][i], 32);
+            memcpy(st[e >> 6][e & 3][(e >> 2) & 15], tmp[w][eb][i], 32);
           }
       for (int w = 0; w < 4; w++)
+        for (int eb = 0; eb < 4; eb++) dec_Astar<false>(st[w][eb], w);
+      a_to_s(st, false);
+      for (int w = 0; w < 4; w++)
         for (int eb = 0; eb < 4; eb++)
-          dec_A<false>(st[w][eb], w, (eb & 1) ? 0xFFFFFFFFu : 0u, (eb & 2) ? 0xFFFFFFFFu : 0u);
+          dec_A<false, 2>(st[w][eb], w, (eb & 1) ? 0xFFFFFFFFu : 0u, (eb & 2) ? 0xFFFFFFFFu : 0u);
       for (int w = 0; w < 4; w++)
         for (int eb = 0; eb < 4; eb++)
           for (int j = 0; j < 16; j++) {
