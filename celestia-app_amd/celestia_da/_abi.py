@@ -9,7 +9,8 @@ import ctypes
 import os
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG_ROOT, "libdagpu.so")
+# DAGPU_LIB selects another build of the same library (A/B runs of kernel variants)
+LIB_PATH = os.environ.get("DAGPU_LIB") or os.path.join(_PKG_ROOT, "libdagpu.so")
 
 SHARE_SIZE = 512
 NAMESPACE_SIZE = 29
