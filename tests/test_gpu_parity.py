@@ -285,6 +285,24 @@ def test_codec_decode_matches_oracle(ctx, k, shard):
         assert b"".join(out) == full.tobytes()
 
 
+@pytest.mark.parametrize("pattern", ["data_half", "parity_half", "alternate", "first_k_plus_1"])
+def test_codec_decode_k128_structured(ctx, pattern):
+    """The bit-sliced k = 128 decoder (rs_decode_sliced.hip, whole 512-B chunks;
+    4 chunks here) on structured erasures: every data shard lost, every parity
+    shard lost, every other shard lost, and k + 1 present at the front."""
+    k, shard = 128, 2048
+    rng = np.random.default_rng(31 * len(pattern))
+    codec = da.LeoRSCodec(ctx)
+    data = rng.integers(0, 256, (k, shard), dtype=np.uint8)
+    full = np.concatenate([data, oracle.encode(data)])
+    idx = np.arange(2 * k)
+    keep = {"data_half": idx >= k, "parity_half": idx < k, "alternate": idx % 2 == 0,
+            "first_k_plus_1": idx <= k}[pattern]
+    shards = [full[i].tobytes() if keep[i] else None for i in range(2 * k)]
+    out = codec.decode(shards)
+    assert b"".join(out) == full.tobytes()
+
+
 def test_codec_decode_too_few(ctx):
     k = 8
     codec = da.LeoRSCodec(ctx)
