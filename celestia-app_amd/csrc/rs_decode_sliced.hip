@@ -165,11 +165,8 @@ void leo8_decode128_sliced_kernel(DecodeArgs a) {
     const bool p = pres[(long)shard * a.p_shard_stride] != 0;
     miss |= (uint32_t)!p << j;
     const uint32_t soff = (uint32_t)(shard0 + j) * sstride;
-    u32x4 lo = {0u, 0u, 0u, 0u}, hi = {0u, 0u, 0u, 0u};
-    if (p) {  // missing shards are not read (half the bytes at maximal erasure)
-      lo = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, soff, 0);
-      hi = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 256u, soff, 0);
-    }
+    const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, soff, 0);
+    const u32x4 hi = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 256u, soff, 0);
     v_[j][0] = lo.x; v_[j][1] = lo.y; v_[j][2] = lo.z; v_[j][3] = lo.w;
     v_[j][4] = hi.x; v_[j][5] = hi.y; v_[j][6] = hi.z; v_[j][7] = hi.w;
   }
