@@ -2,7 +2,8 @@
 RS of every group on stream R and the NMT/DAH work of group i on stream H
 after RS(i) (so RS(i+1..) can run beside the hashing of group i).  ODS in
 place (Q0 of the EDS buffer).  Prints ms per 256 squares for each S and stream
-priority setting, and checks the DAHs against the unsliced run."""
+priority setting (argument nmt_hi: the hashing stream at high priority
+instead), and checks the DAHs against the unsliced run."""
 import os
 import sys
 import time
@@ -26,13 +27,13 @@ del ref
 torch.cuda.empty_cache()
 
 
-def run(S, prio):
+def run(S, prio, nmt_hi=False):
     groups = [DeviceSquares(k, B // S, ctx=ctx, in_place=True) for _ in range(S)]
     for i, g in enumerate(groups):
         g.load_ods(host[i * (B // S):(i + 1) * (B // S)])
     lo, hi = torch.cuda.Stream.priority_range()
     sr = torch.cuda.Stream(priority=hi if prio else 0)
-    sh = torch.cuda.Stream(priority=0)
+    sh = torch.cuda.Stream(priority=hi if nmt_hi else 0)
     evs = [torch.cuda.Event() for _ in range(S)]
     torch.cuda.synchronize()
 
@@ -60,11 +61,17 @@ def run(S, prio):
     ms = (time.perf_counter() - t0) / n * 1e3
     got = torch.cat([g.dah.cpu() for g in groups])
     ok = bool(torch.equal(got, want))
-    print(f"S={S} prio={int(prio)}: {ms:.3f} ms/256 squares  {B / ms * 1e3:.0f} squares/s  dah_ok={ok}", flush=True)
+    print(f"S={S} prio={int(prio)} nmt_hi={int(nmt_hi)}: {ms:.3f} ms/256 squares  {B / ms * 1e3:.0f} squares/s  dah_ok={ok}", flush=True)
     del groups
     torch.cuda.empty_cache()
 
 
+modes = sys.argv[1:] or ["all"]
 for S in (1, 2, 4, 8):
+    if "nmt_hi" in modes:
+        if S > 1:
+            run(S, False)
+            run(S, False, nmt_hi=True)
+        continue
     for prio in ((False, True) if S > 1 else (False,)):
         run(S, prio)
