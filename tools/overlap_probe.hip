@@ -13,7 +13,8 @@
 //      group, writes 64 KB.
 // Prints ms alone and concurrent (two non-blocking streams).
 // argv: <sha LDS KB> <rs variant> [sha WG size] [sha persistent WGs per CU] [work queue 0/1] [variant 5: rs WGs per CU]
-// rs variant 5 = rs2 as a persistent grid taking groups from a counter
+// rs variant 5 = rs2 as a persistent grid taking groups from a counter; 6 = rs6 (8-wave, 2 vectors,
+// ~90 VGPRs), 7 = rs6 as a persistent grid
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++20 tools/overlap_probe.hip -o tools/overlap_probe
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -297,6 +298,68 @@ __global__ __launch_bounds__(256) void rs5_kernel(const u32x4* __restrict__ in, 
   for (int j = 0; j < 16; j++) dst[j * 256 + threadIdx.x] = (u32x4){x[4 * j], x[4 * j + 1], x[4 * j + 2], x[4 * j + 3]};
 }
 
+
+// rs6: the low-VGPR shape -- an 8-wave workgroup holds 2 vectors (128 KB):
+// 64 data dwords per lane (~90 VGPRs, 4 waves/SIMD), one 64-KB LDS exchange in
+// two halves; OPS x 64 bitop3 per lane (OPS = 55: the real encoder's VALU work
+// per byte spread over twice the waves).
+template <int OPS>
+__device__ __forceinline__ void rs6_body(const u32x4* __restrict__ in, u32x4* __restrict__ out, long g, u32x4* lds) {
+  const u32x4* src = in + g * 8192;  // 128 KB per group
+  u32x4* dst = out + g * 8192;
+  uint32_t x[64];
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    const u32x4 d = src[j * 512 + threadIdx.x];
+    x[4 * j] = d.x; x[4 * j + 1] = d.y; x[4 * j + 2] = d.z; x[4 * j + 3] = d.w;
+  }
+#pragma unroll 1
+  for (int r = 0; r < OPS; r++) {
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+      const uint32_t a = x[(j + 1) & 63], b = x[(j + 7) & 63];
+      asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(x[j]) : "v"(a), "v"(b));
+    }
+    if (r == OPS / 2) {
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+          lds[j * 512 + threadIdx.x] = (u32x4){x[32 * h + 4 * j], x[32 * h + 4 * j + 1], x[32 * h + 4 * j + 2], x[32 * h + 4 * j + 3]};
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          const u32x4 q = lds[j * 512 + (threadIdx.x ^ 64)];
+          x[32 * h + 4 * j] = q.x; x[32 * h + 4 * j + 1] = q.y; x[32 * h + 4 * j + 2] = q.z; x[32 * h + 4 * j + 3] = q.w;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 16; j++) dst[j * 512 + threadIdx.x] = (u32x4){x[4 * j], x[4 * j + 1], x[4 * j + 2], x[4 * j + 3]};
+}
+template <int OPS>
+__global__ __launch_bounds__(512) void rs6_kernel(const u32x4* __restrict__ in, u32x4* __restrict__ out, long ngrp) {
+  __shared__ u32x4 lds[4096];  // 64 KB
+  if ((long)blockIdx.x >= ngrp) return;
+  rs6_body<OPS>(in, out, blockIdx.x, lds);
+}
+template <int OPS>
+__global__ __launch_bounds__(512) void rs6_queue_kernel(const u32x4* __restrict__ in, u32x4* __restrict__ out, long ngrp,
+                                                        unsigned long long* counter) {
+  __shared__ u32x4 lds[4096];
+  __shared__ long g_s;
+  for (;;) {
+    __syncthreads();
+    if (threadIdx.x == 0) g_s = (long)atomicAdd(counter, 1ull);
+    __syncthreads();
+    const long g = g_s;
+    if (g >= ngrp) return;
+    rs6_body<OPS>(in, out, g, lds);
+  }
+}
+
 int main(int argc, char** argv) {
   const long ncell = 256L * 65536;  // leaves per 256-square step
   const long nvec = 256L * 384;  // RS vectors per step (k = 128, 64 KB each)
@@ -341,6 +404,11 @@ int main(int argc, char** argv) {
     else if (variant == 1) hipLaunchKernelGGL(rs2_kernel<55>, dim3((unsigned)(nvec / 2)), dim3(256), 0, s, rin, rout, nvec / 2);
     else if (variant == 2) hipLaunchKernelGGL(rs3_kernel<52>, dim3((unsigned)nvec), dim3(256), 0, s, rin, rout, nvec);
     else if (variant == 3) hipLaunchKernelGGL(rs4_kernel<55>, dim3((unsigned)(nvec / 2)), dim3(256), 0, s, rin, rout, nvec / 2);
+    else if (variant == 6) hipLaunchKernelGGL(rs6_kernel<55>, dim3((unsigned)(nvec / 2)), dim3(512), 0, s, rin, rout, nvec / 2);
+    else if (variant == 7) {
+      (void)hipMemsetAsync(rcounter, 0, 8, s);
+      hipLaunchKernelGGL(rs6_queue_kernel<55>, dim3((unsigned)(256 * rs_wgs)), dim3(512), 0, s, rin, rout, nvec / 2, rcounter);
+    }
     else if (variant == 5) {
       (void)hipMemsetAsync(rcounter, 0, 8, s);
       hipLaunchKernelGGL(rs2_queue_kernel<55>, dim3((unsigned)(256 * rs_wgs)), dim3(256), 0, s, rin, rout, nvec / 2, rcounter);
