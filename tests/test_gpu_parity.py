@@ -389,6 +389,28 @@ def test_repair_byzantine_and_errors(ctx):
     assert (fixed == eds).all()
 
 
+def test_repair_k128_byzantine_and_unrepairable(ctx):
+    """The error classes through the bit-sliced k = 128 decoder: a corrupted
+    present share under the maximal erasure pattern makes the rebuilt axes
+    miss their roots (ErrByzantineData); one row and one column fewer leaves
+    nothing decodable (ErrUnrepairableDataSquare)."""
+    k = 128
+    w = 2 * k
+    ods = synth.random_blob_square(k, 4242)
+    eds, rr, cr, _ = oracle.extend_and_dah(ods, k, nthreads=8)
+    present = _subgrid(k, 77)
+    r, c = np.argwhere(present)[5]
+    bad = eds * present[:, :, None]
+    bad[r, c, 311] ^= 0x08
+    with pytest.raises(da.ErrByzantineData):
+        da.repair(bad, present, rr, cr, ctx)
+    few = present.copy()
+    few[r, :] = False
+    few[:, c] = False
+    with pytest.raises(da.ErrUnrepairableDataSquare):
+        da.repair(eds * few[:, :, None], few, rr, cr, ctx)
+
+
 def test_repair_device_batch(ctx):
     """C4 on the device-resident batch API: 8 squares at k=128."""
     import torch
