@@ -641,8 +641,9 @@ int dagpu_decode(dagpu_ctx* ctx, uint32_t k, size_t nvec, size_t shard_size, uin
   da.p_shard_stride = 1;
   da.err = (uint8_t*)ctx->ws.p;
   da.flags = (int32_t*)((uint8_t*)ctx->ws.p + errb);
-  da.err_same = da.flags + nvec;
-  da.err_head = da.flags + 2 * nvec;
+  // locator sharing runs one workgroup over all vectors of a "square" (<= 1024)
+  da.err_same = nvec <= 1024 ? da.flags + nvec : nullptr;
+  da.err_head = nvec <= 1024 ? da.flags + 2 * nvec : nullptr;
   da.too_few = (int32_t*)ctx->status.p;
   da.nsq = 1;
   da.nvec = (long)nvec;

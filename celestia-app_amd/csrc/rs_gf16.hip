@@ -1146,35 +1146,34 @@ hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mar
   return e;
 }
 
-// Error-locator sharing (DecodeArgs.err_same / err_head): a wave per vector
-// compares its 2k presence flags with vector v - 1's; then a scan per square
-// finds the head of each run of equal patterns.
-__global__ __launch_bounds__(64) void errloc_same_kernel(DecodeArgs a) {
-  const long v = blockIdx.x;
-  if (v == 0) {
-    if (threadIdx.x == 0) a.err_same[0] = 0;
-    return;
-  }
-  const long u = v - 1;
-  const uint8_t* pv = a.present + (v / a.nvec) * a.p_sq_stride + (v % a.nvec) * a.p_vec_stride;
-  const uint8_t* pu = a.present + (u / a.nvec) * a.p_sq_stride + (u % a.nvec) * a.p_vec_stride;
-  bool diff = false;
-  for (int i = threadIdx.x; i < 2 * a.k; i += 64)
-    diff |= (pv[(long)i * a.p_shard_stride] != 0) != (pu[(long)i * a.p_shard_stride] != 0);
-  const bool any = __builtin_amdgcn_ballot_w64(diff) != 0;
-  if (threadIdx.x == 0) a.err_same[v] = any ? 0 : 1;
-}
-
-// head[v] = last u <= v of v's square whose pattern differs from u - 1 (a
-// run never crosses a square): prefix max of (same ? -1 : index) per square,
-// one workgroup per square, Hillis-Steele in LDS (nvec <= 1024).
-__global__ __launch_bounds__(1024) void errloc_head_kernel(DecodeArgs a) {
+// Error-locator sharing.  err_same[v] = vector v's erasure pattern (its 2k
+// presence flags) equals vector v - 1's; err_head[v] = the last u <= v of v's
+// square whose pattern differs from u - 1's (a run never crosses a square),
+// whose locators v then uses.  One workgroup per square: its 16 waves compare
+// neighbouring vectors (64 lanes over the 2k flags, one ballot per vector),
+// then a prefix max of (same ? -1 : index) in LDS (Hillis-Steele, nvec <= 1024).
+// One launch per axis instead of one workgroup per vector plus a scan launch.
+__global__ __launch_bounds__(1024) void errloc_runs_kernel(DecodeArgs a) {
   __shared__ int32_t h[1024];
   const long sq = blockIdx.x;
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int nvec = (int)a.nvec;
   const long v0 = sq * a.nvec;
-  if (t < nvec) h[t] = (t == 0 || !a.err_same[v0 + t]) ? t : -1;
+  const uint8_t* base = a.present + sq * a.p_sq_stride;
+  for (int v = wave; v < nvec; v += 16) {
+    bool diff = v == 0;  // the first vector of a square starts a run
+    if (v > 0) {
+      const uint8_t* pv = base + (long)v * a.p_vec_stride;
+      const uint8_t* pu = pv - a.p_vec_stride;
+      for (int i = lane; i < 2 * a.k; i += 64)
+        diff |= (pv[(long)i * a.p_shard_stride] != 0) != (pu[(long)i * a.p_shard_stride] != 0);
+    }
+    const bool any = __builtin_amdgcn_ballot_w64(diff) != 0;
+    if (lane == 0) {
+      a.err_same[v0 + v] = any ? 0 : 1;
+      h[v] = any ? v : -1;
+    }
+  }
   __syncthreads();
   for (int off = 1; off < nvec; off <<= 1) {
     const int x = (t < nvec && t >= off) ? h[t - off] : -1;
@@ -1187,13 +1186,9 @@ __global__ __launch_bounds__(1024) void errloc_head_kernel(DecodeArgs a) {
 
 hipError_t launch_errloc_heads(const DecodeArgs& a, hipStream_t s) {
   if (!a.err_same || !a.err_head) return hipSuccess;
-  const long nv = a.nsq * a.nvec;
-  if (nv <= 0) return hipSuccess;
-  hipLaunchKernelGGL(errloc_same_kernel, dim3((unsigned)nv), dim3(64), 0, s, a);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  if (a.nsq * a.nvec <= 0) return hipSuccess;
   if (a.nvec > 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(errloc_head_kernel, dim3((unsigned)a.nsq), dim3(1024), 0, s, a);
+  hipLaunchKernelGGL(errloc_runs_kernel, dim3((unsigned)a.nsq), dim3(1024), 0, s, a);
   return hipGetLastError();
 }
 

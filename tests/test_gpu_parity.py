@@ -303,6 +303,28 @@ def test_codec_decode_k128_structured(ctx, pattern):
     assert b"".join(out) == full.tobytes()
 
 
+@pytest.mark.parametrize("nvec,k,shard", [(300, 16, 512), (1100, 4, 64), (24, 128, 512)])
+def test_codec_decode_batch_shared_patterns(ctx, nvec, k, shard):
+    """dagpu_decode over many vectors in one call: runs of equal erasure
+    patterns share their error locators (one workgroup scans <= 1024 vectors;
+    larger batches decode without sharing), mixed with distinct patterns."""
+    from celestia_da import _abi
+    rng = np.random.default_rng(nvec + k)
+    data = rng.integers(0, 256, (nvec, k, shard), dtype=np.uint8)
+    full = np.stack([np.concatenate([d, oracle.encode(d)]) for d in data])
+    present = np.zeros((nvec, 2 * k), np.uint8)
+    v = 0
+    while v < nvec:
+        run = int(rng.integers(1, 6))
+        pat = np.zeros(2 * k, np.uint8)
+        pat[rng.choice(2 * k, k + int(rng.integers(0, k + 1)) if k > 1 else 1, replace=False)] = 1
+        present[v:v + run] = pat
+        v += run
+    buf = (full * present[:, :, None]).copy()
+    ctx.check(ctx._L.dagpu_decode(ctx.handle, k, nvec, shard, _abi.addr(buf), _abi.addr(present)))
+    assert np.array_equal(buf, full)
+
+
 def test_codec_decode_too_few(ctx):
     k = 8
     codec = da.LeoRSCodec(ctx)
