@@ -15,6 +15,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <vector>
+#include <stdlib.h>
 
 static __constant__ const uint32_t kK[64] = {
     0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
@@ -507,6 +508,43 @@ static void launch_mix(uint32_t* out, int iters) {
   hipLaunchKernelGGL(mix_kernel<MODE>, dim3(g_blocks / 2), dim3(512), 0, 0, out, iters, 1u);
 }
 
+
+// ---- mixed formulations: workgroups alternate between two SHA formulations so
+// that every SIMD holds waves of both (slow-class rot 0/3 beside fast-class rot 1).
+// Workgroup b uses RB when (b & 3) < NB, else RA.
+template <int RA, int RB, int NB>
+__global__ __launch_bounds__(256) void sha_mix_kernel(uint32_t* out, int iters, uint32_t seed) {
+  uint32_t st[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                    0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+  uint32_t m[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) m[i] = seed + threadIdx.x * 16 + i + blockIdx.x;
+  if ((int)(blockIdx.x & 3) < NB) {
+    for (int it = 0; it < iters; it++) {
+      uint32_t w[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) w[i] = RB == 3 ? xad0(m[i], st[i & 7]) : m[i] ^ st[i & 7];
+      if constexpr (RB == 3) compress_slow(st, w);
+      else compress<RB>(st, w);
+    }
+  } else {
+    for (int it = 0; it < iters; it++) {
+      uint32_t w[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) w[i] = RA == 3 ? xad0(m[i], st[i & 7]) : m[i] ^ st[i & 7];
+      if constexpr (RA == 3) compress_slow(st, w);
+      else compress<RA>(st, w);
+    }
+  }
+  const long t = (long)blockIdx.x * 256 + threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 8; i++) out[t * 8 + i] = st[i];
+}
+template <int RA, int RB, int NB>
+static void launch_shamix(uint32_t* out, int iters) {
+  hipLaunchKernelGGL((sha_mix_kernel<RA, RB, NB>), dim3(g_blocks), dim3(256), 0, 0, out, iters, 1u);
+}
+
 int main() {
   hipDeviceProp_t p;
   (void)hipGetDeviceProperties(&p, 0);
@@ -516,6 +554,26 @@ int main() {
   (void)hipMalloc(&out, (size_t)g_blocks * 256 * 8 * 4);
   std::vector<uint32_t> h0((size_t)g_blocks * 256 * 8), h1(h0.size()), h2(h0.size());
   const double clk = 2.4e9;
+  if (getenv("SHA_MIX_ONLY")) {
+    const int iters = 100;
+    const double comp = (double)g_blocks * 256 * iters;
+    auto line = [&](const char* name, void (*fn)(uint32_t*, int)) {
+      const float ms = time_ms(fn, out, iters);
+      (void)hipMemcpy(h1.data(), out, h1.size() * 4, hipMemcpyDeviceToHost);
+      printf("{\"sha_mix\":\"%s\",\"ms\":%.3f,\"gcompr_per_s\":%.2f}\n", name, ms, comp / ms / 1e6);
+    };
+    line("rot0_all", launch_sha<0>);
+    line("rot1_all", launch_sha<1>);
+    line("rot3_all", launch_sha<3>);
+    line("rot0+rot1_1of4", launch_shamix<0, 1, 1>);
+    line("rot0+rot1_2of4", launch_shamix<0, 1, 2>);
+    line("rot0+rot1_3of4", launch_shamix<0, 1, 3>);
+    line("rot3+rot1_1of4", launch_shamix<3, 1, 1>);
+    line("rot3+rot1_2of4", launch_shamix<3, 1, 2>);
+    line("rot3+rot1_3of4", launch_shamix<3, 1, 3>);
+    line("rot0+rot3_2of4", launch_shamix<0, 3, 2>);
+    return 0;
+  }
   auto op_line = [&](int op, void (*fn)(uint32_t*, int)) {
     const int iters = 400;
     const float ms = time_ms(fn, out, iters);
