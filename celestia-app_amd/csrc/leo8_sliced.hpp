@@ -93,7 +93,7 @@ inline constexpr WMasks kWMasksHost = make_wmasks();
 constexpr uint8_t kXor3 = 0x96;    // a ^ b ^ c
 constexpr uint8_t kXorAnd = 0x78;  // a ^ (b & c)
 constexpr uint8_t kXorAndN = 0xB4; // a ^ (b & ~c)
-constexpr uint8_t kXorThenAnd = 0x28;  // (a ^ b) & c
+constexpr uint8_t kSelect = 0xD8;      // c ? b : a (per bit)
 
 #if defined(__HIP_DEVICE_COMPILE__)
 #define SL_BOP3(a, b, c, tt) __builtin_amdgcn_bitop3_b32((a), (b), (c), (tt))
@@ -112,27 +112,22 @@ __host__ inline uint32_t sl_bop3_host(uint32_t a, uint32_t b, uint32_t c, uint8_
 
 // 8x8 bit transpose of the bytes of 8 dwords, 4 byte positions at once:
 // afterwards d[p] byte q bit w = old d[w] byte q bit p.  Its own inverse.
+// Each swap of a pair is two shifts and two v_bitop3 bit selects (4 fast ops;
+// the xor-swap form t = (hi >> s ^ lo) & m; lo ^= t; hi ^= t << s takes 5).
+__host__ __device__ __forceinline__ void swap_bits(uint32_t& hi, uint32_t& lo, int s, uint32_t m) {
+  const uint32_t h = hi, l = lo;
+  lo = SL_BOP3(l, h >> s, m, kSelect);         // lo with its m bits taken from hi >> s
+  hi = SL_BOP3(h, l << s, m << s, kSelect);    // hi with its m << s bits taken from lo << s
+}
 __host__ __device__ __forceinline__ void transpose8(uint32_t (&d)[8]) {
 #pragma unroll
-  for (int w = 0; w < 4; w++) {
-    const uint32_t t = SL_BOP3(d[w] >> 4, d[w + 4], 0x0F0F0F0Fu, kXorThenAnd);
-    d[w + 4] ^= t;
-    d[w] ^= t << 4;
-  }
+  for (int w = 0; w < 4; w++) swap_bits(d[w], d[w + 4], 4, 0x0F0F0F0Fu);
 #pragma unroll
   for (int w0 = 0; w0 < 8; w0 += 4)
 #pragma unroll
-    for (int w = w0; w < w0 + 2; w++) {
-      const uint32_t t = SL_BOP3(d[w] >> 2, d[w + 2], 0x33333333u, kXorThenAnd);
-      d[w + 2] ^= t;
-      d[w] ^= t << 2;
-    }
+    for (int w = w0; w < w0 + 2; w++) swap_bits(d[w], d[w + 2], 2, 0x33333333u);
 #pragma unroll
-  for (int w = 0; w < 8; w += 2) {
-    const uint32_t t = SL_BOP3(d[w] >> 1, d[w + 1], 0x55555555u, kXorThenAnd);
-    d[w + 1] ^= t;
-    d[w] ^= t << 1;
-  }
+  for (int w = 0; w < 8; w += 2) swap_bits(d[w], d[w + 1], 1, 0x55555555u);
 }
 
 // Compile-time loop: f(std::integral_constant<int, I>{}) for I = 0 .. N-1, so
