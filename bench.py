@@ -319,6 +319,10 @@ def main():
         "kernel_sum_ms_per_step": kernel_ms_step,
         "roofline": roof,
     }
+    # single-square latency first: after the replay's 64 GiB page-locked
+    # allocation the same device->host copies ran slower (k=128 with the EDS
+    # returned: 1.40 vs 0.89 ms, profiles/single_square_r02.log)
+    single = bench_single(ctx) if world == 1 and not args.no_e2e else None
     if not args.no_replay:
         out["block_replay"] = bench_replay(dist, rank, world, local, ctx, ds, args.replay_blocks,
                                            args.replay_dump)
@@ -327,7 +331,7 @@ def main():
         torch.cuda.empty_cache()
         out["end_to_end"] = bench_e2e(ctx, local, k, np.stack([host[i % nd] for i in range(B)]),
                                       max(3, args.steps // 4))
-        out["end_to_end"]["single_square"] = bench_single(ctx)
+        out["end_to_end"]["single_square"] = single
     if world == 1 and not args.no_configs:
         # configs[2] and configs[3] (and the GF(2^16) stress repair) at bounded
         # step counts, so that the driver's own run records them too

@@ -228,13 +228,20 @@ int run_group_host(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* ods, uin
   const size_t m = pipeline_chunk(k, n);
   if (n > m) return run_group_pipelined(ctx, k, n, m, ods, eds_out, rr, cr, dah, status);
   hipStream_t s = ctx->stream;
+  // roots, DAHs and status share one device buffer and come back in ONE copy
+  // to page-locked staging (four small copies into the caller's possibly
+  // pageable arrays cost ~20 us each on the single-square latency path)
+  const size_t rb = w * kNodeSize * n;
+  const size_t res_bytes = 2 * rb + 32 * n + sizeof(int32_t) * n;
   HIP_TRY(ctx, ctx->ods.ensure(ods_bytes(k) * n));
   HIP_TRY(ctx, ctx->eds.ensure(eds_bytes(k) * n));
-  HIP_TRY(ctx, ctx->rr.ensure(w * kNodeSize * n));
-  HIP_TRY(ctx, ctx->cr.ensure(w * kNodeSize * n));
-  HIP_TRY(ctx, ctx->dah.ensure(32 * n));
-  HIP_TRY(ctx, ctx->status.ensure(sizeof(int32_t) * n));
+  HIP_TRY(ctx, ctx->res.ensure(res_bytes));
+  HIP_TRY(ctx, ctx->h_out.ensure(res_bytes));
   HIP_TRY(ctx, ctx->ws.ensure(dagpu_workspace_size(k, n)));
+  uint8_t* d_rr = (uint8_t*)ctx->res.p;
+  uint8_t* d_cr = d_rr + rb;
+  uint8_t* d_dah = d_cr + rb;
+  int32_t* d_st = (int32_t*)(d_dah + 32 * n);  // rb = 180 k n: 4-byte aligned
   HIP_TRY(ctx, hipMemcpyAsync(ctx->ods.p, ods, ods_bytes(k) * n, hipMemcpyHostToDevice, s));
   // An EDS requested back goes down on the copy stream while the kernels run:
   // the top halves ([Q0|Q1], final after the row pass) during the column pass
@@ -255,18 +262,17 @@ int run_group_host(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* ods, uin
       HIP_TRY(ctx, hipMemcpyAsync(eds_out + i * eb + half, d + i * eb + half, half,
                                   hipMemcpyDeviceToHost, cs));
   }
-  rc = enqueue_roots(ctx, k, n, (const uint8_t*)ctx->eds.p, (uint8_t*)ctx->rr.p,
-                     (uint8_t*)ctx->cr.p, (uint8_t*)ctx->dah.p, (int32_t*)ctx->status.p,
-                     ctx->ws.p, s);
+  rc = enqueue_roots(ctx, k, n, (const uint8_t*)ctx->eds.p, d_rr, d_cr, d_dah, d_st, ctx->ws.p, s);
   if (rc) return rc;
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->h_out.p, ctx->res.p, res_bytes, hipMemcpyDeviceToHost, s));
   if (eds_out) HIP_TRY(ctx, hipStreamSynchronize(cs));
-  HIP_TRY(ctx, hipMemcpyAsync(rr, ctx->rr.p, w * kNodeSize * n, hipMemcpyDeviceToHost, s));
-  HIP_TRY(ctx, hipMemcpyAsync(cr, ctx->cr.p, w * kNodeSize * n, hipMemcpyDeviceToHost, s));
-  HIP_TRY(ctx, hipMemcpyAsync(dah, ctx->dah.p, 32 * n, hipMemcpyDeviceToHost, s));
-  std::vector<int32_t> st(n);
-  HIP_TRY(ctx, hipMemcpyAsync(st.data(), ctx->status.p, sizeof(int32_t) * n,
-                              hipMemcpyDeviceToHost, s));
   HIP_TRY(ctx, hipStreamSynchronize(s));
+  const uint8_t* h = (const uint8_t*)ctx->h_out.p;
+  memcpy(rr, h, rb);
+  memcpy(cr, h + rb, rb);
+  memcpy(dah, h + 2 * rb, 32 * n);
+  std::vector<int32_t> st(n);
+  memcpy(st.data(), h + 2 * rb + 32 * n, sizeof(int32_t) * n);
   return finish_status(ctx, st.data(), n, status);
 }
 
@@ -306,6 +312,7 @@ void dagpu_destroy(dagpu_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
   c->h_out.release();
+  c->res.release();
   c->ods.release(); c->eds.release(); c->rr.release(); c->cr.release();
   c->dah.release(); c->status.release(); c->ws.release();
   for (DevBuf* b : {&c->t_leaf_data, &c->t_leaves, &c->t_inner, &c->t_meta, &c->t_out, &c->t_status, &c->t_flags})

@@ -69,6 +69,7 @@ struct dagpu_ctx {
   std::mutex err_mu;
   std::string err;
   DevBuf ods, eds, rr, cr, dah, status, ws;
+  DevBuf res;  // host path: roots | roots | DAHs | status, one device->host copy
   // host-mode pipeline (dagpu.cpp run_group_pipelined): H2D on copy_stream,
   // kernels + D2H on stream, two slots handed over with events
   hipStream_t copy_stream = nullptr;
