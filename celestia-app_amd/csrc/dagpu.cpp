@@ -219,29 +219,54 @@ int run_group_pipelined(dagpu_ctx* ctx, uint32_t k, size_t n, size_t m, const ui
   return finish_status(ctx, st.data(), n, status);
 }
 
+// Roots, DAHs and status of a host-path call share one device buffer
+// (ctx->res: rr | cr | dah | status) and come back in ONE copy to page-locked
+// staging, then go to the caller's (possibly pageable) arrays by memcpy: four
+// small device->host copies cost ~20 us each on the single-square latency path
+// (profiles/single_square_r02.log).  Caller holds ctx->mu.
+struct HostResults {
+  size_t n = 0, rb = 0, bytes = 0;
+  uint8_t *rr = nullptr, *cr = nullptr, *dah = nullptr;
+  int32_t* st = nullptr;
+  hipError_t alloc(dagpu_ctx* ctx, uint32_t k, size_t cnt) {
+    n = cnt;
+    rb = 2 * (size_t)k * kNodeSize * n;
+    bytes = 2 * rb + 32 * n + sizeof(int32_t) * n;
+    hipError_t e = ctx->res.ensure(bytes);
+    if (e == hipSuccess) e = ctx->h_out.ensure(bytes);
+    if (e != hipSuccess) return e;
+    rr = (uint8_t*)ctx->res.p;
+    cr = rr + rb;
+    dah = cr + rb;
+    st = (int32_t*)(dah + 32 * n);  // rb = 180 k n: 4-byte aligned
+    return hipSuccess;
+  }
+  hipError_t download(dagpu_ctx* ctx, hipStream_t s) const {
+    return hipMemcpyAsync(ctx->h_out.p, ctx->res.p, bytes, hipMemcpyDeviceToHost, s);
+  }
+  // after the stream has synchronised
+  void deliver(const dagpu_ctx* ctx, uint8_t* o_rr, uint8_t* o_cr, uint8_t* o_dah, int32_t* o_st) const {
+    const uint8_t* h = (const uint8_t*)ctx->h_out.p;
+    memcpy(o_rr, h, rb);
+    memcpy(o_cr, h + rb, rb);
+    memcpy(o_dah, h + 2 * rb, 32 * n);
+    memcpy(o_st, h + 2 * rb + 32 * n, sizeof(int32_t) * n);
+  }
+};
+
 // Runs one uniform-k group from host memory.  Caller holds ctx->mu.
 int run_group_host(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* ods, uint8_t* eds_out,
                    uint8_t* rr, uint8_t* cr, uint8_t* dah, int32_t* status) {
   int rc = check_k(ctx, k);
   if (rc) return rc;
-  const size_t w = 2 * (size_t)k;
   const size_t m = pipeline_chunk(k, n);
   if (n > m) return run_group_pipelined(ctx, k, n, m, ods, eds_out, rr, cr, dah, status);
   hipStream_t s = ctx->stream;
-  // roots, DAHs and status share one device buffer and come back in ONE copy
-  // to page-locked staging (four small copies into the caller's possibly
-  // pageable arrays cost ~20 us each on the single-square latency path)
-  const size_t rb = w * kNodeSize * n;
-  const size_t res_bytes = 2 * rb + 32 * n + sizeof(int32_t) * n;
+  HostResults res;
   HIP_TRY(ctx, ctx->ods.ensure(ods_bytes(k) * n));
   HIP_TRY(ctx, ctx->eds.ensure(eds_bytes(k) * n));
-  HIP_TRY(ctx, ctx->res.ensure(res_bytes));
-  HIP_TRY(ctx, ctx->h_out.ensure(res_bytes));
+  HIP_TRY(ctx, res.alloc(ctx, k, n));
   HIP_TRY(ctx, ctx->ws.ensure(dagpu_workspace_size(k, n)));
-  uint8_t* d_rr = (uint8_t*)ctx->res.p;
-  uint8_t* d_cr = d_rr + rb;
-  uint8_t* d_dah = d_cr + rb;
-  int32_t* d_st = (int32_t*)(d_dah + 32 * n);  // rb = 180 k n: 4-byte aligned
   HIP_TRY(ctx, hipMemcpyAsync(ctx->ods.p, ods, ods_bytes(k) * n, hipMemcpyHostToDevice, s));
   // An EDS requested back goes down on the copy stream while the kernels run:
   // the top halves ([Q0|Q1], final after the row pass) during the column pass
@@ -262,17 +287,13 @@ int run_group_host(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* ods, uin
       HIP_TRY(ctx, hipMemcpyAsync(eds_out + i * eb + half, d + i * eb + half, half,
                                   hipMemcpyDeviceToHost, cs));
   }
-  rc = enqueue_roots(ctx, k, n, (const uint8_t*)ctx->eds.p, d_rr, d_cr, d_dah, d_st, ctx->ws.p, s);
+  rc = enqueue_roots(ctx, k, n, (const uint8_t*)ctx->eds.p, res.rr, res.cr, res.dah, res.st, ctx->ws.p, s);
   if (rc) return rc;
-  HIP_TRY(ctx, hipMemcpyAsync(ctx->h_out.p, ctx->res.p, res_bytes, hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, res.download(ctx, s));
   if (eds_out) HIP_TRY(ctx, hipStreamSynchronize(cs));
   HIP_TRY(ctx, hipStreamSynchronize(s));
-  const uint8_t* h = (const uint8_t*)ctx->h_out.p;
-  memcpy(rr, h, rb);
-  memcpy(cr, h + rb, rb);
-  memcpy(dah, h + 2 * rb, 32 * n);
   std::vector<int32_t> st(n);
-  memcpy(st.data(), h + 2 * rb + 32 * n, sizeof(int32_t) * n);
+  res.deliver(ctx, rr, cr, dah, st.data());
   return finish_status(ctx, st.data(), n, status);
 }
 
@@ -558,24 +579,18 @@ int dagpu_roots(dagpu_ctx* ctx, uint32_t k, const uint8_t* eds, uint8_t* row_roo
   (void)hipSetDevice(ctx->device);
   int rc = check_k(ctx, k);
   if (rc) return rc;
-  const size_t w = 2 * (size_t)k;
   hipStream_t s = ctx->stream;
+  HostResults res;
   HIP_TRY(ctx, ctx->eds.ensure(eds_bytes(k)));
-  HIP_TRY(ctx, ctx->rr.ensure(w * kNodeSize));
-  HIP_TRY(ctx, ctx->cr.ensure(w * kNodeSize));
-  HIP_TRY(ctx, ctx->dah.ensure(32));
-  HIP_TRY(ctx, ctx->status.ensure(sizeof(int32_t)));
+  HIP_TRY(ctx, res.alloc(ctx, k, 1));
   HIP_TRY(ctx, ctx->ws.ensure(dagpu_workspace_size(k, 1)));
   HIP_TRY(ctx, hipMemcpyAsync(ctx->eds.p, eds, eds_bytes(k), hipMemcpyHostToDevice, s));
-  rc = enqueue_roots(ctx, k, 1, (const uint8_t*)ctx->eds.p, (uint8_t*)ctx->rr.p,
-                     (uint8_t*)ctx->cr.p, (uint8_t*)ctx->dah.p, (int32_t*)ctx->status.p, ctx->ws.p, s);
+  rc = enqueue_roots(ctx, k, 1, (const uint8_t*)ctx->eds.p, res.rr, res.cr, res.dah, res.st, ctx->ws.p, s);
   if (rc) return rc;
-  int32_t st = 0;
-  HIP_TRY(ctx, hipMemcpyAsync(row_roots, ctx->rr.p, w * kNodeSize, hipMemcpyDeviceToHost, s));
-  HIP_TRY(ctx, hipMemcpyAsync(col_roots, ctx->cr.p, w * kNodeSize, hipMemcpyDeviceToHost, s));
-  HIP_TRY(ctx, hipMemcpyAsync(dah, ctx->dah.p, 32, hipMemcpyDeviceToHost, s));
-  HIP_TRY(ctx, hipMemcpyAsync(&st, ctx->status.p, sizeof st, hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, res.download(ctx, s));
   HIP_TRY(ctx, hipStreamSynchronize(s));
+  int32_t st = 0;
+  res.deliver(ctx, row_roots, col_roots, dah, &st);
   if (st & kStatusPushOrder)
     return set_err(ctx, DAGPU_ERR_PUSH_ORDER, "invalid push order: namespaces of original data square are not sorted");
   return DAGPU_OK;
