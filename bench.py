@@ -58,7 +58,10 @@ def dist_init():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # DAGPU_BENCH_FORCE_DIST=1 (under torch.distributed.run) keeps the process
+    # group even at one rank, so the N > 1 code path -- RCCL collectives
+    # included -- runs on a one-GPU box (tests/test_gpu_bench_checks.py)
+    if world > 1 or os.environ.get("DAGPU_BENCH_FORCE_DIST") == "1":
         import torch.distributed as dist
         import datetime
         if os.environ.get("DAGPU_BENCH_SHARED_GPU") == "1":
@@ -346,7 +349,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.cpu_threads or host_threads())
         out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
-    if world > 1 and not args.no_split:
+    if dist is not None and not args.no_split:
         # configs[4] stress: one oversized square split over all ranks (RCCL all-to-all)
         del ds
         torch.cuda.empty_cache()

@@ -8,6 +8,8 @@ bench's cross-rank checks:
   ranks sharing GPU 0 (DAGPU_BENCH_SHARED_GPU=1, gloo collectives) replays
   distinct squares host-streamed and device-resident, and the sampled DAHs it
   reports match the oracle;
+* the same path with ONE rank keeping its RCCL ("nccl") process group, so the
+  replay's and the split square's collectives run through RCCL on this box;
 * a deliberately wrong DAH (DAGPU_BENCH_CORRUPT) after the gather, inside a
   rank's own results, or in the split square makes bench.py exit non-zero;
 * two host threads issuing device-resident calls on ONE context, one of them
@@ -74,13 +76,22 @@ def _free_port():
     return p
 
 
-def _run_bench(args, corrupt=None, timeout=110):
-    env = dict(os.environ, DAGPU_BENCH_SHARED_GPU="1", MASTER_ADDR="127.0.0.1")
+def _run_bench(args, corrupt=None, timeout=110, nccl=False):
+    """bench.py under torch.distributed.run: 2 ranks sharing GPU 0 over gloo,
+    or (nccl=True) ONE rank that keeps its RCCL process group, so the N > 1
+    code path runs its collectives through RCCL on a one-GPU box."""
+    if nccl:
+        env = dict(os.environ, DAGPU_BENCH_FORCE_DIST="1", MASTER_ADDR="127.0.0.1")
+        env.pop("DAGPU_BENCH_SHARED_GPU", None)
+        nproc = "1"
+    else:
+        env = dict(os.environ, DAGPU_BENCH_SHARED_GPU="1", MASTER_ADDR="127.0.0.1")
+        nproc = "2"
     if corrupt:
         env["DAGPU_BENCH_CORRUPT"] = corrupt
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", nproc,
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(ROOT, "bench.py"), "--gpus", "2"] + args
+           os.path.join(ROOT, "bench.py"), "--gpus", nproc] + args
     return subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
 
 
@@ -118,6 +129,32 @@ def test_split_corruption_is_fatal():
                      corrupt="split")
     assert out.returncode != 0
     assert "FATAL: split square k=16" in out.stderr
+
+
+def test_rccl_path_one_rank(tmp_path):
+    """The N > 1 bench path with its RCCL process group kept at one rank: the
+    replay's all-gathers and max-reduces and the split square's all-to-all and
+    all-gathers run through RCCL (torch backend "nccl"); outputs bit-exact."""
+    dump = str(tmp_path / "replay.json")
+    out = _run_bench(["--steps", "2", "--warmup", "1", "--batch", "8", "--replay-blocks", "24", "--no-cpu",
+                      "--split-k", "16", "256", "--split-steps", "1", "--replay-dump", dump], nccl=True)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 1 and line["block_replay"]["bit_exact"] is True
+    for k in ("16", "256"):
+        sp = line["split_stress"][k]
+        assert sp["dah_matches_single_gpu"] is True and "nccl" in sp["collective"], sp
+    d = json.load(open(dump))
+    for b, hexdah in d["sampled_dah"].items():
+        sq = synth.blob_squares(d["k"], d["seed"], int(b), 1)[0].reshape(d["k"] ** 2, 512)
+        _, _, _, odah = oracle.extend_and_dah(sq, d["k"], nthreads=16, want_eds=False)
+        assert odah.hex() == hexdah, b
+
+
+def test_rccl_replay_corruption_is_fatal():
+    out = _run_bench(_REPLAY, corrupt="replay-gather", nccl=True)
+    assert out.returncode != 0
+    assert "FATAL: block replay DAH check failed" in out.stderr
 
 
 def test_two_threads_one_context(ctx):
