@@ -351,7 +351,8 @@ def main():
         out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
     if dist is not None and not args.no_split:
         # configs[4] stress: one oversized square split over all ranks (RCCL all-to-all)
-        del ds
+        if "ds" in locals():
+            del ds
         torch.cuda.empty_cache()
         out["split_stress"] = {str(sk): bench_split(dist, rank, world, local, ctx, sk, args.split_steps, 1)
                                for sk in args.split_k}
