@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import oracle
-from celestia_da import da, synth
+from celestia_da import _abi, da, synth
 
 from conftest import GOLDEN
 
@@ -198,7 +198,7 @@ def test_codec_encode_sliced_shapes(ctx, k, shard):
 _PACKED_CHILD = r"""
 import hashlib, sys
 sys.path[:0] = sys.argv[1:3]
-from celestia_da import da, synth
+from celestia_da import _abi, da, synth
 ctx = da.Context(0)
 for k in (16, 32, 64, 128):
     eds = da.extend_shares(synth.random_blob_square(k, 100 + k), ctx)
@@ -456,3 +456,39 @@ def test_repair_device_batch(ctx):
     assert (status.cpu().numpy() == 0).all()
     assert bool((present == 1).all())
     assert torch.equal(ds.eds, eds_ref)
+
+
+def test_repair_device_batch_mixed_outcomes(ctx):
+    """C4 on a 64-square device batch at k = 64: distinct maximal erasure
+    patterns, one byzantine square and one unrepairable square; every status
+    lands on its own square and every other square is rebuilt bit-exactly."""
+    import torch
+    from celestia_da.device import DeviceSquares
+
+    k, n = 64, 64
+    w = 2 * k
+    ds = DeviceSquares(k, n, ctx=ctx)
+    host = synth.blob_squares(k, 6464, 0, n)
+    ds.load_ods(host)
+    ds.extend()
+    eds_ref = ds.eds.clone()
+    pres = np.stack([_subgrid(k, 900 + i) for i in range(n)])
+    byz, unrep = 20, 40
+    r, c = np.argwhere(pres[unrep])[0]
+    pres[unrep][r, :] = False
+    pres[unrep][:, c] = False
+    present = torch.from_numpy(pres.reshape(n, -1).astype(np.uint8)).cuda()
+    mask = present.view(n, w * w, 1)
+    ds.eds.copy_((ds.eds.view(n, w * w, 512) * mask).view(n, -1))
+    rb, cb = np.argwhere(pres[byz])[3]
+    ds.eds.view(n, w, w, 512)[byz, rb, cb, 77] ^= 0x10
+    status = torch.full((n,), -99, dtype=torch.int32, device="cuda")
+    ds.repair(present, status, ds.repair_workspace())
+    torch.cuda.synchronize()
+    st = status.cpu().numpy()
+    want = np.zeros(n, np.int32)
+    want[byz], want[unrep] = _abi.ERR_BYZANTINE, _abi.ERR_UNREPAIRABLE
+    assert (st == want).all(), st
+    ok = [i for i in range(n) if i not in (byz, unrep)]
+    assert torch.equal(ds.eds[ok], eds_ref[ok])
+    assert bool((present[ok] == 1).all())
