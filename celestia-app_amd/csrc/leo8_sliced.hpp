@@ -312,11 +312,11 @@ __host__ __device__ __forceinline__ void muladd_ct_lane(uint32_t (&x)[8], const 
   });
 }
 
-// IFFT layers 0..2 in the two-vector layout A (K = 128), wave w, lane mask of eb.
-template <int K>
+// IFFT layers 0..NL-1 in the two-vector layout A (K = 128), wave w, lane mask of eb.
+template <int K, int NL = 3>
 __host__ __device__ __forceinline__ void ifft_A2(uint32_t (&v)[16][8], int w, uint32_t ebmask) {
   static_assert(K == 128, "two-vector layout: k = 128");
-  static_for<3>([&](auto m) {
+  static_for<NL>([&](auto m) {
     constexpr int D = 1 << m;
     SL_FENCE();
     static_for<16>([&](auto j) {
@@ -342,12 +342,12 @@ __host__ __device__ __forceinline__ void ifft_A2(uint32_t (&v)[16][8], int w, ui
   });
 }
 
-// FFT layers 2..0 in the two-vector layout A.
-template <int K>
+// FFT layers NL-1..0 in the two-vector layout A.
+template <int K, int NL = 3>
 __host__ __device__ __forceinline__ void fft_A2(uint32_t (&v)[16][8], int w, uint32_t ebmask) {
   static_assert(K == 128, "two-vector layout: k = 128");
-  static_for<3>([&](auto mm) {
-    constexpr int m = 2 - mm;
+  static_for<NL>([&](auto mm) {
+    constexpr int m = NL - 1 - mm;
     constexpr int D = 1 << m;
     SL_FENCE();
     static_for<16>([&](auto j) {
@@ -372,6 +372,63 @@ __host__ __device__ __forceinline__ void fft_A2(uint32_t (&v)[16][8], int w, uin
   });
 }
 
+
+// Two-vector layout A* (K = 128): e = eb + 2 r + 32 w, the lane bit is element
+// bit 0 (a wave-local transpose of A).  Layers 1..2 pair register bits 0..1 of
+// r; their skews depend on element bits above the pair bit only, so the lane
+// bit drops out: C(register bits) ^ w0 S32 ^ w1 S64, no lane term.
+template <int K>
+__host__ __device__ __forceinline__ void ifft_As2(uint32_t (&v)[16][8], int w) {
+  static_assert(K == 128, "two-vector layout: k = 128");
+  static_for<2>([&](auto mm) {
+    constexpr int m = 1 + mm;
+    constexpr int D = 1 << m, R = D >> 1;
+    SL_FENCE();
+    static_for<16>([&](auto r) {
+      if constexpr (!(r & R)) {
+        constexpr int c = skew_elem(D - 1 + K + ((2 * r) & ~(2 * D - 1)));
+        xor8(v[r + R], v[r]);
+        muladd_ct<c>(v[r], v[r + R]);
+      }
+    });
+    if (w & 1) {
+      static_for<16>([&](auto r) {
+        if constexpr (!(r & R)) muladd_ct<skew_elem(D - 1 + 32)>(v[r], v[r + R]);
+      });
+    }
+    if (w & 2) {
+      static_for<16>([&](auto r) {
+        if constexpr (!(r & R)) muladd_ct<skew_elem(D - 1 + 64)>(v[r], v[r + R]);
+      });
+    }
+  });
+}
+
+template <int K>
+__host__ __device__ __forceinline__ void fft_As2(uint32_t (&v)[16][8], int w) {
+  static_assert(K == 128, "two-vector layout: k = 128");
+  static_for<2>([&](auto mm) {
+    constexpr int m = 2 - mm;
+    constexpr int D = 1 << m, R = D >> 1;
+    SL_FENCE();
+    static_for<16>([&](auto r) {
+      if constexpr (!(r & R)) muladd_ct<skew_elem(D - 1 + ((2 * r) & ~(2 * D - 1)))>(v[r], v[r + R]);
+    });
+    if (w & 1) {
+      static_for<16>([&](auto r) {
+        if constexpr (!(r & R)) muladd_ct<skew_elem(D - 1 + 32)>(v[r], v[r + R]);
+      });
+    }
+    if (w & 2) {
+      static_for<16>([&](auto r) {
+        if constexpr (!(r & R)) muladd_ct<skew_elem(D - 1 + 64)>(v[r], v[r + R]);
+      });
+    }
+    static_for<16>([&](auto r) {
+      if constexpr (!(r & R)) xor8(v[r + R], v[r]);
+    });
+  });
+}
 
 // ---------------------------------------------------------------------------
 // Bit-sliced decode for k = 128 (rs_decode_sliced.hip leo8_decode128_sliced_kernel):

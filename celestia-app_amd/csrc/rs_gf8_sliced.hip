@@ -152,25 +152,60 @@ void leo8_encode_sliced_kernel(EncodeArgs a) {
 // vv = (l >> 4) & 1 (vector), eb = l >> 5 (element bit).  LDS slot of element e
 // for lane (vv, t): e * 32 + vv * 16 + t, 4 planes per pass, two passes.
 // ---------------------------------------------------------------------------
-template <bool A_TO_B>
-__device__ __forceinline__ void exchange2(uint32_t (&v)[16][8], u32x4* lds, int w, int eb, int col) {
+// A* <-> B through the workgroup's lds: A* holds element e = eb + 2 r + 32 w.
+template <bool S_TO_B>
+__device__ __forceinline__ void exchange2s(uint32_t (&v)[16][8], u32x4* lds, int w, int eb, int col) {
 #pragma unroll
   for (int h = 0; h < 2; h++) {
     if (h) __syncthreads();
 #pragma unroll
     for (int r = 0; r < 16; r++) {
-      const int e = A_TO_B ? r + 16 * eb + 32 * w : eb + 2 * w + 8 * r;
+      const int e = S_TO_B ? eb + 2 * r + 32 * w : eb + 2 * w + 8 * r;
       lds[e * 32 + col] = (u32x4){v[r][4 * h], v[r][4 * h + 1], v[r][4 * h + 2], v[r][4 * h + 3]};
     }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < 16; r++) {
-      const int e = A_TO_B ? eb + 2 * w + 8 * r : r + 16 * eb + 32 * w;
+      const int e = S_TO_B ? eb + 2 * w + 8 * r : eb + 2 * r + 32 * w;
       const u32x4 q = lds[e * 32 + col];
       v[r][4 * h] = q.x;
       v[r][4 * h + 1] = q.y;
       v[r][4 * h + 2] = q.z;
       v[r][4 * h + 3] = q.w;
+    }
+  }
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// A <-> A*: the wave's own 32 elements swap element bit 0 (register bit in A)
+// with element bit 4 (the lane bit eb in A), through the wave's quarter of lds
+// (16 KB per half of 4 planes); a wave's LDS operations complete in order, so
+// wave-scope fences separate the phases.
+template <bool A_TO_S>
+__device__ __forceinline__ void transpose_wave2(uint32_t (&v)[16][8], u32x4* lds, int w, int eb, int col) {
+  u32x4* q = lds + w * 32 * 32;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    if (h) wave_lds_sync();
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      const int e = A_TO_S ? r + 16 * eb : eb + 2 * r;
+      q[e * 32 + col] = (u32x4){v[r][4 * h], v[r][4 * h + 1], v[r][4 * h + 2], v[r][4 * h + 3]};
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      const int e = A_TO_S ? eb + 2 * r : r + 16 * eb;
+      const u32x4 x = q[e * 32 + col];
+      v[r][4 * h] = x.x;
+      v[r][4 * h + 1] = x.y;
+      v[r][4 * h + 2] = x.z;
+      v[r][4 * h + 3] = x.w;
     }
   }
 }
@@ -224,14 +259,22 @@ void leo8_encode_sliced2_kernel(EncodeArgs a) {
 #pragma unroll
   for (int j = 0; j < 16; j++) transpose8(v[j]);
 
+  // layer 0 in A (lane term), layers 1..2 in A* (element bit 0 in the lane:
+  // no lane term), layers 3..6 in B (compile-time skews), and back
   const int col = vv * 16 + t;
-  ifft_A2<K>(v, w, ebmask);
-  exchange2<true>(v, lds, w, eb, col);
+  ifft_A2<K, 1>(v, w, ebmask);
+  transpose_wave2<true>(v, lds, w, eb, col);
+  ifft_As2<K>(v, w);
+  __syncthreads();  // every wave's wave-local reads are done before the exchange writes
+  exchange2s<true>(v, lds, w, eb, col);
   ifft_B<K>(v);
   fft_B<K>(v);
   __syncthreads();
-  exchange2<false>(v, lds, w, eb, col);
-  fft_A2<K>(v, w, ebmask);
+  exchange2s<false>(v, lds, w, eb, col);
+  fft_As2<K>(v, w);
+  __syncthreads();  // other waves' last exchange reads of this wave's quarter are done
+  transpose_wave2<false>(v, lds, w, eb, col);
+  fft_A2<K, 1>(v, w, ebmask);
 
 #pragma unroll
   for (int j = 0; j < 16; j++) transpose8(v[j]);

@@ -59,7 +59,8 @@ void encode_chunk_lane(const uint8_t* data, uint8_t* parity, long shard, long co
 
 // Two-vector layout of leo8_encode_sliced2_kernel (k = 128): one vector's
 // column block t, the 8 (wave w, lane element bit eb) "lanes" of layout A
-// (e = j + 16 eb + 32 w) and layout B (e = eb + 2 w + 8 i).
+// (e = j + 16 eb + 32 w, layer 0), A* (e = eb + 2 r + 32 w, layers 1..2) and
+// B (e = eb + 2 w + 8 i).
 void encode2_chunk_lane(const uint8_t* data, uint8_t* parity, long shard, long col0) {
   constexpr int K = 128;
   static uint32_t st[4][2][16][8], tmp[4][2][16][8];
@@ -73,27 +74,44 @@ void encode2_chunk_lane(const uint8_t* data, uint8_t* parity, long shard, long c
         transpose8(d);
         memcpy(st[w][eb][j], d, 32);
       }
+  static uint32_t as[4][2][16][8];  // layout A*: e = eb + 2 r + 32 w
   for (int w = 0; w < 4; w++)
-    for (int eb = 0; eb < 2; eb++) ifft_A2<K>(st[w][eb], w, eb ? 0xFFFFFFFFu : 0u);
-  for (int w = 0; w < 4; w++)  // A -> B
+    for (int eb = 0; eb < 2; eb++) ifft_A2<K, 1>(st[w][eb], w, eb ? 0xFFFFFFFFu : 0u);
+  for (int w = 0; w < 4; w++)  // A -> A* (wave-local)
+    for (int eb = 0; eb < 2; eb++)
+      for (int r = 0; r < 16; r++) {
+        const int e = eb + 2 * r;  // within the wave
+        memcpy(as[w][eb][r], st[w][e >> 4][e & 15], 32);
+      }
+  for (int w = 0; w < 4; w++)
+    for (int eb = 0; eb < 2; eb++) ifft_As2<K>(as[w][eb], w);
+  for (int w = 0; w < 4; w++)  // A* -> B
     for (int eb = 0; eb < 2; eb++)
       for (int i = 0; i < 16; i++) {
         const int e = eb + 2 * w + 8 * i;
-        memcpy(tmp[w][eb][i], st[e >> 5][(e >> 4) & 1][e & 15], 32);
+        memcpy(tmp[w][eb][i], as[e >> 5][e & 1][(e >> 1) & 15], 32);
       }
   for (int w = 0; w < 4; w++)
     for (int eb = 0; eb < 2; eb++) {
       ifft_B<K>(tmp[w][eb]);
       fft_B<K>(tmp[w][eb]);
     }
-  for (int w = 0; w < 4; w++)  // B -> A
+  for (int w = 0; w < 4; w++)  // B -> A*
     for (int eb = 0; eb < 2; eb++)
       for (int i = 0; i < 16; i++) {
         const int e = eb + 2 * w + 8 * i;
-        memcpy(st[e >> 5][(e >> 4) & 1][e & 15], tmp[w][eb][i], 32);
+        memcpy(as[e >> 5][e & 1][(e >> 1) & 15], tmp[w][eb][i], 32);
       }
   for (int w = 0; w < 4; w++)
-    for (int eb = 0; eb < 2; eb++) fft_A2<K>(st[w][eb], w, eb ? 0xFFFFFFFFu : 0u);
+    for (int eb = 0; eb < 2; eb++) fft_As2<K>(as[w][eb], w);
+  for (int w = 0; w < 4; w++)  // A* -> A (wave-local)
+    for (int eb = 0; eb < 2; eb++)
+      for (int r = 0; r < 16; r++) {
+        const int e = eb + 2 * r;
+        memcpy(st[w][e >> 4][e & 15], as[w][eb][r], 32);
+      }
+  for (int w = 0; w < 4; w++)
+    for (int eb = 0; eb < 2; eb++) fft_A2<K, 1>(st[w][eb], w, eb ? 0xFFFFFFFFu : 0u);
   for (int w = 0; w < 4; w++)
     for (int eb = 0; eb < 2; eb++)
       for (int j = 0; j < 16; j++) {
