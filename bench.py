@@ -173,6 +173,35 @@ def load_traffic(kernel: str):
         return None
 
 
+def valu_issue(k: int, B: int, ms_step: float, leaf_ms: float):
+    """Whole-step VALU issue rate: the kernels' VALU wave-instructions per step
+    (rocprofv3 SQ_INSTS_VALU per launch, profiles/pmc_valu.json, collected on
+    this same k=128 x 256-square step by tools/gpu_profile.sh) over the measured
+    step time x CUs x the clock the chip holds (GRBM_GUI_ACTIVE of the leaf
+    launch, summed over MI355X's 8 XCDs, over this run's leaf time).  The
+    ceiling of any stream with slow-class ops (v_alignbit, v_add3, v_perm) is
+    ~1 wave-instruction per clock per CU (profiles/issue_bench_r01.log)."""
+    path = os.path.join(ROOT, "profiles", "pmc_valu.json")
+    try:
+        d = json.load(open(path))
+        per = {n: d[n]["valu_wave_instr_per_launch"] for n in
+               ("rs_encode_sliced2", "nmt_leaves", "nmt_trees_l1", "nmt_trees_ln", "dah")}
+        grbm = d["nmt_leaves"]["grbm_gui_active_per_launch"]
+        tag = d["nmt_leaves"].get("tag")
+    except Exception:
+        return None
+    if k != 128 or B != 256 or not grbm or not leaf_ms:
+        return None
+    levels = 8  # tree levels at k = 128: level 1 + 7 level launches
+    total = 2 * per["rs_encode_sliced2"] + per["nmt_leaves"] + per["nmt_trees_l1"] \
+        + (levels - 1) * per["nmt_trees_ln"] + per["dah"]
+    clock = grbm / 8 / (leaf_ms * 1e-3)
+    cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    return {"wave_instr_per_step": total, "clock_ghz": clock / 1e9, "cus": cus,
+            "wave_instr_per_clk_per_cu": total / (ms_step * 1e-3 * cus * clock),
+            "ceiling": 1.0, "source": f"profiles/pmc_valu.json ({tag}) + this run's step and leaf times"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -321,6 +350,7 @@ def main():
         "kernel_ms_note": "separate profiled pass (HIP events around each kernel on the launch stream); the timed steps run unprofiled",
         "kernel_sum_ms_per_step": kernel_ms_step,
         "roofline": roof,
+        "valu_issue": valu_issue(k, B, ms_step, per["nmt_leaves"]),
     }
     # single-square latency first: after the replay's 64 GiB page-locked
     # allocation the same device->host copies ran slower (k=128 with the EDS

@@ -4,6 +4,7 @@ Reads gpurun_out/prof/{trace,pmc}_<tag>* CSVs written by rocprofv3 and writes
   profiles/kernel_stats_<tag>.csv   (rocprofv3 --kernel-trace --stats summary)
   profiles/pmc_<tag>.json           (per-kernel counters, averaged per dispatch)
   profiles/pmc_traffic.json         (HBM bytes per launch, gfx950-corrected)
+  profiles/pmc_valu.json            (VALU wave-instructions and GRBM_GUI_ACTIVE per launch)
 HBM bytes = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes): on gfx950 FETCH_SIZE
 reads half of a wide streaming read's bytes (MI355X_MICROARCH.md §HBM).
 """
@@ -59,6 +60,13 @@ def main(tag: str) -> None:
                           "tag": tag}
     if traffic:
         json.dump(traffic, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
+    # VALU wave-instructions and GRBM_GUI_ACTIVE (summed over the 8 XCDs) per launch: bench.py's
+    # whole-step issue rate (instructions per step / (step time x CUs x clock))
+    valu = {k: {"valu_wave_instr_per_launch": d["SQ_INSTS_VALU"],
+                "grbm_gui_active_per_launch": d.get("GRBM_GUI_ACTIVE"), "tag": tag}
+            for k, d in out.items() if "SQ_INSTS_VALU" in d}
+    if valu:
+        json.dump(valu, open(os.path.join(ROOT, "profiles", "pmc_valu.json"), "w"), indent=1)
     print(json.dumps(traffic, indent=1))
 
 
