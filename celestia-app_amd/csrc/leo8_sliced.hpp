@@ -558,91 +558,35 @@ __host__ __device__ __forceinline__ void deriv_local(uint32_t (&v)[16][8]) {
   });
 }
 
-// x * c for a per-lane field element c (the decoder's error-locator
-// multiplies).  c is given in the power basis of G = 94: c = XOR over bits k of
-// cp of G^k (kDecPow below maps a log value to that form), so
-//   x * c = XOR over bits k of cp of (x * G^k),
-// a chain of compile-time multiplies by G -- 8 ops each, the cheapest such G
-// (every row of its matrix has at most 3 set bits) -- and one and-xor per
-// plane and power.  Only full-rate ops (no v_perm table lookups).
-constexpr int kDecG = 94;
-
-struct DecPow {
-  uint8_t cp[256];  // cp[lm]: exp(lm) in the power basis of G (exp(255) = exp(0) = 1)
-};
-constexpr DecPow make_decpow() {
-  // columns G^0..G^7; solve c = P * cp by Gaussian elimination over GF(2)
-  uint8_t pw[8] = {};
-  pw[0] = 1;
-  for (int k = 1; k < 8; k++) pw[k] = gmul(pw[k - 1], (uint8_t)kDecG);
-  DecPow t{};
-  for (int lm = 0; lm < 256; lm++) {
-    const uint8_t c = kGf8.exp[lm];
-    // augmented rows: bit i of each column k, plus the target bit i of c
-    uint16_t row[8] = {};
-    for (int i = 0; i < 8; i++) {
-      uint16_t r = 0;
-      for (int k = 0; k < 8; k++) r |= (uint16_t)(((pw[k] >> i) & 1) << k);
-      r |= (uint16_t)(((c >> i) & 1) << 8);
-      row[i] = r;
-    }
-    int rk = 0;
-    for (int col = 0; col < 8; col++) {
-      int piv = -1;
-      for (int i = rk; i < 8; i++)
-        if ((row[i] >> col) & 1) { piv = i; break; }
-      if (piv < 0) continue;
-      const uint16_t tmp = row[rk]; row[rk] = row[piv]; row[piv] = tmp;
-      for (int i = 0; i < 8; i++)
-        if (i != rk && ((row[i] >> col) & 1)) row[i] ^= row[rk];
-      rk++;
-    }
-    uint8_t cp = 0;
-    for (int i = 0; i < 8; i++)
-      for (int col = 0; col < 8; col++)
-        if (row[i] & (1 << col)) { cp |= (uint8_t)(((row[i] >> 8) & 1) << col); break; }
-    t.cp[lm] = cp;
-  }
-  return t;
+// x * exp(lm) on PACKED bytes (before the bit transpose / after the inverse
+// one): tb = {t[0][lm], t[1][lm], t[2][lm], t[3][lm]} (gf_const.hpp: bytes
+// c * (v << 2g), v = 0..3), or all zero for a missing shard.  Per dword: four
+// 2-bit byte-table lookups (v_perm) and two xors, 13 ops for 4 bytes against
+// the earlier bit-plane power-basis multiply's ~136 for 32 bytes.
+typedef unsigned int tab4 __attribute__((ext_vector_type(4)));
+__host__ __device__ __forceinline__ uint32_t perm4(uint32_t tab, uint32_t idx) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_perm(tab, tab, idx);
+#else
+  uint32_t r = 0;
+  for (int b = 0; b < 4; b++) r |= ((tab >> (8 * ((idx >> (8 * b)) & 3))) & 0xFFu) << (8 * b);
+  return r;
+#endif
 }
-inline constexpr DecPow kDecPow = make_decpow();
-constexpr bool decpow_ok() {
-  uint8_t pw[8] = {};
-  pw[0] = 1;
-  for (int k = 1; k < 8; k++) pw[k] = gmul(pw[k - 1], (uint8_t)kDecG);
-  for (int lm = 0; lm < 256; lm++) {
-    uint8_t c = 0;
-    for (int k = 0; k < 8; k++)
-      if ((kDecPow.cp[lm] >> k) & 1) c ^= pw[k];
-    if (c != kGf8.exp[lm]) return false;
-  }
-  return true;
-}
-static_assert(decpow_ok(), "power-basis table of the decoder's runtime multiplies");
-
-__host__ __device__ __forceinline__ void mul_lane(uint32_t (&x)[8], uint32_t cp) {
-  uint32_t acc[8], cur[8];
-  {
-    const uint32_t m = (uint32_t)(-(int32_t)(cp & 1u));
-    static_for<8>([&](auto p) {
-      cur[p] = x[p];
-      acc[p] = x[p] & m;
-    });
-  }
-  static_for<7>([&](auto kk) {
-    constexpr int k = kk + 1;
-    uint32_t n[8];
-    static_for<8>([&](auto i) {
-      constexpr int R = kMat.row[kDecG][i];
-      n[i] = row_sum<R>(cur);
-    });
-    const uint32_t m = (uint32_t)(-(int32_t)((cp >> k) & 1u));
-    static_for<8>([&](auto p) {
-      cur[p] = n[p];
-      acc[p] = SL_BOP3(acc[p], n[p], m, kXorAnd);
-    });
+__host__ __device__ __forceinline__ void mul_packed(uint32_t (&d)[8], const tab4 tb) {
+  static_for<8>([&](auto i) {
+    const uint32_t y = d[i];
+    const uint32_t p0 = perm4(tb.x, y & 0x03030303u);
+    const uint32_t p1 = perm4(tb.y, (y >> 2) & 0x03030303u);
+    const uint32_t p2 = perm4(tb.z, (y >> 4) & 0x03030303u);
+    const uint32_t p3 = perm4(tb.w, (y >> 6) & 0x03030303u);
+    d[i] = SL_BOP3(SL_BOP3(p0, p1, p2, kXor3), p3, 0u, kXor3);
   });
-  static_for<8>([&](auto p) { x[p] = acc[p]; });
 }
+__host__ __device__ inline tab4 mul_table(int lm) {  // lm < 0: the zero multiplier
+  if (lm < 0) return (tab4){0u, 0u, 0u, 0u};
+  return (tab4){kGf8.t[0][lm], kGf8.t[1][lm], kGf8.t[2][lm], kGf8.t[3][lm]};
+}
+
 }  // namespace sliced
 }  // namespace dagpu

@@ -229,8 +229,8 @@ extern "C" int sliced_dec_emu(long shard, uint8_t* shards, const uint8_t* presen
             uint32_t d[8];
             memcpy(d, src + col0, 16);
             memcpy(d + 4, src + col0 + 256, 16);
+            mul_packed(d, mul_table(present[shard_of(e)] ? (int)(err[e] & 0xFF) : -1));
             transpose8(d);
-            mul_lane(d, present[shard_of(e)] ? kDecPow.cp[err[e] & 0xFF] : 0u);
             memcpy(st[w][eb][j], d, 32);
           }
       for (int w = 0; w < 4; w++)
@@ -281,8 +281,8 @@ extern "C" int sliced_dec_emu(long shard, uint8_t* shards, const uint8_t* presen
             if (present[shard_of(e)]) continue;
             uint32_t d[8];
             memcpy(d, st[w][eb][j], 32);
-            mul_lane(d, kDecPow.cp[255u - (err[e] & 0xFF)]);
             transpose8(d);
+            mul_packed(d, mul_table((int)(255u - (err[e] & 0xFF))));
             uint8_t* dst = shards + (long)shard_of(e) * shard;
             memcpy(dst + col0, d, 16);
             memcpy(dst + col0 + 256, d + 4, 16);
