@@ -559,34 +559,39 @@ __host__ __device__ __forceinline__ void deriv_local(uint32_t (&v)[16][8]) {
 }
 
 // x * exp(lm) on PACKED bytes (before the bit transpose / after the inverse
-// one): tb = {t[0][lm], t[1][lm], t[2][lm], t[3][lm]} (gf_const.hpp: bytes
-// c * (v << 2g), v = 0..3), or all zero for a missing shard.  Per dword: four
-// 2-bit byte-table lookups (v_perm) and two xors, 13 ops for 4 bytes against
-// the earlier bit-plane power-basis multiply's ~136 for 32 bytes.
+// one), with the 3/3/2-bit byte tables of gf_const.hpp: tb = t8[lm][0..3]
+// (c * (0..7) as lo | hi, c * ((0..7) << 3) as lo | hi) and t2 = t8[lm][4]
+// (c * ((0..3) << 6)), all zero for a missing shard.  Per dword: three v_perm
+// lookups (an 8-byte pool each for the two 3-bit groups), five index ops and
+// one xor3 -- 9 ops for 4 bytes (72 per 32 bytes; the bit-plane power-basis
+// multiply took ~136, four 2-bit lookups 104).
 typedef unsigned int tab4 __attribute__((ext_vector_type(4)));
-__host__ __device__ __forceinline__ uint32_t perm4(uint32_t tab, uint32_t idx) {
+__host__ __device__ __forceinline__ uint32_t perm8v(uint32_t hi, uint32_t lo, uint32_t idx) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  return __builtin_amdgcn_perm(tab, tab, idx);
+  return __builtin_amdgcn_perm(hi, lo, idx);
 #else
   uint32_t r = 0;
-  for (int b = 0; b < 4; b++) r |= ((tab >> (8 * ((idx >> (8 * b)) & 3))) & 0xFFu) << (8 * b);
+  for (int b = 0; b < 4; b++) {
+    const uint32_t i = (idx >> (8 * b)) & 7u;
+    r |= (((i < 4 ? lo : hi) >> (8 * (i & 3))) & 0xFFu) << (8 * b);
+  }
   return r;
 #endif
 }
-__host__ __device__ __forceinline__ void mul_packed(uint32_t (&d)[8], const tab4 tb) {
+__host__ __device__ __forceinline__ void mul_packed(uint32_t (&d)[8], const tab4 tb, uint32_t t2) {
   static_for<8>([&](auto i) {
     const uint32_t y = d[i];
-    const uint32_t p0 = perm4(tb.x, y & 0x03030303u);
-    const uint32_t p1 = perm4(tb.y, (y >> 2) & 0x03030303u);
-    const uint32_t p2 = perm4(tb.z, (y >> 4) & 0x03030303u);
-    const uint32_t p3 = perm4(tb.w, (y >> 6) & 0x03030303u);
-    d[i] = SL_BOP3(SL_BOP3(p0, p1, p2, kXor3), p3, 0u, kXor3);
+    const uint32_t p0 = perm8v(tb.y, tb.x, y & 0x07070707u);
+    const uint32_t p1 = perm8v(tb.w, tb.z, (y >> 3) & 0x07070707u);
+    const uint32_t p2 = perm8v(t2, t2, (y >> 6) & 0x03030303u);
+    d[i] = SL_BOP3(p0, p1, p2, kXor3);
   });
 }
 __host__ __device__ inline tab4 mul_table(int lm) {  // lm < 0: the zero multiplier
   if (lm < 0) return (tab4){0u, 0u, 0u, 0u};
-  return (tab4){kGf8.t[0][lm], kGf8.t[1][lm], kGf8.t[2][lm], kGf8.t[3][lm]};
+  return (tab4){kGf8.t8[lm][0], kGf8.t8[lm][1], kGf8.t8[lm][2], kGf8.t8[lm][3]};
 }
+__host__ __device__ inline uint32_t mul_table2(int lm) { return lm < 0 ? 0u : kGf8.t8[lm][4]; }
 
 }  // namespace sliced
 }  // namespace dagpu

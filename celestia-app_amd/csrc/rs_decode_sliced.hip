@@ -20,8 +20,8 @@
 //   A*, A                     -- FFT layers 3..2, 1..0, postmultiply, store
 // Every op of the transform is a full-rate v_xor / v_bitop3 / shift; the
 // error-locator multiplies run on the packed bytes before the bit transpose and
-// after the inverse one (mul_packed: four v_perm 2-bit lookups per dword, fewer
-// ops than on the planes).  LDS: 64 KB, three workgroup passes (A*->B, derivative,
+// after the inverse one (mul_packed: three v_perm lookups of 3/3/2-bit tables per
+// dword, fewer ops than on the planes).  LDS: 64 KB, three workgroup passes (A*->B, derivative,
 // B->A*) and two wave-local ones (A<->A*), each in two halves of 4 planes;
 // the derivative's cross-lane and cross-wave terms (element bits 0..3 in B)
 // are read from the originals written to LDS, its register bits (4..7) are
@@ -135,12 +135,17 @@ void leo8_decode128_sliced_kernel(DecodeArgs a) {
   constexpr int K = 128;
   __shared__ u32x4 lds[256 * 16];  // 64 KB
   __shared__ tab4 mtab[257];       // packed-byte multiply tables per log value; [256] = zero
+  __shared__ uint32_t mtab2[257];
   const long blk = blockIdx.x;
   const long chunk = blk % a.nchunk;  // 512-B chunks
   const long v = blk / a.nchunk;      // flattened (square, vector)
   if (a.flags[v] == 0) return;        // uniform: nothing to decode for this vector
   mtab[threadIdx.x] = mul_table((int)threadIdx.x);
-  if (threadIdx.x == 0) mtab[256] = mul_table(-1);
+  mtab2[threadIdx.x] = mul_table2((int)threadIdx.x);
+  if (threadIdx.x == 0) {
+    mtab[256] = mul_table(-1);
+    mtab2[256] = 0u;
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -175,7 +180,8 @@ void leo8_decode128_sliced_kernel(DecodeArgs a) {
 #pragma unroll
   for (int j = 0; j < 16; j++) {
     // present: shard * exp(errLocs); missing: 0 -- on packed bytes, then planes
-    mul_packed(v_[j], mtab[((miss >> j) & 1) ? 256u : err_of(j)]);
+    const uint32_t ti = ((miss >> j) & 1) ? 256u : err_of(j);
+    mul_packed(v_[j], mtab[ti], mtab2[ti]);
     transpose8(v_[j]);
   }
   const uint32_t eb0mask = (eb & 1) ? 0xFFFFFFFFu : 0u, eb1mask = (eb & 2) ? 0xFFFFFFFFu : 0u;
@@ -199,7 +205,7 @@ void leo8_decode128_sliced_kernel(DecodeArgs a) {
     const bool m = (miss >> j) & 1;
     if (!__any(m)) continue;  // uniform: no lane of this wave lost element j
     transpose8(v_[j]);
-    mul_packed(v_[j], mtab[255u - err_of(j)]);
+    mul_packed(v_[j], mtab[255u - err_of(j)], mtab2[255u - err_of(j)]);
     if (m) {
       const uint32_t soff = (uint32_t)(shard0 + j) * sstride;
       __builtin_amdgcn_raw_buffer_store_b128((u32x4){v_[j][0], v_[j][1], v_[j][2], v_[j][3]}, rsrc, voff, soff, 0);

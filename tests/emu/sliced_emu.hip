@@ -229,7 +229,8 @@ extern "C" int sliced_dec_emu(long shard, uint8_t* shards, const uint8_t* presen
             uint32_t d[8];
             memcpy(d, src + col0, 16);
             memcpy(d + 4, src + col0 + 256, 16);
-            mul_packed(d, mul_table(present[shard_of(e)] ? (int)(err[e] & 0xFF) : -1));
+            const int lm = present[shard_of(e)] ? (int)(err[e] & 0xFF) : -1;
+            mul_packed(d, mul_table(lm), mul_table2(lm));
             transpose8(d);
             memcpy(st[w][eb][j], d, 32);
           }
@@ -282,7 +283,8 @@ extern "C" int sliced_dec_emu(long shard, uint8_t* shards, const uint8_t* presen
             uint32_t d[8];
             memcpy(d, st[w][eb][j], 32);
             transpose8(d);
-            mul_packed(d, mul_table((int)(255u - (err[e] & 0xFF))));
+            const int lm = (int)(255u - (err[e] & 0xFF));
+            mul_packed(d, mul_table(lm), mul_table2(lm));
             uint8_t* dst = shards + (long)shard_of(e) * shard;
             memcpy(dst + col0, d, 16);
             memcpy(dst + col0 + 256, d + 4, 16);
