@@ -251,7 +251,8 @@ def main():
     # up to the batch size if --distinct is smaller
     nd = min(args.distinct, B)
     host = synth.blob_squares(k, HEADLINE_SEED, rank * B, nd, threads=host_threads())
-    ds.load_ods(np.stack([host[i % nd] for i in range(B)]))
+    batch_ods = np.stack([host[i % nd] for i in range(B)])
+    ds.load_ods(batch_ods)
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream()
@@ -273,6 +274,9 @@ def main():
     barrier(dist)
     el = time.perf_counter() - t0
     el_max = max_over_ranks(dist, el, local)
+    # the timed batch proves its own output before anything else runs on it
+    headline_check = check_headline(dist, local, ctx, ds, batch_ods)
+    del batch_ods
 
     # ---- per-kernel times: a separate profiled pass (HIP events on the launch
     # stream around every kernel; the library runs the batch serially while
@@ -351,6 +355,8 @@ def main():
         "kernel_sum_ms_per_step": kernel_ms_step,
         "roofline": roof,
         "valu_issue": valu_issue(k, B, ms_step, per["nmt_leaves"]),
+        "headline_bit_exact": headline_check["bit_exact"],
+        "headline_check": headline_check,
     }
     # single-square latency first: after the replay's 64 GiB page-locked
     # allocation the same device->host copies ran slower (k=128 with the EDS
@@ -391,6 +397,33 @@ def main():
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def check_headline(dist, local, ctx, ds, batch_ods):
+    """Bit-exactness of the timed configuration itself (ODS in place or not,
+    the RS/NMT slice pipeline as the timed steps ran it): every DAH and every
+    row/column root of the last timed step against the drop-in host API
+    dagpu_extend_batch on the same host ODS (its own, unsliced kernel chain;
+    oracle-pinned in tests/test_gpu_parity.py).  Fatal on every rank on any
+    mismatch.  DAGPU_BENCH_CORRUPT=headline flips one byte to prove it fires."""
+    from celestia_da import da
+
+    torch.cuda.synchronize()
+    dah = ds.dah.cpu().numpy()
+    rr = ds.row_roots.cpu().numpy()
+    cr = ds.col_roots.cpu().numpy()
+    st = ds.status.cpu().numpy()
+    if os.environ.get("DAGPU_BENCH_CORRUPT") == "headline":
+        dah[len(dah) - 1, 7] ^= 0x10
+    n = ds.n
+    _, hrr, hcr, hdah, hst = da.extend_batch(batch_ods.reshape(-1), [ds.k] * n, ctx)
+    bad_dah = int((hdah != dah).any(axis=1).sum())
+    bad_roots = sum(int(not (np.array_equal(hrr[i], rr[i]) and np.array_equal(hcr[i], cr[i]))) for i in range(n))
+    ok = bad_dah == 0 and bad_roots == 0 and bool((st == 0).all()) and bool((hst == 0).all())
+    _fail(dist, not ok, local, f"headline bit-exact check ({bad_dah} DAHs, {bad_roots} root sets differ)")
+    return {"bit_exact": ok, "squares": n, "dah_mismatches": bad_dah, "root_mismatches": bad_roots,
+            "against": "dagpu_extend_batch (host API, unsliced) on the same host ODS",
+            "pipeline_slices": int(os.environ.get("DAGPU_PIPE_SLICES", "0")) or "default"}
 
 
 def bench_e2e(ctx, local, k, host_ods, steps, total=256):

@@ -54,7 +54,9 @@ EXPORTS = (
     "dagpu_decode",
     "dagpu_repair_workspace_size",
     "dagpu_repair_batch_device",
+    "dagpu_repair_batch_device_ex",
     "dagpu_repair",
+    "dagpu_repair_ex",
     "dagpu_profile_enable",
     "dagpu_profile_read",
     "dagpu_dah_hash",
@@ -136,6 +138,9 @@ def lib() -> ctypes.CDLL:
         L.dagpu_repair_workspace_size.argtypes = [ctypes.c_uint32, sz]
         L.dagpu_repair_workspace_size.restype = sz
         L.dagpu_repair.argtypes = [vp, ctypes.c_uint32, vp, vp, vp, vp]
+        L.dagpu_repair_ex.argtypes = [vp, ctypes.c_uint32, vp, vp, vp, vp, vp]
+        L.dagpu_repair_batch_device_ex.argtypes = [vp, ctypes.c_uint32, sz, vp, vp, vp, vp, vp, vp,
+                                                   vp, vp]
         L.dagpu_dah_hash.argtypes = [vp, vp, sz, vp]
         L.dagpu_nmt_roots.argtypes = [vp, sz, vp, vp, sz, ctypes.c_int, vp, ctypes.c_int, vp, vp]
         L.dagpu_wrapper_roots.argtypes = [vp, ctypes.c_uint64, sz, vp, vp, vp, sz, vp, vp]

@@ -46,7 +46,14 @@ class ErrInvalidPushOrder(DAError):
 
 
 class ErrByzantineData(DAError):
-    pass
+    """rsmt2d ErrByzantineData: axis ("row" / "col") and index of the failing
+    axis; rebuilt_axis / rebuilt_index name the row or column whose repair
+    failed (the same axis unless a newly completed orthogonal axis failed),
+    whose present shares are ErrByzantineData.Shares."""
+    axis = None
+    index = None
+    rebuilt_axis = None
+    rebuilt_index = None
 
 
 class ErrUnrepairableDataSquare(DAError):
@@ -428,21 +435,35 @@ class LeoRSCodec:
         return [buf[i].tobytes() for i in range(n)]
 
 
+AXIS_NAMES = ("row", "col")
+
+
 def repair(eds: np.ndarray, present: np.ndarray, row_roots, col_roots,
            ctx: Optional[Context] = None):
     """rsmt2d ExtendedDataSquare.Repair(rowRoots, colRoots) on the GPU.
 
     eds: (2k, 2k, 512) uint8 with arbitrary bytes in missing cells; present:
     (2k, 2k) bool.  Returns (repaired eds, present after repair).  Raises
-    ErrByzantineData, ErrUnrepairableDataSquare or DAError("bad root input")."""
+    ErrByzantineData (with .axis/.index/.rebuilt_axis/.rebuilt_index, and
+    .eds/.present as rsmt2d leaves the square), ErrUnrepairableDataSquare or
+    DAError("bad root input: <axis> <i> expected ... got ...")."""
     ctx = ctx or default_context()
     e = np.ascontiguousarray(eds, dtype=np.uint8).copy()
     w = e.shape[0]
     p = np.ascontiguousarray(present, dtype=np.uint8).reshape(w, w).copy()
     rr = np.ascontiguousarray(np.frombuffer(b"".join(bytes(r) for r in row_roots), np.uint8))
     cr = np.ascontiguousarray(np.frombuffer(b"".join(bytes(c) for c in col_roots), np.uint8))
-    rc = ctx._L.dagpu_repair(ctx.handle, w // 2, _abi.addr(e), _abi.addr(p), _abi.addr(rr), _abi.addr(cr))
-    ctx.check(rc)
+    byz = np.full(4, -1, np.int32)
+    rc = ctx._L.dagpu_repair_ex(ctx.handle, w // 2, _abi.addr(e), _abi.addr(p), _abi.addr(rr), _abi.addr(cr),
+                                _abi.addr(byz))
+    if rc != 0:
+        err = _ERR_CLASS.get(rc, DAError)(rc, ctx.last_error())
+        if isinstance(err, ErrByzantineData) and byz[0] >= 0:
+            err.axis, err.index = AXIS_NAMES[byz[0]], int(byz[1])
+            err.rebuilt_axis, err.rebuilt_index = AXIS_NAMES[byz[2]], int(byz[3])
+        err.byz = [int(x) for x in byz]
+        err.eds, err.present = e, p.astype(bool)
+        raise err
     return e, p.astype(bool)
 
 

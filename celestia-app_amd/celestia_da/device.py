@@ -95,12 +95,23 @@ class DeviceSquares:
             _stream_handle(stream)))
 
     def repair(self, present: torch.Tensor, status: torch.Tensor, workspace: torch.Tensor,
-               stream: Optional[torch.cuda.Stream] = None) -> None:
+               stream: Optional[torch.cuda.Stream] = None, byz: Optional[torch.Tensor] = None) -> None:
         """Device-resident rsmt2d Repair of self.eds against self.row/col_roots.
-        present: (n, (2k)^2) uint8, updated in place; status: (n,) int32."""
-        self._ck(self.ctx._L.dagpu_repair_batch_device(
+        present: (n, (2k)^2) uint8, updated in place; status: (n,) int32;
+        byz (optional): (n, 4) int32 on the device -> failing axis per square
+        (dagpu_repair_batch_device_ex)."""
+        L = self.ctx._L
+        if byz is None:
+            self._ck(L.dagpu_repair_batch_device(
+                self.ctx.handle, self.k, self.n, _abi.addr(self.eds), _abi.addr(present),
+                _abi.addr(self.row_roots), _abi.addr(self.col_roots), _abi.addr(status),
+                _abi.addr(workspace), _stream_handle(stream)))
+            return
+        if byz.dtype != torch.int32 or byz.numel() != 4 * self.n or byz.device != self.eds.device:
+            raise ValueError("byz must be an (n, 4) int32 tensor on this device")
+        self._ck(L.dagpu_repair_batch_device_ex(
             self.ctx.handle, self.k, self.n, _abi.addr(self.eds), _abi.addr(present),
-            _abi.addr(self.row_roots), _abi.addr(self.col_roots), _abi.addr(status),
+            _abi.addr(self.row_roots), _abi.addr(self.col_roots), _abi.addr(status), _abi.addr(byz),
             _abi.addr(workspace), _stream_handle(stream)))
 
     def repair_workspace(self) -> torch.Tensor:

@@ -271,13 +271,24 @@ int run_group_host(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* ods, uin
   // An EDS requested back goes down on the copy stream while the kernels run:
   // the top halves ([Q0|Q1], final after the row pass) during the column pass
   // and the NMT kernels, the bottom halves ([Q2|Q3]) during the NMT kernels.
+  // The whole kernel chain and the results download are queued on `s` BEFORE
+  // the EDS copies: a device->host copy into pageable caller memory runs
+  // synchronously on this thread, and must not hold back the NMT launches.
   rc = enqueue_rs(ctx, k, n, (const uint8_t*)ctx->ods.p, (uint8_t*)ctx->eds.p, s,
                   eds_out ? ctx->ev_loaded[0] : nullptr);
   if (rc) return rc;
-  hipStream_t cs = ctx->copy_stream;
-  const size_t eb = eds_bytes(k), half = eb / 2;
+  if (eds_out) HIP_TRY(ctx, hipEventRecord(ctx->ev_loaded[1], s));
+  rc = enqueue_roots(ctx, k, n, (const uint8_t*)ctx->eds.p, res.rr, res.cr, res.dah, res.st, ctx->ws.p, s);
+  if (rc) return rc;
+  HIP_TRY(ctx, res.download(ctx, s));
   if (eds_out) {
-    HIP_TRY(ctx, hipEventRecord(ctx->ev_loaded[1], s));
+    hipStream_t cs = ctx->copy_stream;
+    // from here on DMA may be writing into eds_out: every return path waits for it
+    struct CopyJoin {
+      hipStream_t cs;
+      ~CopyJoin() { (void)hipStreamSynchronize(cs); }
+    } join{cs};
+    const size_t eb = eds_bytes(k), half = eb / 2;
     HIP_TRY(ctx, hipStreamWaitEvent(cs, ctx->ev_loaded[0], 0));
     const uint8_t* d = (const uint8_t*)ctx->eds.p;
     for (size_t i = 0; i < n; i++)  // plain 1D copies: the DMA engines' fast path
@@ -286,11 +297,8 @@ int run_group_host(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* ods, uin
     for (size_t i = 0; i < n; i++)
       HIP_TRY(ctx, hipMemcpyAsync(eds_out + i * eb + half, d + i * eb + half, half,
                                   hipMemcpyDeviceToHost, cs));
+    HIP_TRY(ctx, hipStreamSynchronize(cs));
   }
-  rc = enqueue_roots(ctx, k, n, (const uint8_t*)ctx->eds.p, res.rr, res.cr, res.dah, res.st, ctx->ws.p, s);
-  if (rc) return rc;
-  HIP_TRY(ctx, res.download(ctx, s));
-  if (eds_out) HIP_TRY(ctx, hipStreamSynchronize(cs));
   HIP_TRY(ctx, hipStreamSynchronize(s));
   std::vector<int32_t> st(n);
   res.deliver(ctx, rr, cr, dah, st.data());
@@ -312,9 +320,9 @@ int dagpu_init(int device, dagpu_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return DAGPU_ERR_DEVICE;
   dagpu_ctx* c = new dagpu_ctx();
   c->device = device;
+  c->gen = next_ctx_gen();
   bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
-            hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) == hipSuccess &&
-            hipStreamCreateWithFlags(&c->rs_stream, hipStreamNonBlocking) == hipSuccess;
+            hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) == hipSuccess;
   for (int i = 0; ok && i < 2; i++)
     ok = hipEventCreateWithFlags(&c->ev_loaded[i], hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&c->ev_done[i], hipEventDisableTiming) == hipSuccess;
@@ -328,7 +336,7 @@ int dagpu_init(int device, dagpu_ctx** out) {
 
 void dagpu_destroy(dagpu_ctx* c) {
   if (!c) return;
-  if (thread_err().ctx == c) thread_err() = ThreadErr{};
+  if (thread_err().ctx == c && thread_err().gen == c->gen) thread_err() = ThreadErr{};
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
@@ -344,9 +352,9 @@ void dagpu_destroy(dagpu_ctx* c) {
     if (c->ev_loaded[i]) (void)hipEventDestroy(c->ev_loaded[i]);
     if (c->ev_done[i]) (void)hipEventDestroy(c->ev_done[i]);
   }
-  if (c->rs_stream) (void)hipStreamSynchronize(c->rs_stream);
+  for (auto& cs : c->side) (void)hipStreamSynchronize(cs.second);
   for (auto e : c->ev_pool) (void)hipEventDestroy(e);
-  if (c->rs_stream) (void)hipStreamDestroy(c->rs_stream);
+  for (auto& cs : c->side) (void)hipStreamDestroy(cs.second);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -377,9 +385,10 @@ int dagpu_host_unregister(void* p) {
 const char* dagpu_last_error(dagpu_ctx* c) {
   if (!c) return "null context";
   ThreadErr& t = thread_err();
-  if (t.ctx == c && t.own) return t.msg.c_str();
+  if (t.ctx == c && t.gen == c->gen && t.own) return t.msg.c_str();
   std::lock_guard<std::mutex> g(c->err_mu);
   t.ctx = c;
+  t.gen = c->gen;
   t.own = false;
   t.msg = c->err;
   return t.msg.c_str();
@@ -491,20 +500,39 @@ void ev_give(dagpu_ctx* c, hipEvent_t e) {
   c->ev_pool.push_back(e);
 }
 
+long env_long(const char* name) {
+  const char* e = getenv(name);
+  return e ? atol(e) : 0L;
+}
+
 // Slices of a device batch for the RS/NMT pipeline: RS of slice i+1.. runs on
-// ctx->rs_stream while the NMT kernels of slice i run on the caller's stream
+// a side stream while the NMT kernels of slice i run on the caller's stream
 // (bench: 256 squares at k = 128, 4 slices 11.98 -> 11.63 ms; tools/pipe_exp.py).
-// DAGPU_PIPE_SLICES overrides (1 = off).  Off while profiling, so that every
-// kernel's event bracket times that kernel alone.
+// DAGPU_PIPE_SLICES overrides (1 = off; read per call, so tests can vary it).
+// Off while profiling, so that every kernel's event bracket times that kernel alone.
 size_t pipe_slices(dagpu_ctx* ctx, uint32_t k, size_t n) {
-  static const long env = [] {
-    const char* e = getenv("DAGPU_PIPE_SLICES");
-    return e ? atol(e) : 0L;
-  }();
+  const long env = env_long("DAGPU_PIPE_SLICES");
   if (ctx->prof) return 1;
   size_t s = env > 0 ? (size_t)env : (k >= 128 && n >= 64 ? 4 : 1);
   while (s > 1 && n / s < 8) s >>= 1;
   return s < 1 ? 1 : s;
+}
+
+// The RS side stream paired with caller stream `s` (created on first use).
+hipStream_t side_stream(dagpu_ctx* ctx, hipStream_t s) {
+  std::lock_guard<std::mutex> g(ctx->side_mu);
+  for (auto& p : ctx->side)
+    if (p.first == s) return p.second;
+  if (ctx->side.size() >= dagpu_ctx::kMaxSideStreams) {
+    // more caller streams than side streams: share them round-robin (the
+    // callers then serialise their RS slices, results are unaffected)
+    const size_t i = (size_t)((((uint64_t)(uintptr_t)s) * 0x9E3779B97F4A7C15ull) >> 32) % ctx->side.size();
+    return ctx->side[i].second;
+  }
+  hipStream_t side = nullptr;
+  if (hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  ctx->side.emplace_back(s, side);
+  return side;
 }
 
 }  // namespace
@@ -524,7 +552,7 @@ int dagpu_extend_batch_device(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_
     if (rc) return rc;
     return enqueue_roots(ctx, k, n, d_eds, d_row_roots, d_col_roots, d_dah, d_status, d_workspace, s);
   }
-  // fork: rs_stream starts after the work already queued on the caller's stream
+  // fork: the side stream starts after the work already queued on the caller's stream
   std::vector<hipEvent_t> ev(S + 1, nullptr);
   for (auto& e : ev)
     if (!(e = ev_take(ctx))) {
@@ -535,17 +563,15 @@ int dagpu_extend_batch_device(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_
     for (auto x : ev) ev_give(ctx, x);
     return r;
   };
-  hipStream_t rs = ctx->rs_stream;
+  hipStream_t rs = side_stream(ctx, s);
+  if (!rs) return done(set_err(ctx, DAGPU_ERR_DEVICE, "hipStreamCreate failed"));
   const size_t w = 2 * (size_t)k;
   if (hipEventRecord(ev[S], s) != hipSuccess || hipStreamWaitEvent(rs, ev[S], 0) != hipSuccess)
     return done(set_err(ctx, DAGPU_ERR_DEVICE, "pipeline fork failed"));
   // slice boundaries: a smaller first slice shortens the RS run nothing overlaps
   std::vector<size_t> cut(S + 1);
   {
-    static const long first_env = [] {
-      const char* e = getenv("DAGPU_PIPE_FIRST");
-      return e ? atol(e) : 0L;
-    }();
+    const long first_env = env_long("DAGPU_PIPE_FIRST");
     size_t f = first_env > 0 ? (size_t)first_env : n / S;
     if (f < 1) f = 1;
     if (f > n - (S - 1)) f = n - (S - 1);
@@ -560,7 +586,7 @@ int dagpu_extend_batch_device(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_
     if (hipEventRecord(ev[i], rs) != hipSuccess) return done(set_err(ctx, DAGPU_ERR_DEVICE, "hipEventRecord failed"));
   }
   // the slices' NMT work runs in order on the caller's stream and shares the
-  // front of the workspace; waiting on the last slice's event also joins rs_stream
+  // front of the workspace; waiting on the last slice's event also joins the side stream
   for (size_t i = 0; i < S; i++) {
     const size_t a = cut[i], b = cut[i + 1];
     if (hipStreamWaitEvent(s, ev[i], 0) != hipSuccess)
@@ -691,11 +717,14 @@ struct RepairWs {
   uint8_t* p0;          // presence before repair
   int32_t* complete_before;
   int32_t* complete_now;
+  int32_t* root_bad;    // [axis][sq][idx]: complete-before axis whose root differs
+  int32_t* parity_bad;  // [axis][sq][idx]: complete-before axis whose parity != Encode(data)
   uint8_t* err_rows;
   uint8_t* err_cols;
   int32_t* flags_rows;
   int32_t* flags_cols;
   int32_t* err_share[2][2];  // [axis][same, head]
+  int32_t* sel;         // exact-order repair: level of each axis' attempt, [2][w]
   int32_t* bits;
   int32_t* counters;    // [0] decodable rows, [1] decodable cols
 };
@@ -707,9 +736,10 @@ size_t repair_ws_bytes(uint32_t k, size_t n) {
   size_t t = a256(nmt_workspace_bytes((int)k, (long)n));
   t += 2 * a256(n * w * kNodeSize) + a256(n * 32) + a256(n * 4);  // got roots, dah, nmt status
   t += a256(n * w * w);                                           // p0
-  t += 2 * a256(n * 2 * w * 4);                                   // complete before/now
+  t += 4 * a256(n * 2 * w * 4);                                   // complete before/now, root/parity bad
   t += 2 * a256(n * w * rs_err_bytes((int)k)) + 2 * a256(n * w * 4);  // err, flags
   t += 4 * a256(n * w * 4);                                             // err_same, err_head per axis
+  t += a256(2 * w * 4);                                                 // sel
   t += a256(n * 4) + 256;                                         // bits, counters
   return t;
 }
@@ -729,6 +759,8 @@ RepairWs carve_repair(uint32_t k, size_t n, void* base) {
   r.p0 = p; p += a256(n * w * w);
   r.complete_before = (int32_t*)p; p += a256(n * 2 * w * 4);
   r.complete_now = (int32_t*)p; p += a256(n * 2 * w * 4);
+  r.root_bad = (int32_t*)p; p += a256(n * 2 * w * 4);
+  r.parity_bad = (int32_t*)p; p += a256(n * 2 * w * 4);
   r.err_rows = p; p += a256(n * w * rs_err_bytes((int)k));
   r.err_cols = p; p += a256(n * w * rs_err_bytes((int)k));
   r.flags_rows = (int32_t*)p; p += a256(n * w * 4);
@@ -738,6 +770,7 @@ RepairWs carve_repair(uint32_t k, size_t n, void* base) {
       r.err_share[ax][j] = (int32_t*)p;
       p += a256(n * w * 4);
     }
+  r.sel = (int32_t*)p; p += a256(2 * w * 4);
   r.bits = (int32_t*)p; p += a256(n * 4);
   r.counters = (int32_t*)p;
   return r;
@@ -770,14 +803,182 @@ DecodeArgs axis_decode_args(uint32_t k, size_t n, uint8_t* eds, uint8_t* present
   return d;
 }
 
+extern "C++" {  // (this file's helpers sit inside the extern "C" block)
+// rsmt2d solveCrossword (v0.11.0) replayed on presence bitmaps alone: the
+// attempts in its sequential order (for each pass, i = 0..2k-1: row i, then
+// column i; an incomplete axis with >= k shares is rebuilt), each with the
+// orthogonal axes it completes (verified by rsmt2d right after the rebuild, in
+// ascending index), and a dependency level: an attempt reads the cells of its
+// own axis and of those orthogonal axes, so it must run after every earlier
+// attempt that filled one of them.  Attempts of one level touch disjoint
+// missing cells and run as one batched decode per orientation.
+struct CrossPlan {
+  std::vector<int> axis, idx, level;
+  std::vector<int> ortho_off, ortho;  // CSR: orthogonal axes completed by attempt j
+  std::vector<int32_t> att_level;     // [axis][w]: level of the axis' attempt, -1 = none
+  int nlevels = 0;
+  bool complete = false;              // the crossword fills the square
+};
+
+CrossPlan plan_crossword(int k, const uint8_t* p0) {
+  const int w = 2 * k;
+  CrossPlan pl;
+  pl.att_level.assign(2 * (size_t)w, -1);
+  std::vector<uint8_t> pres(p0, p0 + (size_t)w * w);
+  std::vector<int> miss[2] = {std::vector<int>(w, 0), std::vector<int>(w, 0)};
+  std::vector<int> lvl[2] = {std::vector<int>(w, -1), std::vector<int>(w, -1)};
+  long missing = 0;
+  for (int r = 0; r < w; r++)
+    for (int c = 0; c < w; c++)
+      if (!pres[(size_t)r * w + c]) { miss[0][r]++; miss[1][c]++; missing++; }
+  pl.ortho_off.push_back(0);
+  while (missing > 0) {
+    bool progress = false;
+    for (int i = 0; i < w; i++) {
+      for (int ax = 0; ax < 2; ax++) {
+        if (miss[ax][i] == 0 || w - miss[ax][i] < k) continue;
+        int L = lvl[ax][i];
+        const size_t o0 = pl.ortho.size();
+        for (int j = 0; j < w; j++) {
+          const size_t cell = ax == 0 ? (size_t)i * w + j : (size_t)j * w + i;
+          if (pres[cell]) continue;
+          if (miss[1 - ax][j] == 1) {  // this cell is the orthogonal axis' last gap
+            pl.ortho.push_back(j);
+            L = std::max(L, lvl[1 - ax][j]);
+          }
+        }
+        L += 1;
+        for (int j = 0; j < w; j++) {
+          const size_t cell = ax == 0 ? (size_t)i * w + j : (size_t)j * w + i;
+          if (pres[cell]) continue;
+          pres[cell] = 1;
+          miss[ax][i]--;
+          miss[1 - ax][j]--;
+          lvl[1 - ax][j] = std::max(lvl[1 - ax][j], L);
+          missing--;
+        }
+        lvl[ax][i] = std::max(lvl[ax][i], L);
+        (void)o0;
+        pl.axis.push_back(ax);
+        pl.idx.push_back(i);
+        pl.level.push_back(L);
+        pl.ortho_off.push_back((int)pl.ortho.size());
+        pl.att_level[(size_t)ax * w + i] = L;
+        pl.nlevels = std::max(pl.nlevels, L + 1);
+        progress = true;
+      }
+    }
+    if (!progress) break;
+  }
+  pl.complete = missing == 0;
+  return pl;
+}
+
+std::string go_bytes(const uint8_t* p, size_t n) {  // fmt %v of a []byte
+  std::string s = "[";
+  for (size_t i = 0; i < n; i++) {
+    if (i) s += ' ';
+    s += std::to_string(p[i]);
+  }
+  return s + "]";
+}
+
+}  // extern "C++"
+
+// Square `sq` of a batch whose parallel crossword found a rebuilt axis with the
+// wrong root: rerun it in rsmt2d's sequential order to name the axis rsmt2d
+// reports.  Every rebuild that verifies restores committed bytes, so up to the
+// first failing attempt the batched level order fills exactly the cells
+// rsmt2d's order fills, with the same bytes; an attempt's result is final once
+// its axis (and the orthogonal axes it completes) are full, so one root pass at
+// the end decides every attempt.  Leaves present[] as rsmt2d leaves it (cells
+// of the attempts before the failing one) and byz[4] = {axis, index, rebuilt
+// axis, rebuilt index}.  Synchronises `s`.
+int exact_repair(dagpu_ctx* ctx, uint32_t k, size_t n, size_t sq, uint8_t* d_eds, uint8_t* d_present,
+                 const uint8_t* d_rr, const uint8_t* d_cr, int32_t* d_byz, const RepairWs& r,
+                 hipStream_t s) {
+  const size_t w = 2 * (size_t)k;
+  uint8_t* eds = d_eds + sq * eds_bytes(k);
+  uint8_t* pres = d_present + sq * w * w;
+  std::vector<uint8_t> p0(w * w);
+  HIP_TRY(ctx, hipMemcpyAsync(p0.data(), r.p0 + sq * w * w, w * w, hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipStreamSynchronize(s));
+  const CrossPlan pl = plan_crossword((int)k, p0.data());
+  HIP_TRY(ctx, hipMemcpyAsync(pres, r.p0 + sq * w * w, w * w, hipMemcpyDeviceToDevice, s));
+  HIP_TRY(ctx, hipMemcpyAsync(r.sel, pl.att_level.data(), 2 * w * 4, hipMemcpyHostToDevice, s));
+  std::vector<uint8_t> has(2 * (size_t)pl.nlevels, 0);
+  for (size_t j = 0; j < pl.axis.size(); j++) has[2 * (size_t)pl.level[j] + pl.axis[j]] = 1;
+  for (int L = 0; L < pl.nlevels; L++) {
+    for (int ax = 0; ax < 2; ax++) {
+      if (!has[2 * (size_t)L + ax]) continue;
+      DecodeArgs d = axis_decode_args(k, 1, eds, pres, ax, r);
+      d.err_same = d.err_head = nullptr;
+      d.ndecodable = nullptr;
+      d.sel_level = r.sel + (size_t)ax * w;
+      d.sel_value = L;
+      HIP_TRY(ctx, launch_rs_errlocs(d, s));
+      HIP_TRY(ctx, launch_rs_decode_only(d, s, true));
+    }
+  }
+  int rc = enqueue_roots(ctx, k, 1, eds, r.sa.row_roots, r.sa.col_roots, r.sa.dah, r.sa.status, r.sa.digests, s);
+  if (rc) return rc;
+  std::vector<uint8_t> got(2 * w * kNodeSize), want(2 * w * kNodeSize);
+  HIP_TRY(ctx, hipMemcpyAsync(got.data(), r.sa.row_roots, w * kNodeSize, hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipMemcpyAsync(got.data() + w * kNodeSize, r.sa.col_roots, w * kNodeSize, hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipMemcpyAsync(want.data(), d_rr + sq * w * kNodeSize, w * kNodeSize, hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipMemcpyAsync(want.data() + w * kNodeSize, d_cr + sq * w * kNodeSize, w * kNodeSize,
+                              hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipStreamSynchronize(s));
+  auto bad = [&](int ax, int i) {
+    const size_t off = ((size_t)ax * w + i) * kNodeSize;
+    return memcmp(got.data() + off, want.data() + off, kNodeSize) != 0;
+  };
+  int32_t byz[4] = {-1, -1, -1, -1};
+  size_t fail = pl.axis.size();
+  for (size_t j = 0; j < pl.axis.size() && fail == pl.axis.size(); j++) {
+    const int ax = pl.axis[j], i = pl.idx[j];
+    if (bad(ax, i)) {
+      byz[0] = byz[2] = ax;
+      byz[1] = byz[3] = i;
+      fail = j;
+      break;
+    }
+    for (int o = pl.ortho_off[j]; o < pl.ortho_off[j + 1]; o++)
+      if (bad(1 - ax, pl.ortho[o])) {
+        byz[0] = 1 - ax;
+        byz[1] = pl.ortho[o];
+        byz[2] = ax;
+        byz[3] = i;
+        fail = j;
+        break;
+      }
+  }
+  if (fail < pl.axis.size()) {  // presence as rsmt2d leaves it: attempts before the failing one
+    std::vector<uint8_t> p = p0;
+    for (size_t j = 0; j < fail; j++)
+      for (size_t t = 0; t < w; t++) {
+        const size_t cell = pl.axis[j] == 0 ? (size_t)pl.idx[j] * w + t : t * w + pl.idx[j];
+        p[cell] = 1;
+      }
+    HIP_TRY(ctx, hipMemcpyAsync(pres, p.data(), w * w, hipMemcpyHostToDevice, s));
+  }
+  HIP_TRY(ctx, hipMemcpyAsync(d_byz + 4 * sq, byz, sizeof byz, hipMemcpyHostToDevice, s));
+  HIP_TRY(ctx, hipStreamSynchronize(s));
+  (void)n;
+  return DAGPU_OK;
+}
+
 // rsmt2d Repair for n same-k squares resident on the device (see repair.hip).
+// d_byz (optional, n * 4 int32): failing axis per square; asking for it makes
+// the call resolve crossword failures in rsmt2d's order (exact_repair).
 int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t* d_present,
-                  const uint8_t* d_rr, const uint8_t* d_cr, int32_t* d_status, void* d_ws,
+                  const uint8_t* d_rr, const uint8_t* d_cr, int32_t* d_status, int32_t* d_byz, void* d_ws,
                   hipStream_t s) {
   const long w = 2L * k;
   RepairWs r = carve_repair(k, n, d_ws);
   HIP_TRY(ctx, hipMemcpyAsync(r.p0, d_present, n * w * w, hipMemcpyDeviceToDevice, s));
   HIP_TRY(ctx, hipMemsetAsync(r.bits, 0, n * sizeof(int32_t), s));
+  HIP_TRY(ctx, hipMemsetAsync(r.parity_bad, 0, n * 2 * w * sizeof(int32_t), s));
   HIP_TRY(ctx, launch_axis_complete(d_present, (int)k, (long)n, r.complete_before, s));
   // prerepairSanityCheck: complete axes must satisfy parity == Encode(data)
   for (int axis = 0; axis < 2; axis++) {
@@ -795,7 +996,8 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
     e.nsq = (long)n; e.nvec = w; e.nchunk = 1; e.shard_bytes = kSS;
     e.vec_flags = r.complete_before + (long)axis * n * w;
     e.mismatch = r.bits;
-    e.mismatch_bit = kRepPreByz;
+    e.mismatch_bit = 0;
+    e.mismatch_vec = r.parity_bad + (long)axis * n * w;
     HIP_TRY(ctx, launch_rs_encode((int)k, e, s));
   }
   // solveCrossword: each round rebuilds every decodable row or every decodable
@@ -822,8 +1024,20 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
                          r.sa.digests, s);
   if (rc) return rc;
   HIP_TRY(ctx, launch_verify_roots(d_rr, d_cr, r.sa.row_roots, r.sa.col_roots, r.complete_now,
-                                   r.complete_before, (int)k, (long)n, r.bits, s));
-  HIP_TRY(ctx, launch_finalize_repair(r.bits, (long)n, d_status, s));
+                                   r.complete_before, (int)k, (long)n, r.bits, r.root_bad, s));
+  HIP_TRY(ctx, launch_finalize_repair(r.bits, r.complete_before, r.root_bad, r.parity_bad, (int)k, (long)n,
+                                      d_status, d_byz, s));
+  if (!d_byz) return DAGPU_OK;
+  // crossword failures: name the axis in rsmt2d's order (rare; synchronises)
+  std::vector<int32_t> st(n), bz(4 * n);
+  HIP_TRY(ctx, hipMemcpyAsync(st.data(), d_status, n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipMemcpyAsync(bz.data(), d_byz, 4 * n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipStreamSynchronize(s));
+  for (size_t i = 0; i < n; i++) {
+    if (st[i] != DAGPU_ERR_BYZANTINE || bz[4 * i] >= 0) continue;
+    rc = exact_repair(ctx, k, n, i, d_eds, d_present, d_rr, d_cr, d_byz, r, s);
+    if (rc) return rc;
+  }
   return DAGPU_OK;
 }
 
@@ -834,24 +1048,33 @@ size_t dagpu_repair_workspace_size(uint32_t k, size_t n) {
   return repair_ws_bytes(k, n) + 256;
 }
 
-int dagpu_repair_batch_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds,
-                              uint8_t* d_present, const uint8_t* d_row_roots,
-                              const uint8_t* d_col_roots, int32_t* d_status, void* d_workspace,
-                              void* stream) {
+int dagpu_repair_batch_device_ex(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds,
+                                 uint8_t* d_present, const uint8_t* d_row_roots,
+                                 const uint8_t* d_col_roots, int32_t* d_status, int32_t* d_byz,
+                                 void* d_workspace, void* stream) {
   if (!ctx || !d_eds || !d_present || !d_row_roots || !d_col_roots || !d_status || !d_workspace)
     return DAGPU_ERR_ARG;
   int rc = check_k(ctx, k);
   if (rc) return rc;
   if (n == 0) return DAGPU_OK;
-  return repair_device(ctx, k, n, d_eds, d_present, d_row_roots, d_col_roots, d_status, d_workspace,
+  return repair_device(ctx, k, n, d_eds, d_present, d_row_roots, d_col_roots, d_status, d_byz, d_workspace,
                        (hipStream_t)stream);
 }
 
-int dagpu_repair(dagpu_ctx* ctx, uint32_t k, uint8_t* eds, uint8_t* present,
-                 const uint8_t* row_roots, const uint8_t* col_roots) {
+int dagpu_repair_batch_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds,
+                              uint8_t* d_present, const uint8_t* d_row_roots,
+                              const uint8_t* d_col_roots, int32_t* d_status, void* d_workspace,
+                              void* stream) {
+  return dagpu_repair_batch_device_ex(ctx, k, n, d_eds, d_present, d_row_roots, d_col_roots, d_status,
+                                      nullptr, d_workspace, stream);
+}
+
+int dagpu_repair_ex(dagpu_ctx* ctx, uint32_t k, uint8_t* eds, uint8_t* present,
+                    const uint8_t* row_roots, const uint8_t* col_roots, int32_t* byz) {
   if (!ctx || !eds || !present || !row_roots || !col_roots) return DAGPU_ERR_ARG;
   std::lock_guard<std::mutex> g(ctx->mu);
   (void)hipSetDevice(ctx->device);
+  if (byz) byz[0] = byz[1] = byz[2] = byz[3] = -1;
   int rc = check_k(ctx, k);
   if (rc) return rc;
   const size_t w = 2 * (size_t)k;
@@ -860,27 +1083,47 @@ int dagpu_repair(dagpu_ctx* ctx, uint32_t k, uint8_t* eds, uint8_t* present,
   HIP_TRY(ctx, ctx->ods.ensure(w * w));
   HIP_TRY(ctx, ctx->rr.ensure(w * kNodeSize));
   HIP_TRY(ctx, ctx->cr.ensure(w * kNodeSize));
-  HIP_TRY(ctx, ctx->status.ensure(sizeof(int32_t)));
+  HIP_TRY(ctx, ctx->status.ensure(5 * sizeof(int32_t)));
   HIP_TRY(ctx, ctx->ws.ensure(dagpu_repair_workspace_size(k, 1)));
   HIP_TRY(ctx, hipMemcpyAsync(ctx->eds.p, eds, eds_bytes(k), hipMemcpyHostToDevice, s));
   HIP_TRY(ctx, hipMemcpyAsync(ctx->ods.p, present, w * w, hipMemcpyHostToDevice, s));
   HIP_TRY(ctx, hipMemcpyAsync(ctx->rr.p, row_roots, w * kNodeSize, hipMemcpyHostToDevice, s));
   HIP_TRY(ctx, hipMemcpyAsync(ctx->cr.p, col_roots, w * kNodeSize, hipMemcpyHostToDevice, s));
+  int32_t* d_st = (int32_t*)ctx->status.p;
   rc = repair_device(ctx, k, 1, (uint8_t*)ctx->eds.p, (uint8_t*)ctx->ods.p, (const uint8_t*)ctx->rr.p,
-                     (const uint8_t*)ctx->cr.p, (int32_t*)ctx->status.p, ctx->ws.p, s);
+                     (const uint8_t*)ctx->cr.p, d_st, d_st + 1, ctx->ws.p, s);
   if (rc) return rc;
-  int32_t st = 0;
-  HIP_TRY(ctx, hipMemcpyAsync(&st, ctx->status.p, sizeof st, hipMemcpyDeviceToHost, s));
+  int32_t st[5] = {0, -1, -1, -1, -1};
+  HIP_TRY(ctx, hipMemcpyAsync(st, d_st, sizeof st, hipMemcpyDeviceToHost, s));
   HIP_TRY(ctx, hipMemcpyAsync(eds, ctx->eds.p, eds_bytes(k), hipMemcpyDeviceToHost, s));
   HIP_TRY(ctx, hipMemcpyAsync(present, ctx->ods.p, w * w, hipMemcpyDeviceToHost, s));
   HIP_TRY(ctx, hipStreamSynchronize(s));
-  switch (st) {
+  if (byz) memcpy(byz, st + 1, 4 * sizeof(int32_t));
+  const char* axn = st[1] == 1 ? "col" : "row";
+  switch (st[0]) {
     case DAGPU_OK: return DAGPU_OK;
-    case DAGPU_ERR_BAD_ROOTS: return set_err(ctx, st, "bad root input");
-    case DAGPU_ERR_BYZANTINE: return set_err(ctx, st, "byzantine data");
-    case DAGPU_ERR_UNREPAIRABLE: return set_err(ctx, st, "failed to solve data square");
-    default: return set_err(ctx, st, "repair failed");
+    case DAGPU_ERR_BAD_ROOTS: {
+      // "bad root input: row %d expected %v got %v" (prerepairSanityCheck)
+      const RepairWs r = carve_repair(k, 1, ctx->ws.p);
+      std::vector<uint8_t> got(kNodeSize);
+      const uint8_t* src = (st[1] == 1 ? r.sa.col_roots : r.sa.row_roots) + (size_t)st[2] * kNodeSize;
+      HIP_TRY(ctx, hipMemcpy(got.data(), src, kNodeSize, hipMemcpyDeviceToHost));
+      const uint8_t* want = (st[1] == 1 ? col_roots : row_roots) + (size_t)st[2] * kNodeSize;
+      return set_err(ctx, st[0], std::string("bad root input: ") + axn + " " + std::to_string(st[2]) +
+                                     " expected " + go_bytes(want, kNodeSize) + " got " +
+                                     go_bytes(got.data(), kNodeSize));
+    }
+    case DAGPU_ERR_BYZANTINE:  // ErrByzantineData.Error(): "byzantine %s: %d"
+      return set_err(ctx, st[0], st[1] >= 0 ? std::string("byzantine ") + axn + ": " + std::to_string(st[2])
+                                            : std::string("byzantine data"));
+    case DAGPU_ERR_UNREPAIRABLE: return set_err(ctx, st[0], "failed to solve data square");
+    default: return set_err(ctx, st[0], "repair failed");
   }
+}
+
+int dagpu_repair(dagpu_ctx* ctx, uint32_t k, uint8_t* eds, uint8_t* present,
+                 const uint8_t* row_roots, const uint8_t* col_roots) {
+  return dagpu_repair_ex(ctx, k, eds, present, row_roots, col_roots, nullptr);
 }
 
 int dagpu_profile_enable(dagpu_ctx* ctx, int on) {

@@ -36,6 +36,7 @@ struct EncodeArgs {
   const int32_t* vec_flags;
   int32_t* mismatch;
   int mismatch_bit;
+  int32_t* mismatch_vec;  // optional: mismatch_vec[square * nvec + vec] = 1 on a difference
 };
 
 hipError_t launch_leo8_encode(int k, const EncodeArgs& a, hipStream_t s);
@@ -64,9 +65,18 @@ struct DecodeArgs {
   // v uses.  Both nsq * nvec int32 of workspace; NULL = one computation per vector.
   int32_t* err_same;
   int32_t* err_head;
+  // Optional vector selection (exact-order Repair, dagpu.cpp): only vectors v
+  // with sel_level[v] == sel_value are decodable in this pass.  Requires
+  // err_same/err_head = NULL (an unselected run head computes no locators).
+  const int32_t* sel_level;
+  int sel_value;
   long nsq, nvec, nchunk, shard_bytes;
   int k;
 };
+
+__device__ __forceinline__ bool vec_selected(const DecodeArgs& a, long v) {
+  return !a.sel_level || a.sel_level[v] == a.sel_value;
+}
 
 // vector whose error locators vector v uses
 __device__ __forceinline__ long err_vec(const DecodeArgs& a, long v) { return a.err_head ? a.err_head[v] : v; }
@@ -91,17 +101,25 @@ hipError_t launch_rs_decode_only(const DecodeArgs& a, hipStream_t s, bool mark_p
 hipError_t launch_rs_decode(const DecodeArgs& a, hipStream_t s, bool mark_present);
 
 // Repair helpers (repair.hip).  Status bits per square:
-constexpr int kRepPreByz = 1;      // complete axis whose parity != Encode(data)
-constexpr int kRepBadRoots = 2;    // axis complete before repair, root mismatch
 constexpr int kRepByz = 4;         // rebuilt axis, root mismatch
 constexpr int kRepIncomplete = 8;  // crossword could not finish
-// complete[sq*2w + axis*w + idx] = axis fully present
+// Axis arrays (complete, root_bad, parity_bad) are [axis][square][idx].
+// complete[axis*nsq*w + sq*w + idx] = axis fully present
 hipError_t launch_axis_complete(const uint8_t* present, int k, long nsq, int32_t* complete, hipStream_t s);
+// root_bad[a] = 1 for an axis complete before the repair whose root differs
+// (pre-repair "bad root input"); a rebuilt axis whose root differs ORs kRepByz
+// into bits[sq]; an incomplete axis ORs kRepIncomplete
 hipError_t launch_verify_roots(const uint8_t* exp_rr, const uint8_t* exp_cr, const uint8_t* got_rr,
                                const uint8_t* got_cr, const int32_t* complete_now,
                                const int32_t* complete_before, int k, long nsq, int32_t* bits,
-                               hipStream_t s);
-hipError_t launch_finalize_repair(const int32_t* bits, long nsq, int32_t* status, hipStream_t s);
+                               int32_t* root_bad, hipStream_t s);
+// status[sq] and (optional) byz[sq*4 .. +3] = {axis, index, rebuilt axis,
+// rebuilt index} (-1 = none / not known): the first pre-repair failure in the
+// order i = 0..2k-1 x {row root, col root, row parity, col parity}, else a
+// crossword failure (kRepByz, axis resolved by the host), else unrepairable
+hipError_t launch_finalize_repair(const int32_t* bits, const int32_t* complete_before, const int32_t* root_bad,
+                                  const int32_t* parity_bad, int k, long nsq, int32_t* status, int32_t* byz,
+                                  hipStream_t s);
 
 struct SquareArgs {
   const uint8_t* eds;   // nsq squares, each (2k)^2 * 512 B, row-major

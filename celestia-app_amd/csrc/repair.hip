@@ -55,13 +55,14 @@ __global__ __launch_bounds__(256) void verify_roots_kernel(const uint8_t* exp_rr
                                                            const uint8_t* got_rr, const uint8_t* got_cr,
                                                            const int32_t* complete_now,
                                                            const int32_t* complete_before, int k,
-                                                           long nsq, int32_t* bits) {
+                                                           long nsq, int32_t* bits, int32_t* root_bad) {
   const long a = (long)blockIdx.x * 256 + threadIdx.x;
   const int w = 2 * k;
   if (a >= nsq * 2L * w) return;
   long sq;
   int axis, idx;
   axis_of(a, w, nsq, sq, axis, idx);
+  root_bad[a] = 0;
   if (!complete_now[a]) {
     atomicOr(&bits[sq], kRepIncomplete);
     return;
@@ -72,38 +73,78 @@ __global__ __launch_bounds__(256) void verify_roots_kernel(const uint8_t* exp_rr
   uint32_t diff = 0;
 #pragma unroll
   for (int h = 0; h < kNodeSize / 2; h++) diff |= (uint32_t)(e16[h] ^ g16[h]);
-  if (diff) atomicOr(&bits[sq], complete_before[a] ? kRepBadRoots : kRepByz);
+  if (!diff) return;
+  if (complete_before[a]) root_bad[a] = 1;  // untouched by the crossword: pre-repair check
+  else atomicOr(&bits[sq], kRepByz);
 }
 
 hipError_t launch_verify_roots(const uint8_t* exp_rr, const uint8_t* exp_cr, const uint8_t* got_rr,
                                const uint8_t* got_cr, const int32_t* complete_now,
                                const int32_t* complete_before, int k, long nsq, int32_t* bits,
-                               hipStream_t s) {
+                               int32_t* root_bad, hipStream_t s) {
   const long n = nsq * 4L * k;
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(verify_roots_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, exp_rr,
-                     exp_cr, got_rr, got_cr, complete_now, complete_before, k, nsq, bits);
+                     exp_cr, got_rr, got_cr, complete_now, complete_before, k, nsq, bits, root_bad);
   return hipGetLastError();
 }
 
-// precedence follows the reference's order of checks: the pre-repair sanity
-// check first, then rebuilt-axis verification, then "no progress".
-__global__ void finalize_repair_kernel(const int32_t* bits, long nsq, int32_t* status) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= nsq) return;
-  const int b = bits[i];
-  int st = DAGPU_OK;
-  if (b & kRepBadRoots) st = DAGPU_ERR_BAD_ROOTS;
-  else if (b & kRepPreByz) st = DAGPU_ERR_BYZANTINE;
-  else if (b & kRepByz) st = DAGPU_ERR_BYZANTINE;
-  else if (b & kRepIncomplete) st = DAGPU_ERR_UNREPAIRABLE;
-  status[i] = st;
+// One workgroup per square.  prerepairSanityCheck first: rsmt2d v0.11.0 runs
+// its per-axis checks concurrently (errgroup) and returns whichever fails
+// first in time; here the first in launch order wins -- for i = 0..2k-1: row i
+// root, col i root, row i parity, col i parity (key = 4i + check) -- which the
+// oracle (orc_repair) follows too.  A root failure is "bad root input: <axis>
+// <i>", a parity failure ErrByzantineData{axis, i, that axis' shares}.  Then
+// the crossword: a failing rebuilt axis (kRepByz) is ErrByzantineData whose
+// axis and index the host resolves in rsmt2d's sequential order (dagpu.cpp
+// exact_repair); then "no progress" (ErrUnrepairableDataSquare).
+__global__ __launch_bounds__(256) void finalize_repair_kernel(const int32_t* bits, const int32_t* complete_before,
+                                                              const int32_t* root_bad, const int32_t* parity_bad,
+                                                              int k, long nsq, int32_t* status, int32_t* byz) {
+  __shared__ int key_s;
+  const long sq = blockIdx.x;
+  const int w = 2 * k;
+  if (threadIdx.x == 0) key_s = 0x7fffffff;
+  __syncthreads();
+  int key = 0x7fffffff;
+  for (int i = threadIdx.x; i < w; i += 256) {
+    const long r = sq * w + i, c = (nsq + sq) * w + i;  // [axis][square][idx]
+    int kk = 0x7fffffff;
+    if (complete_before[c] && parity_bad[c]) kk = 4 * i + 3;
+    if (complete_before[r] && parity_bad[r]) kk = 4 * i + 2;
+    if (root_bad[c]) kk = 4 * i + 1;
+    if (root_bad[r]) kk = 4 * i;
+    key = key < kk ? key : kk;
+  }
+  atomicMin(&key_s, key);
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const int b = bits[sq];
+  int st = DAGPU_OK, ax = -1, ix = -1;
+  if (key_s != 0x7fffffff) {
+    st = (key_s & 3) < 2 ? DAGPU_ERR_BAD_ROOTS : DAGPU_ERR_BYZANTINE;
+    ax = key_s & 1;
+    ix = key_s >> 2;
+  } else if (b & kRepByz) {
+    st = DAGPU_ERR_BYZANTINE;
+  } else if (b & kRepIncomplete) {
+    st = DAGPU_ERR_UNREPAIRABLE;
+  }
+  status[sq] = st;
+  if (byz) {
+    byz[4 * sq + 0] = ax;
+    byz[4 * sq + 1] = ix;
+    byz[4 * sq + 2] = ax;
+    byz[4 * sq + 3] = ix;
+  }
 }
 
-hipError_t launch_finalize_repair(const int32_t* bits, long nsq, int32_t* status, hipStream_t s) {
+hipError_t launch_finalize_repair(const int32_t* bits, const int32_t* complete_before, const int32_t* root_bad,
+                                  const int32_t* parity_bad, int k, long nsq, int32_t* status, int32_t* byz,
+                                  hipStream_t s) {
   if (nsq <= 0) return hipSuccess;
-  hipLaunchKernelGGL(finalize_repair_kernel, dim3((unsigned)((nsq + 255) / 256)), dim3(256), 0, s, bits,
-                     nsq, status);
+  hipLaunchKernelGGL(finalize_repair_kernel, dim3((unsigned)nsq), dim3(256), 0, s, bits, complete_before,
+                     root_bad, parity_bad, k, nsq, status, byz);
   return hipGetLastError();
 }
 

@@ -94,7 +94,7 @@ __global__ __launch_bounds__(64 * kErrVecs) void leo8_errlocs_kernel(DecodeArgs 
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);  // present shards
-    const bool decode = cnt >= k && cnt < n;
+    const bool decode = cnt >= k && cnt < n && vec_selected(a, v);
     if (lane == 0) {
       a.flags[v] = decode ? 1 : 0;
       if (cnt < k && a.too_few) atomicOr(a.too_few, 1);

@@ -195,8 +195,10 @@ __global__ __launch_bounds__(kThreads16) void leo16_encode_kernel(EncodeArgs a, 
       dst[q + 8] = hi;
     }
   }
-  if (a.mismatch && __builtin_amdgcn_ballot_w64(diff) != 0 && (threadIdx.x & 63) == 0)
+  if (a.mismatch && __builtin_amdgcn_ballot_w64(diff) != 0 && (threadIdx.x & 63) == 0) {
     atomicOr(a.mismatch + sq, a.mismatch_bit);
+    if (a.mismatch_vec) a.mismatch_vec[sq * a.nvec + vec] = 1;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -247,7 +249,7 @@ __global__ __launch_bounds__(kErrThreads) void leo16_errlocs_kernel(DecodeArgs a
   atomicAdd(&cnt_s, cnt);
   __syncthreads();
   const int present = cnt_s;
-  const bool decode = present >= k && present < n;
+  const bool decode = present >= k && present < n && vec_selected(a, v);
   if (threadIdx.x == 0) {
     a.flags[v] = decode ? 1 : 0;
     if (present < k && a.too_few) atomicOr(a.too_few, 1);
@@ -566,7 +568,10 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(3, 8))) void 
       diff |= w.lo[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, col, so, 0);
       diff |= w.hi[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, col + 32u, so, 0);
     }
-    if (diff) atomicOr(&a.mismatch[sq], a.mismatch_bit);
+    if (diff) {
+      atomicOr(&a.mismatch[sq], a.mismatch_bit);
+      if (a.mismatch_vec) a.mismatch_vec[sq * a.nvec + vec] = 1;
+    }
     return;
   }
 #pragma unroll
@@ -1149,31 +1154,61 @@ hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mar
 // Error-locator sharing.  err_same[v] = vector v's erasure pattern (its 2k
 // presence flags) equals vector v - 1's; err_head[v] = the last u <= v of v's
 // square whose pattern differs from u - 1's (a run never crosses a square),
-// whose locators v then uses.  One workgroup per square: its 16 waves compare
-// neighbouring vectors (64 lanes over the 2k flags, one ballot per vector),
-// then a prefix max of (same ? -1 : index) in LDS (Hillis-Steele, nvec <= 1024).
-// One launch per axis instead of one workgroup per vector plus a scan launch.
-__global__ __launch_bounds__(1024) void errloc_runs_kernel(DecodeArgs a) {
+// whose locators v then uses.
+//
+// Two launches: the neighbour compare over a grid of (square, vector) blocks,
+// so a few large squares (k = 512 Repair: 2 squares x 1024 vectors x 1024
+// flags per axis) still fill the chip, then one scan workgroup per square.
+// (Round 2 ran both in one workgroup per square: at 2 squares that was 2 of
+// 256 CUs walking 1 M strided flags per axis and round, 182 -> 137 squares/s.)
+// Flag layouts: p_shard_stride == 1 (row axis, codec API): one wave per
+// vector, lanes over its contiguous flags; otherwise (column axis, where
+// adjacent vectors are adjacent bytes) one lane per vector, the 2k flags split
+// over the 16 waves of the block and OR-ed in LDS.
+__global__ __launch_bounds__(1024) void errloc_same_rows_kernel(DecodeArgs a) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long gv = (long)blockIdx.x * 16 + wave;  // wave-uniform
+  if (gv >= a.nsq * a.nvec) return;
+  const long sq = gv / a.nvec;
+  const long v = gv - sq * a.nvec;
+  bool diff = v == 0;  // the first vector of a square starts a run
+  if (v > 0) {
+    const uint8_t* pv = a.present + sq * a.p_sq_stride + v * a.p_vec_stride;
+    const uint8_t* pu = pv - a.p_vec_stride;
+    for (int i = lane; i < 2 * a.k; i += 64) diff |= (pv[i] != 0) != (pu[i] != 0);
+  }
+  const bool any = __builtin_amdgcn_ballot_w64(diff) != 0;
+  if (lane == 0) a.err_same[gv] = any ? 0 : 1;
+}
+
+__global__ __launch_bounds__(1024) void errloc_same_cols_kernel(DecodeArgs a) {
+  __shared__ int32_t acc[64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long nb = (a.nvec + 63) / 64;
+  const long sq = blockIdx.x / nb;
+  const long v = (blockIdx.x - sq * nb) * 64 + lane;
+  if (threadIdx.x < 64) acc[threadIdx.x] = 0;
+  __syncthreads();
+  if (v > 0 && v < a.nvec) {
+    const uint8_t* pv = a.present + sq * a.p_sq_stride + v * a.p_vec_stride;
+    const uint8_t* pu = pv - a.p_vec_stride;
+    bool diff = false;
+    for (int i = wave; i < 2 * a.k; i += 16)
+      diff |= (pv[(long)i * a.p_shard_stride] != 0) != (pu[(long)i * a.p_shard_stride] != 0);
+    if (diff) acc[lane] = 1;  // every writer stores the same value
+  }
+  __syncthreads();
+  if (wave == 0 && v < a.nvec) a.err_same[sq * a.nvec + v] = (v == 0 || acc[lane]) ? 0 : 1;
+}
+
+// Prefix max of (same ? -1 : index) per square in LDS (Hillis-Steele, nvec <= 1024).
+__global__ __launch_bounds__(1024) void errloc_heads_kernel(DecodeArgs a) {
   __shared__ int32_t h[1024];
   const long sq = blockIdx.x;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x;
   const int nvec = (int)a.nvec;
   const long v0 = sq * a.nvec;
-  const uint8_t* base = a.present + sq * a.p_sq_stride;
-  for (int v = wave; v < nvec; v += 16) {
-    bool diff = v == 0;  // the first vector of a square starts a run
-    if (v > 0) {
-      const uint8_t* pv = base + (long)v * a.p_vec_stride;
-      const uint8_t* pu = pv - a.p_vec_stride;
-      for (int i = lane; i < 2 * a.k; i += 64)
-        diff |= (pv[(long)i * a.p_shard_stride] != 0) != (pu[(long)i * a.p_shard_stride] != 0);
-    }
-    const bool any = __builtin_amdgcn_ballot_w64(diff) != 0;
-    if (lane == 0) {
-      a.err_same[v0 + v] = any ? 0 : 1;
-      h[v] = any ? v : -1;
-    }
-  }
+  if (t < nvec) h[t] = a.err_same[v0 + t] ? -1 : t;
   __syncthreads();
   for (int off = 1; off < nvec; off <<= 1) {
     const int x = (t < nvec && t >= off) ? h[t - off] : -1;
@@ -1186,9 +1221,17 @@ __global__ __launch_bounds__(1024) void errloc_runs_kernel(DecodeArgs a) {
 
 hipError_t launch_errloc_heads(const DecodeArgs& a, hipStream_t s) {
   if (!a.err_same || !a.err_head) return hipSuccess;
-  if (a.nsq * a.nvec <= 0) return hipSuccess;
+  const long nv = a.nsq * a.nvec;
+  if (nv <= 0) return hipSuccess;
   if (a.nvec > 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(errloc_runs_kernel, dim3((unsigned)a.nsq), dim3(1024), 0, s, a);
+  if (a.p_shard_stride == 1)
+    hipLaunchKernelGGL(errloc_same_rows_kernel, dim3((unsigned)((nv + 15) / 16)), dim3(1024), 0, s, a);
+  else
+    hipLaunchKernelGGL(errloc_same_cols_kernel, dim3((unsigned)(a.nsq * ((a.nvec + 63) / 64))), dim3(1024), 0,
+                       s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(errloc_heads_kernel, dim3((unsigned)a.nsq), dim3(1024), 0, s, a);
   return hipGetLastError();
 }
 

@@ -172,7 +172,10 @@ __device__ __forceinline__ void encode_half(const EncodeArgs& a, long sq, long v
 #pragma unroll
     for (int j = 0; j < E; j++)
       diff |= w[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, col, (HH * E + j) * out_stride, 0);
-    if (diff) atomicOr(&a.mismatch[sq], a.mismatch_bit);
+    if (diff) {
+      atomicOr(&a.mismatch[sq], a.mismatch_bit);
+      if (a.mismatch_vec) a.mismatch_vec[sq * a.nvec + vec] = 1;
+    }
     return;
   }
 #pragma unroll

@@ -6,8 +6,10 @@
 #include <stdint.h>
 #include <stdio.h>
 
+#include <atomic>
 #include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/dagpu.h"
@@ -61,6 +63,10 @@ struct ProfRec {
 
 struct dagpu_ctx {
   int device = 0;
+  // unique per context ever opened in this process: a thread's saved error is
+  // tied to (pointer, generation), so a later context at the same address
+  // never reports a destroyed one's message (see dagpu_last_error)
+  uint64_t gen = 0;
   hipStream_t stream = nullptr;
   std::mutex mu;
   // Last error message.  Device-resident entry points run without `mu`
@@ -73,9 +79,14 @@ struct dagpu_ctx {
   // host-mode pipeline (dagpu.cpp run_group_pipelined): H2D on copy_stream,
   // kernels + D2H on stream, two slots handed over with events
   hipStream_t copy_stream = nullptr;
-  // device-resident pipeline (dagpu.cpp dagpu_extend_batch_device): RS of later slices
-  // on rs_stream beside the NMT work of earlier slices on the caller's stream
-  hipStream_t rs_stream = nullptr;
+  // device-resident pipeline (dagpu.cpp dagpu_extend_batch_device): RS of later
+  // slices on a side stream beside the NMT work of earlier slices on the caller's
+  // stream.  One side stream per caller stream (up to kMaxSideStreams, then
+  // callers share them round-robin), so concurrent callers on different streams
+  // do not queue their RS slices behind each other.
+  static constexpr size_t kMaxSideStreams = 16;
+  std::mutex side_mu;
+  std::vector<std::pair<hipStream_t, hipStream_t>> side;  // caller -> side stream
   std::mutex ev_mu;
   std::vector<hipEvent_t> ev_pool;  // timing-disabled events, recycled per call
   hipEvent_t ev_loaded[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
@@ -100,6 +111,7 @@ inline bool is_pow2(uint64_t v) { return v != 0 && (v & (v - 1)) == 0; }
 // same context.
 struct ThreadErr {
   const dagpu_ctx* ctx = nullptr;
+  uint64_t gen = 0;
   bool own = false;  // msg is this thread's own failure (not a snapshot)
   std::string msg;
 };
@@ -116,6 +128,7 @@ inline int set_err(dagpu_ctx* c, int code, const std::string& msg) {
   }
   ThreadErr& t = thread_err();
   t.ctx = c;
+  t.gen = c->gen;
   t.own = true;
   t.msg = msg;
   return code;
@@ -132,6 +145,11 @@ inline int hip_fail(dagpu_ctx* c, hipError_t e, const char* what) {
     hipError_t e_ = (expr);                                  \
     if (e_ != hipSuccess) return hip_fail((ctx), e_, #expr); \
   } while (0)
+
+inline uint64_t next_ctx_gen() {
+  static std::atomic<uint64_t> g{0};
+  return ++g;
+}
 
 inline hipEvent_t pool_get(dagpu_ctx* c) {
   if (!c->pool.empty()) {

@@ -139,16 +139,45 @@ int dagpu_decode(dagpu_ctx* ctx, uint32_t k, size_t nvec, size_t shard_size,
 int dagpu_repair(dagpu_ctx* ctx, uint32_t k, uint8_t* eds, uint8_t* present,
                  const uint8_t* row_roots, const uint8_t* col_roots);
 
+/* dagpu_repair plus the failing axis, for rsmt2d's ErrByzantineData{Axis,
+ * Index, Shares} (the input of celestia-node's bad-encoding fraud proof) and
+ * its "bad root input: <axis> <i> ..." error.  byz (4 int32, may be NULL) =
+ * {axis (0 row, 1 col), index, rebuilt axis, rebuilt index}, all -1 when the
+ * status is neither DAGPU_ERR_BYZANTINE nor DAGPU_ERR_BAD_ROOTS.
+ *   - prerepairSanityCheck failures: the first in the order i = 0..2k-1 x
+ *     {row root, col root, row parity, col parity} (upstream runs these checks
+ *     concurrently and returns whichever fails first in time); rebuilt = axis.
+ *   - solveCrossword failures: the first failing attempt in rsmt2d's
+ *     sequential order (each pass: row i, then column i).  Either the rebuilt
+ *     axis' own root differs (axis = rebuilt axis) or an orthogonal axis it
+ *     completed does (axis = that orthogonal axis; rebuilt = the row/column
+ *     whose rebuild completed it, whose shares rsmt2d v0.11.0 attaches).
+ * On DAGPU_ERR_BYZANTINE, present[] is left as rsmt2d leaves the square: the
+ * cells filled by the attempts before the failing one (their bytes in eds are
+ * the committed ones); ErrByzantineData.Shares = the cells of the rebuilt axis
+ * with present[] set.  Replaces ExtendedDataSquare.Repair (rsmt2d v0.11.0). */
+int dagpu_repair_ex(dagpu_ctx* ctx, uint32_t k, uint8_t* eds, uint8_t* present,
+                    const uint8_t* row_roots, const uint8_t* col_roots, int32_t* byz);
+
 /* Device-resident batched Repair: n squares of width k (device pointers),
  * d_present = n * (2k)^2 flags (updated in place), expected roots as produced by
  * dagpu_extend_batch_device.  d_status gets one dagpu_status per square.
  * d_workspace: dagpu_repair_workspace_size(k, n) bytes.  Enqueued on `stream`;
- * the call synchronises once per crossword round to read two counters. */
+ * the call synchronises once per crossword round to read two counters.
+ * The _ex form also writes d_byz (n * 4 int32, device memory, as byz of
+ * dagpu_repair_ex); a square whose crossword fails is then re-run in rsmt2d's
+ * sequential order on the device to name its axis (synchronises `stream`).
+ * Without d_byz the crossword's failing axis is not resolved and the cells of
+ * a square with a failure are left as the batched crossword filled them. */
 size_t dagpu_repair_workspace_size(uint32_t k, size_t n);
 int dagpu_repair_batch_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds,
                               uint8_t* d_present, const uint8_t* d_row_roots,
                               const uint8_t* d_col_roots, int32_t* d_status,
                               void* d_workspace, void* stream);
+int dagpu_repair_batch_device_ex(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds,
+                                 uint8_t* d_present, const uint8_t* d_row_roots,
+                                 const uint8_t* d_col_roots, int32_t* d_status, int32_t* d_byz,
+                                 void* d_workspace, void* stream);
 
 /* Per-kernel timing with HIP events recorded on the launch stream around each
  * kernel the pipeline enqueues (for bench.py's roofline; off by default).

@@ -799,29 +799,47 @@ static int vector_root(int k, int axis_index, const uint8_t* vec, uint8_t out[90
   return rc;
 }
 
-int orc_repair(int k, uint8_t* eds, uint8_t* present, const uint8_t* row_roots,
-               const uint8_t* col_roots) {
+/* byz (optional, 4 ints): {axis, index, rebuilt axis, rebuilt index}, -1 when
+ * none.  ORC_ERR_BAD_ROOTS: the axis/index of the "bad root input" message;
+ * ORC_ERR_BYZANTINE: ErrByzantineData{Axis, Index} plus the vector whose
+ * repair failed (for an orthogonal-root failure the rebuilt row/column whose
+ * shares rsmt2d attaches).  On a failure eds/present are left as before the
+ * failing attempt, as rsmt2d leaves them.
+ * prerepairSanityCheck: upstream runs the four checks of each i concurrently
+ * (errgroup) and returns whichever fails first in time; this restatement takes
+ * them in launch order: row i root, col i root, row i parity, col i parity. */
+int orc_repair_ex(int k, uint8_t* eds, uint8_t* present, const uint8_t* row_roots,
+                  const uint8_t* col_roots, int32_t* byz) {
   orc_init();
+  if (byz) byz[0] = byz[1] = byz[2] = byz[3] = -1;
   if (!is_pow2(k)) return ORC_ERR_ARG;
   int w = 2 * k;
   uint8_t* vec = (uint8_t*)malloc((size_t)w * SS);
   uint8_t* pv = (uint8_t*)malloc((size_t)w);
   uint8_t root[90];
   uint8_t* par = (uint8_t*)malloc((size_t)k * SS);
-  int rc = ORC_OK;
+  int rc = ORC_OK, fa = -1, fi = -1, ra = -1, ri = -1;
   /* prerepairSanityCheck */
   for (int i = 0; i < w && rc == ORC_OK; i++) {
-    for (int axis = 0; axis < 2 && rc == ORC_OK; axis++) {
-      if (!axis_complete(k, present, axis, i)) continue;
+    int complete[2] = {axis_complete(k, present, 0, i), axis_complete(k, present, 1, i)};
+    for (int axis = 0; axis < 2 && rc == ORC_OK; axis++) {  /* roots */
+      if (!complete[axis]) continue;
       gather_axis(k, eds, axis, i, vec);
       int r2 = vector_root(k, i, vec, root);
       if (r2 != ORC_OK) { rc = r2; break; }
       if (memcmp(root, (axis == 0 ? row_roots : col_roots) + (size_t)i * 90, 90) != 0) {
         rc = ORC_ERR_BAD_ROOTS;
-        break;
+        fa = ra = axis; fi = ri = i;
       }
+    }
+    for (int axis = 0; axis < 2 && rc == ORC_OK; axis++) {  /* parity == Encode(data) */
+      if (!complete[axis]) continue;
+      gather_axis(k, eds, axis, i, vec);
       orc_encode(k, SS, vec, par);
-      if (memcmp(par, vec + (size_t)k * SS, (size_t)k * SS) != 0) rc = ORC_ERR_BYZANTINE;
+      if (memcmp(par, vec + (size_t)k * SS, (size_t)k * SS) != 0) {
+        rc = ORC_ERR_BYZANTINE;
+        fa = ra = axis; fi = ri = i;
+      }
     }
   }
   /* solveCrossword */
@@ -844,6 +862,7 @@ int orc_repair(int k, uint8_t* eds, uint8_t* present, const uint8_t* row_roots,
         int r2 = vector_root(k, i, vec, root);
         if (r2 != ORC_OK || memcmp(root, (axis == 0 ? row_roots : col_roots) + (size_t)i * 90, 90)) {
           rc = ORC_ERR_BYZANTINE;
+          fa = ra = axis; fi = ri = i;
           break;
         }
         /* newly completed orthogonal axes */
@@ -864,8 +883,10 @@ int orc_repair(int k, uint8_t* eds, uint8_t* present, const uint8_t* row_roots,
           memcpy(ov + (size_t)pos * SS, vec + (size_t)j * SS, SS);
           int r3 = vector_root(k, oi, ov, root);
           if (r3 != ORC_OK ||
-              memcmp(root, (axis == 0 ? col_roots : row_roots) + (size_t)oi * 90, 90))
+              memcmp(root, (axis == 0 ? col_roots : row_roots) + (size_t)oi * 90, 90)) {
             rc = ORC_ERR_BYZANTINE;
+            fa = 1 - axis; fi = oi; ra = axis; ri = i;
+          }
           free(ov);
         }
         if (rc != ORC_OK) break;
@@ -887,8 +908,16 @@ int orc_repair(int k, uint8_t* eds, uint8_t* present, const uint8_t* row_roots,
     (void)solved;
     if (!progress) { rc = ORC_ERR_UNREPAIRABLE; break; }
   }
+  if (byz && (rc == ORC_ERR_BYZANTINE || rc == ORC_ERR_BAD_ROOTS)) {
+    byz[0] = fa; byz[1] = fi; byz[2] = ra; byz[3] = ri;
+  }
   free(vec);
   free(pv);
   free(par);
   return rc;
+}
+
+int orc_repair(int k, uint8_t* eds, uint8_t* present, const uint8_t* row_roots,
+               const uint8_t* col_roots) {
+  return orc_repair_ex(k, eds, present, row_roots, col_roots, NULL);
 }

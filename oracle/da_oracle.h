@@ -107,6 +107,8 @@ int orc_extend_and_dah(int k, const uint8_t* ods, uint8_t* eds, uint8_t* row_roo
  * filled in place.  Verifies rebuilt axes against the given roots. */
 int orc_repair(int k, uint8_t* eds, uint8_t* present, const uint8_t* row_roots,
                const uint8_t* col_roots);
+int orc_repair_ex(int k, uint8_t* eds, uint8_t* present, const uint8_t* row_roots,
+                  const uint8_t* col_roots, int32_t* byz);
 
 #ifdef __cplusplus
 }

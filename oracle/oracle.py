@@ -63,6 +63,7 @@ def lib(portable: bool = False) -> ctypes.CDLL:
         L.orc_dah_hash.argtypes = [u8p, u8p, ctypes.c_size_t, u8p]
         L.orc_extend_and_dah.argtypes = [ctypes.c_int, u8p, u8p, u8p, u8p, u8p, ctypes.c_int]
         L.orc_repair.argtypes = [ctypes.c_int, u8p, u8p, u8p, u8p]
+        L.orc_repair_ex.argtypes = [ctypes.c_int, u8p, u8p, u8p, u8p, ctypes.POINTER(ctypes.c_int32)]
         L.orc_nmt_leaf.argtypes = [u8p, u8p, ctypes.c_size_t, u8p]
         L.orc_nmt_node.argtypes = [u8p, u8p, u8p]
         L.orc_nmt_root_from_leaves.argtypes = [u8p, ctypes.c_size_t, u8p]
@@ -188,6 +189,17 @@ def repair(eds: np.ndarray, present: np.ndarray, k: int, row_roots, col_roots):
     pr = np.ascontiguousarray(present, dtype=np.uint8).copy()
     rc = lib().orc_repair(k, _p(e), _p(pr), _p(_u8(row_roots)), _p(_u8(col_roots)))
     return rc, e
+
+
+def repair_ex(eds: np.ndarray, present: np.ndarray, k: int, row_roots, col_roots):
+    """orc_repair_ex: (status, eds, present, byz) with byz = [axis, index,
+    rebuilt axis, rebuilt index] (-1 = none); eds/present as rsmt2d leaves them."""
+    e = _u8(eds).copy()
+    pr = np.ascontiguousarray(present, dtype=np.uint8).copy()
+    byz = np.full(4, -1, np.int32)
+    rc = lib().orc_repair_ex(k, _p(e), _p(pr), _p(_u8(row_roots)), _p(_u8(col_roots)),
+                             byz.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    return rc, e, pr, [int(x) for x in byz]
 
 
 def nmt_leaf(ns: bytes, data: bytes) -> bytes:

@@ -227,3 +227,92 @@ def test_device_batch_in_place_matches(ctx):
     assert torch.equal(a.row_roots, b.row_roots) and torch.equal(a.col_roots, b.col_roots)
     _, _, _, hdah, _ = da.extend_batch(ods.reshape(-1), [k] * n, ctx)
     assert (b.dah.cpu().numpy() == hdah).all()
+
+
+@pytest.mark.parametrize("n,slices,first,in_place", [
+    (64, None, None, True),     # the headline shape: 4 slices of 16, ODS in Q0
+    (67, None, None, True),     # uneven slices
+    (70, "2", None, False),
+    (65, "8", None, True),
+    (66, "4", "3", True),       # small first slice (DAGPU_PIPE_FIRST)
+    (64, "3", None, False),     # slice count that does not divide n
+    (64, "1", None, True),      # pipeline off
+])
+def test_pipelined_device_batch(ctx, monkeypatch, n, slices, first, in_place):
+    """The RS/NMT slice pipeline of dagpu_extend_batch_device at k = 128 under
+    several slice settings (read per call), with the ODS in place or separate,
+    over two steps: every DAH and root equals the host API's (unsliced chain),
+    and two squares equal the oracle's."""
+    k = 128
+    for name, v in (("DAGPU_PIPE_SLICES", slices), ("DAGPU_PIPE_FIRST", first)):
+        if v is None:
+            monkeypatch.delenv(name, raising=False)
+        else:
+            monkeypatch.setenv(name, v)
+    ods = synth.blob_squares(k, 6400 + n, 0, n, threads=16)
+    ds = DeviceSquares(k, n, ctx=ctx, in_place=in_place)
+    ds.load_ods(ods)
+    for _ in range(2):
+        ds.extend()
+    torch.cuda.synchronize()
+    assert (ds.status.cpu().numpy() == 0).all()
+    _, hrr, hcr, hdah, hst = da.extend_batch(ods.reshape(-1), [k] * n, ctx)
+    assert (hst == 0).all()
+    dah = ds.dah.cpu().numpy()
+    rr, cr = ds.row_roots.cpu().numpy(), ds.col_roots.cpu().numpy()
+    assert (dah == hdah).all()
+    for i in range(n):
+        assert (rr[i] == hrr[i]).all() and (cr[i] == hcr[i]).all(), i
+    for i in (0, n - 1):
+        _, orr, ocr, odah = oracle.extend_and_dah(ods[i].reshape(k * k, 512), k, nthreads=16, want_eds=False)
+        assert dah[i].tobytes() == odah and (rr[i] == orr).all() and (cr[i] == ocr).all(), i
+    del ds
+    torch.cuda.empty_cache()
+
+
+def test_two_threads_pipelined(ctx):
+    """Two host threads, each with its own stream and buffers, issuing the
+    sliced k = 128 device pipeline concurrently on ONE context: every result
+    equals the host API's (each caller stream gets its own RS side stream)."""
+    k, n = 128, 64
+    out, errors = {}, []
+    sets = {}
+    for name, seed in (("a", 900), ("b", 901)):
+        ods = synth.blob_squares(k, seed, 0, n, threads=16)
+        ds = DeviceSquares(k, n, ctx=ctx, in_place=True)
+        ds.load_ods(ods)
+        _, _, _, want, _ = da.extend_batch(ods.reshape(-1), [k] * n, ctx)
+        sets[name] = (ds, want, torch.cuda.Stream())
+    torch.cuda.synchronize()
+
+    def worker(name):
+        ds, _, st = sets[name]
+        try:
+            for _ in range(3):
+                ds.extend(st)
+            st.synchronize()
+            out[name] = ds.dah.cpu().numpy().copy()
+        except Exception as e:  # pragma: no cover
+            errors.append((name, repr(e)))
+
+    ts = [threading.Thread(target=worker, args=(x,)) for x in sets]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=100)
+    assert not errors, errors
+    for name, (ds, want, _) in sets.items():
+        assert (out[name] == want).all(), name
+        assert (ds.status.cpu().numpy() == 0).all()
+    del sets
+    torch.cuda.empty_cache()
+
+
+def test_headline_check_fatal():
+    """bench.py's headline bit-exact check fires on a corrupted DAH."""
+    env = dict(os.environ, DAGPU_BENCH_CORRUPT="headline")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
+                          "--batch", "64", "--no-cpu", "--no-replay", "--no-e2e", "--no-configs"],
+                         env=env, cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert out.returncode != 0
+    assert "FATAL: headline bit-exact check (1 DAHs" in out.stderr, out.stderr[-2000:]
