@@ -144,12 +144,37 @@ def cpu_baseline(seconds: float, threads: int):
         res[k] = (n, el)
     n, el = res[128]
     n64, el64 = res[64]
+    # thread scaling at k = 128 (bounded: ~2 s per point), so the figure can be
+    # read against hosts with more usable cores than this lease
+    scaling = {}
+    ods128 = synth.blob_squares(128, 90128, 0, 4, threads=threads)
+    sq = oracle.SimdSquare(128)
+    t = 1
+    while t < threads:
+        sq.run(ods128[0], t)  # warm (thread team of this size)
+        m, t0 = 0, time.perf_counter()
+        while True:
+            sq.run(ods128[m % len(ods128)], t)
+            m += 1
+            if time.perf_counter() - t0 >= min(2.0, seconds):
+                break
+        e = time.perf_counter() - t0
+        scaling[str(t)] = {"squares_per_s": m / e, "per_thread": m / e / t}
+        t *= 2
+    scaling[str(threads)] = {"squares_per_s": n / el, "per_thread": n / el / threads}
+    quota = cgroup_cpus()
     return {
         "value": n / el,
         "unit": "squares/s",
         "cores": threads,
         "kind": "simd-port",
         "k": 128,
+        "per_core_squares_per_s": n / el / threads,
+        "thread_scaling": scaling,
+        "usable_cpus": threads,
+        "cgroup_cpu_quota": quota,
+        "cpu_share_note": (f"{threads} of the host's {os.cpu_count()} CPUs usable by this process "
+                           f"(cgroup quota {quota}); gpu_over_cpu compares against this per-lease share"),
         "cpu_model": cpu_model(),
         "host_cpus_visible": os.cpu_count(),
         "isa": oracle.simd_isa(),
@@ -239,6 +264,11 @@ def main():
     if args.mode == "repair":
         return bench_repair(args)
 
+    # before anything touches the GPU: this rank's threads and its pinned
+    # replay shard on its GPU's NUMA node (celestia_da/numa.py)
+    from celestia_da import numa
+    numa_report = numa.bind(0 if os.environ.get("DAGPU_BENCH_SHARED_GPU") == "1"
+                            else int(os.environ.get("LOCAL_RANK", "0")))
     dist, rank, world, local = dist_init()
     torch.cuda.set_device(local)
     from celestia_da import _abi, da, synth
@@ -364,7 +394,7 @@ def main():
     single = bench_single(ctx) if world == 1 and not args.no_e2e else None
     if not args.no_replay:
         out["block_replay"] = bench_replay(dist, rank, world, local, ctx, ds, args.replay_blocks,
-                                           args.replay_dump)
+                                           args.replay_dump, numa_report)
     if world == 1 and not args.no_e2e:
         del ds
         torch.cuda.empty_cache()
@@ -385,6 +415,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.cpu_threads or host_threads())
         out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+        out["gpu_over_cpu_core"] = value / out["cpu_baseline"]["per_core_squares_per_s"]
     if dist is not None and not args.no_split:
         # configs[4] stress: one oversized square split over all ranks (RCCL all-to-all)
         if "ds" in locals():
@@ -503,6 +534,17 @@ REPLAY_SEED = 0x5EED_B10C
 HEADLINE_SEED = 1_000_003
 
 
+def cgroup_cpus():
+    """CPUs granted by the cgroup v2 CPU quota (None when unlimited)."""
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            return int(quota) / int(period)
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def host_threads() -> int:
     """CPU threads this process may use: the affinity mask, capped by a cgroup
     CPU quota when one is set (a GPU box's share is smaller than the machine
@@ -525,7 +567,7 @@ def _fail(dist, bad: bool, local: int, what: str):
         raise SystemExit(3)
 
 
-def bench_replay(dist, rank, world, local, ctx, ds, n_blocks, dump=None):
+def bench_replay(dist, rank, world, local, ctx, ds, n_blocks, dump=None, numa_report=None):
     """configs[4] block replay (app/extend_block.go:14-22, per block as in
     app/test/integration_test.go:355-379): n_blocks consecutive DISTINCT k x k
     squares (seeded, csrc/synth.cpp), contiguous shards per rank.
@@ -620,6 +662,10 @@ def bench_replay(dist, rank, world, local, ctx, ds, n_blocks, dump=None):
                 bad = bad or got != want
     host.close()
     _fail(dist, bad, local, "block replay DAH check")
+    numa_all = [numa_report]
+    if dist is not None:
+        numa_all = [None] * world
+        dist.all_gather_object(numa_all, numa_report)
     if dump and rank == 0:
         json.dump({"k": k, "seed": REPLAY_SEED, "blocks": n_blocks, "sampled_dah": sampled},
                   open(dump, "w"))
@@ -630,6 +676,7 @@ def bench_replay(dist, rank, world, local, ctx, ds, n_blocks, dump=None):
                                       "copy stream) -> roots + DAHs in host memory"},
             "device_resident": dev_res,
             "gen_seconds": gen_s, "pin_alloc_seconds": alloc_s,
+            "numa": numa_all,
             "bit_exact": True,
             "checks": "status; host-streamed == device-resident DAHs; every rank's gathered slice vs "
                       "its own digest; first+last block of every shard recomputed by rank 0 "

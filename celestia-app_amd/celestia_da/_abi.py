@@ -30,6 +30,7 @@ ERR_ARG = -9
 ERR_DEVICE = -10
 ERR_UNSUPPORTED = -11
 ERR_PROOF = -12
+ERR_SQUARE = -13
 
 # Every symbol include/dagpu.h declares (checked by tests/test_abi_cpu.py).
 EXPORTS = (
@@ -57,6 +58,8 @@ EXPORTS = (
     "dagpu_repair_batch_device_ex",
     "dagpu_repair",
     "dagpu_repair_ex",
+    "dagpu_square_construct",
+    "dagpu_square_build",
     "dagpu_profile_enable",
     "dagpu_profile_read",
     "dagpu_dah_hash",
@@ -139,6 +142,8 @@ def lib() -> ctypes.CDLL:
         L.dagpu_repair_workspace_size.restype = sz
         L.dagpu_repair.argtypes = [vp, ctypes.c_uint32, vp, vp, vp, vp]
         L.dagpu_repair_ex.argtypes = [vp, ctypes.c_uint32, vp, vp, vp, vp, vp]
+        L.dagpu_square_construct.argtypes = [vp, vp, vp, sz, ctypes.c_uint32, ctypes.c_uint32, vp, sz, vp]
+        L.dagpu_square_build.argtypes = [vp, vp, vp, sz, ctypes.c_uint32, ctypes.c_uint32, vp, sz, vp, vp]
         L.dagpu_repair_batch_device_ex.argtypes = [vp, ctypes.c_uint32, sz, vp, vp, vp, vp, vp, vp,
                                                    vp, vp]
         L.dagpu_dah_hash.argtypes = [vp, vp, sz, vp]

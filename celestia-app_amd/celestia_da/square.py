@@ -344,6 +344,56 @@ def deconstruct(square: Sequence[Share], pfb_blob_sizes: Callable[[bytes], Seque
     return txs
 
 
+# ---- native construction (libdagpu: csrc/square.cpp, dagpu_square_construct/_build) ----------
+
+def _pack(txs: Sequence[bytes]):
+    import numpy as np
+    lens = np.array([len(t) for t in txs], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(bytes(t) for t in txs) or b"\x00", dtype=np.uint8).copy()
+    return buf, lens
+
+
+def _native(fn: str, txs, max_square_size: int, threshold: int, kept=None):
+    import ctypes
+
+    import numpy as np
+
+    from . import _abi
+    L = _abi.lib()
+    buf, lens = _pack(txs)
+    k = ctypes.c_uint32(0)
+    cap = max(1, max_square_size) ** 2 * sh.SHARE_SIZE
+    out = np.empty(cap, np.uint8)
+    args = [None, _abi.addr(buf), _abi.addr(lens), len(txs), max_square_size, threshold, _abi.addr(out), cap,
+            ctypes.addressof(k)]
+    if kept is not None:
+        args.append(_abi.addr(kept))
+    rc = getattr(L, fn)(*args)
+    if rc != 0:
+        msg = L.dagpu_last_error(None).decode()
+        raise ShareError(msg) if rc == _abi.ERR_SQUARE else ValueError(f"{fn}: status {rc}: {msg}")
+    return int(k.value), out[:int(k.value) ** 2 * sh.SHARE_SIZE]
+
+
+def construct_native(txs: Sequence[bytes], max_square_size: int = SQUARE_SIZE_UPPER_BOUND,
+                     threshold: int = SUBTREE_ROOT_THRESHOLD):
+    """square.Construct in the library's C++ (dagpu_square_construct): (k, ODS
+    bytes as a (k*k*512,) uint8 array), byte-identical to construct(txs)."""
+    return _native("dagpu_square_construct", txs, max_square_size, threshold)
+
+
+def build_native(txs: Sequence[bytes], max_square_size: int = SQUARE_SIZE_UPPER_BOUND,
+                 threshold: int = SUBTREE_ROOT_THRESHOLD):
+    """square.Build in C++ (dagpu_square_build): (k, ODS bytes, kept txs in the
+    order Build returns them: normal txs, then blob txs)."""
+    import numpy as np
+    kept = np.zeros(max(1, len(txs)), np.uint8)
+    k, ods = _native("dagpu_square_build", txs, max_square_size, threshold, kept)
+    normal = [t for i, t in enumerate(txs) if kept[i] and not btx.unmarshal_blob_tx(t)[1]]
+    blob = [t for i, t in enumerate(txs) if kept[i] and btx.unmarshal_blob_tx(t)[1]]
+    return k, ods, normal + blob
+
+
 def tx_share_range(txs: Sequence[bytes], tx_index: int, app_version: int = LATEST_VERSION) -> Range:
     return Builder(square_size_upper_bound(app_version), app_version, *txs).find_tx_share_range(tx_index)
 

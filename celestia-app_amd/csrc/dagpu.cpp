@@ -383,8 +383,8 @@ int dagpu_host_unregister(void* p) {
 // failed on `c`, a snapshot of the context's most recent message.  The pointer
 // stays valid until this thread's next call into the library.
 const char* dagpu_last_error(dagpu_ctx* c) {
-  if (!c) return "null context";
   ThreadErr& t = thread_err();
+  if (!c) return t.ctx == nullptr && t.own ? t.msg.c_str() : "null context";
   if (t.ctx == c && t.gen == c->gen && t.own) return t.msg.c_str();
   std::lock_guard<std::mutex> g(c->err_mu);
   t.ctx = c;

@@ -121,7 +121,14 @@ inline ThreadErr& thread_err() {
 }
 
 inline int set_err(dagpu_ctx* c, int code, const std::string& msg) {
-  if (!c) return code;
+  if (!c) {  // context-free host calls (square construction): dagpu_last_error(NULL)
+    ThreadErr& t = thread_err();
+    t.ctx = nullptr;
+    t.gen = 0;
+    t.own = true;
+    t.msg = msg;
+    return code;
+  }
   {
     std::lock_guard<std::mutex> g(c->err_mu);
     c->err = msg;

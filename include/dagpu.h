@@ -53,7 +53,8 @@ typedef enum dagpu_status {
   DAGPU_ERR_ARG = -9,
   DAGPU_ERR_DEVICE = -10,        /* HIP runtime failure */
   DAGPU_ERR_UNSUPPORTED = -11,   /* e.g. k above what this build implements */
-  DAGPU_ERR_PROOF = -12          /* a proof does not verify against the given root */
+  DAGPU_ERR_PROOF = -12,         /* a proof does not verify against the given root */
+  DAGPU_ERR_SQUARE = -13         /* square construction rejected the txs (pkg/square errors) */
 } dagpu_status;
 
 typedef struct dagpu_ctx dagpu_ctx;
@@ -64,7 +65,7 @@ int dagpu_version(void);
 /* Open a context on HIP device `device` (one context per GPU per process). */
 int dagpu_init(int device, dagpu_ctx** out);
 void dagpu_destroy(dagpu_ctx* ctx);
-const char* dagpu_last_error(dagpu_ctx* ctx);
+const char* dagpu_last_error(dagpu_ctx* ctx);  /* NULL: this thread's last context-free call */
 
 /* Replaces da.ExtendShares + da.NewDataAvailabilityHeader + dah.Hash()
  * (pkg/da/data_availability_header.go:65-75, :44-63, :92-108) for one square.
@@ -316,6 +317,28 @@ int dagpu_row_nodes_device(dagpu_ctx* ctx, uint32_t k, const uint8_t* d_eds, uin
                            void* d_workspace, void* stream);
 int dagpu_row_nodes_gather_device(dagpu_ctx* ctx, uint32_t k, const uint8_t* d_nodes, size_t n,
                                   const uint32_t* d_requests, uint8_t* d_out, void* stream);
+
+/* ---- Square construction (host; pkg/square, app version 1) ---------------
+ * square.Construct (pkg/square/square.go:22-63, builder.go): ntx txs packed
+ * back to back in `txs` (tx_lens[i] bytes each; blob txs in the BlobTx proto
+ * wire format, pkg/blob/blob.go:56-90) -> the original data square, k*k
+ * 512-B shares row-major, in ods_out (ods_cap bytes; k*k*512 needed, k <=
+ * max_square_size; *square_size = k is set even when ods_out is too small,
+ * which returns DAGPU_ERR_ARG).  Every tx must fit and normal txs must come
+ * before blob txs, else DAGPU_ERR_SQUARE with the reference's message
+ * ("not enough space to append tx at index 3", ...).  max_square_size =
+ * SquareSizeUpperBound (128) and subtree_root_threshold = 64 for app v1.
+ * The ODS goes straight into dagpu_extend_shares / the device batch API.
+ * ctx may be NULL (then no message is kept).  No device work. */
+int dagpu_square_construct(dagpu_ctx* ctx, const uint8_t* txs, const uint64_t* tx_lens, size_t ntx,
+                           uint32_t max_square_size, uint32_t subtree_root_threshold, uint8_t* ods_out,
+                           size_t ods_cap, uint32_t* square_size);
+/* square.Build: txs that do not fit are skipped (kept[i] = 0), normal txs may
+ * follow blob txs; the reference returns the kept normal txs, then the kept
+ * blob txs, in input order within each group. */
+int dagpu_square_build(dagpu_ctx* ctx, const uint8_t* txs, const uint64_t* tx_lens, size_t ntx,
+                       uint32_t max_square_size, uint32_t subtree_root_threshold, uint8_t* ods_out,
+                       size_t ods_cap, uint32_t* square_size, uint8_t* kept);
 
 #ifdef __cplusplus
 }

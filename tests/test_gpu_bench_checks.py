@@ -107,6 +107,8 @@ def test_replay_rehearsal_two_ranks(tmp_path):
     rep = line["block_replay"]
     assert rep["bit_exact"] is True and rep["distinct_squares"] == 40 and rep["per_rank"] == 20
     assert rep["host_streamed"]["squares_per_s"] > 0 and rep["device_resident"]["squares_per_s"] > 0
+    # each rank's NUMA placement (celestia_da/numa.py), gathered from every rank
+    assert len(rep["numa"]) == 2 and all(r["affinity"] and "numa_node" in r for r in rep["numa"]), rep["numa"]
     d = json.load(open(dump))
     k, seed = d["k"], d["seed"]
     assert sorted(int(b) for b in d["sampled_dah"]) == [0, 19, 20, 39]

@@ -57,3 +57,23 @@ def test_square_share_commitments(ctx, num_txs, blobs_per, max_size, seed):
     assert checked == num_txs * blobs_per
     # the square round-trips through the txs it was built from
     assert sq.deconstruct(square, pfb_blob_sizes) == txs
+
+
+@pytest.mark.parametrize("n_normal,n_blob,max_size,seed", [(2000, 2000, 3000, 7), (30, 12, 9000, 8), (0, 0, 1, 9)])
+def test_native_construct_to_dah(ctx, n_normal, n_blob, max_size, seed):
+    """txs -> DataHash with the native constructor (dagpu_square_construct,
+    csrc/square.cpp) feeding the GPU path, as app/extend_block.go:14-22 does
+    per block: the ODS equals the Python mirror's, the DAH equals the oracle's."""
+    import time
+    rng = random.Random(seed)
+    txs = normal_txs(rng, n_normal, 300) + random_blob_txs(rng, n_blob, max_size)
+    t0 = time.perf_counter()
+    k, ods = sq.construct_native(txs)
+    t_native = time.perf_counter() - t0
+    want = sq.construct(txs)
+    assert k == want.size()
+    assert (ods == np.frombuffer(b"".join(want.square_bytes()), np.uint8)).all()
+    dah = da.new_data_availability_header(da.extend_shares(ods.reshape(k * k, 512), ctx))
+    _, _, _, h = oracle.extend_and_dah(ods.reshape(k * k, 512), k, nthreads=16, want_eds=False)
+    assert dah.hash() == h
+    print(f"k={k}: native construct {t_native * 1e3:.2f} ms (incl. Python packing)")
