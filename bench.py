@@ -222,9 +222,13 @@ def valu_issue(k: int, B: int, ms_step: float, leaf_ms: float):
         + (levels - 1) * per["nmt_trees_ln"] + per["dah"]
     clock = grbm / 8 / (leaf_ms * 1e-3)
     cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
-    return {"wave_instr_per_step": total, "clock_ghz": clock / 1e9, "cus": cus,
-            "wave_instr_per_clk_per_cu": total / (ms_step * 1e-3 * cus * clock),
-            "ceiling": 1.0, "source": f"profiles/pmc_valu.json ({tag}) + this run's step and leaf times"}
+    return {"estimate": True,
+            "wave_instr_per_step_committed": total, "clock_ghz_est": clock / 1e9, "cus": cus,
+            "wave_instr_per_clk_per_cu_est": total / (ms_step * 1e-3 * cus * clock),
+            "ceiling": 1.0, "counts_build": tag,
+            "source": f"ESTIMATE: instruction and GRBM cycle counts committed in profiles/pmc_valu.json "
+                      f"(build {tag}, another run and box) divided by this run's step and leaf times; "
+                      f"stale if a kernel changed since {tag}"}
 
 
 def main():
@@ -487,7 +491,7 @@ def bench_e2e(ctx, local, k, host_ods, steps, total=256):
                     "previous chunk's kernels; roots+DAHs back to host"}
 
 
-def bench_single(ctx, ks=(64, 128), calls=60):
+def bench_single(ctx, ks=(64, 128), calls=60, trace=True):
     """Drop-in latency of ONE square per call, as the production callers use it
     (app/process_proposal.go:147-161, app/prepare_proposal.go:95-107):
     dagpu_extend_shares from page-locked host shares, with eds_out NULL (roots +
@@ -497,6 +501,8 @@ def bench_single(ctx, ks=(64, 128), calls=60):
 
     L = ctx._L
     res = {}
+    if trace:
+        L.dagpu_profile_enable(ctx.handle, 2)
     for k in ks:
         w = 2 * k
         src = da.PinnedBuffer(k * k * SHARE)
@@ -506,8 +512,9 @@ def bench_single(ctx, ks=(64, 128), calls=60):
         cr = np.empty(w * 90, np.uint8)
         dah = np.empty(32, np.uint8)
         r = {}
+        stages = np.zeros(len(_abi.STAGES), np.float32)
         for mode, eds_ptr in (("roots_only", 0), ("with_eds", edsb.ptr)):
-            lat = []
+            lat, tl = [], []
             for i in range(5 + calls):
                 t0 = time.perf_counter()
                 rc = L.dagpu_extend_shares(ctx.handle, src.ptr, k * k, SHARE, eds_ptr, _abi.addr(rr),
@@ -517,9 +524,19 @@ def bench_single(ctx, ks=(64, 128), calls=60):
                     raise SystemExit(f"dagpu_extend_shares k={k}: status {rc}")
                 if i >= 5:
                     lat.append(t * 1e3)
+                    if trace:  # stage timeline of this call (HIP events, read after it returned)
+                        L.dagpu_profile_stages(ctx.handle, _abi.addr(stages))
+                        tl.append(stages.copy())
             lat = np.array(lat)
             r[mode] = {"p50_ms": float(np.percentile(lat, 50)), "p99_ms": float(np.percentile(lat, 99)),
                        "mean_ms": float(lat.mean())}
+            if trace:
+                tl = np.array(tl)
+                order = np.argsort(lat)
+                name = lambda row: {s: round(float(v), 4) for s, v in zip(_abi.STAGES, row) if v >= 0}  # noqa: E731
+                r[mode]["stages_median_ms"] = name(np.median(tl, axis=0))
+                r[mode]["stages_slowest"] = [dict(name(tl[j]), wall_ms=round(float(lat[j]), 4))
+                                             for j in order[-3:][::-1]]
         want = da.new_data_availability_header(da.extend_shares(src.array.reshape(k * k, SHARE), ctx)).hash()
         r["dah_ok"] = dah.tobytes() == want
         res[str(k)] = r
@@ -527,6 +544,8 @@ def bench_single(ctx, ks=(64, 128), calls=60):
         edsb.close()
         if not r["dah_ok"]:
             raise SystemExit(f"single-square DAH mismatch at k={k}")
+    if trace:
+        L.dagpu_profile_enable(ctx.handle, 0)
     return res
 
 

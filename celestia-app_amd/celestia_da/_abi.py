@@ -62,6 +62,7 @@ EXPORTS = (
     "dagpu_square_build",
     "dagpu_profile_enable",
     "dagpu_profile_read",
+    "dagpu_profile_stages",
     "dagpu_dah_hash",
     "dagpu_nmt_roots",
     "dagpu_wrapper_roots",
@@ -85,6 +86,8 @@ PREFIX_PARITY = 2
 PREFIX_FLAGS = 3
 
 PROFILE_KERNELS = ("rs_row", "rs_col", "nmt_leaves", "nmt_trees", "dah", "decode")
+# dagpu_profile_stages (include/dagpu.h DAGPU_STAGE_*)
+STAGES = ("start", "uploaded", "rs_rows", "rs_cols", "leaves", "trees", "dah", "results", "eds_top", "eds_bottom")
 
 _lib = None
 
@@ -93,6 +96,31 @@ u32p = ctypes.POINTER(ctypes.c_uint32)
 i32p = ctypes.POINTER(ctypes.c_int32)
 vp = ctypes.c_void_p
 sz = ctypes.c_size_t
+
+
+class _Unbound:
+    """Stand-in for an entry point an older build (DAGPU_LIB A/B runs) lacks."""
+
+    def __init__(self, name):
+        self.name = name
+
+    def __call__(self, *a):
+        raise AttributeError(f"{LIB_PATH}: no symbol {self.name}")
+
+
+class _Tolerant:
+    """An alternate build under A/B (DAGPU_LIB): symbols it lacks stay unbound."""
+
+    def __init__(self, L):
+        object.__setattr__(self, "_L", L)
+
+    def __getattr__(self, name):
+        try:
+            return getattr(self._L, name)
+        except AttributeError:
+            u = _Unbound(name)
+            object.__setattr__(self, name, u)
+            return u
 
 
 def lib() -> ctypes.CDLL:
@@ -110,6 +138,8 @@ def lib() -> ctypes.CDLL:
         except ImportError:
             pass
         L = ctypes.CDLL(LIB_PATH)
+        if os.environ.get("DAGPU_LIB"):
+            L = _Tolerant(L)
         L.dagpu_version.restype = ctypes.c_int
         L.dagpu_init.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
         L.dagpu_destroy.argtypes = [vp]
@@ -141,6 +171,7 @@ def lib() -> ctypes.CDLL:
         L.dagpu_repair_workspace_size.argtypes = [ctypes.c_uint32, sz]
         L.dagpu_repair_workspace_size.restype = sz
         L.dagpu_repair.argtypes = [vp, ctypes.c_uint32, vp, vp, vp, vp]
+        L.dagpu_profile_stages.argtypes = [vp, vp]
         L.dagpu_repair_ex.argtypes = [vp, ctypes.c_uint32, vp, vp, vp, vp, vp]
         L.dagpu_square_construct.argtypes = [vp, vp, vp, sz, ctypes.c_uint32, ctypes.c_uint32, vp, sz, vp]
         L.dagpu_square_build.argtypes = [vp, vp, vp, sz, ctypes.c_uint32, ctypes.c_uint32, vp, sz, vp, vp]

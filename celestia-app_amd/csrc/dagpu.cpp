@@ -70,6 +70,7 @@ int enqueue_rs(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_ods, uint8
     ProfScope p(ctx, 0, s);
     HIP_TRY(ctx, launch_rs_encode((int)k, ra, s));
   }
+  stage_mark(ctx, DAGPU_STAGE_ROWS, s);
   if (ev_rows) HIP_TRY(ctx, hipEventRecord(ev_rows, s));
   // Column pass: vector c = column c of [Q0|Q1] -> [Q2|Q3].
   EncodeArgs ca{};
@@ -90,6 +91,7 @@ int enqueue_rs(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_ods, uint8
     ProfScope p(ctx, 1, s);
     HIP_TRY(ctx, launch_rs_encode((int)k, ca, s));
   }
+  stage_mark(ctx, DAGPU_STAGE_COLS, s);
   return DAGPU_OK;
 }
 
@@ -112,14 +114,17 @@ int enqueue_roots(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_eds, ui
     ProfScope p(ctx, 2, s);
     HIP_TRY(ctx, launch_nmt_leaves(sa, s));
   }
+  stage_mark(ctx, DAGPU_STAGE_LEAVES, s);
   {
     ProfScope p(ctx, 3, s);
     HIP_TRY(ctx, launch_nmt_trees(sa, s));
   }
+  stage_mark(ctx, DAGPU_STAGE_TREES, s);
   {
     ProfScope p(ctx, 4, s);
     HIP_TRY(ctx, launch_dah(sa, s));
   }
+  stage_mark(ctx, DAGPU_STAGE_DAH, s);
   return DAGPU_OK;
 }
 
@@ -267,7 +272,10 @@ int run_group_host(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* ods, uin
   HIP_TRY(ctx, ctx->eds.ensure(eds_bytes(k) * n));
   HIP_TRY(ctx, res.alloc(ctx, k, n));
   HIP_TRY(ctx, ctx->ws.ensure(dagpu_workspace_size(k, n)));
+  ctx->stage_mask = 0;
+  stage_mark(ctx, DAGPU_STAGE_START, s);
   HIP_TRY(ctx, hipMemcpyAsync(ctx->ods.p, ods, ods_bytes(k) * n, hipMemcpyHostToDevice, s));
+  stage_mark(ctx, DAGPU_STAGE_UPLOADED, s);
   // An EDS requested back goes down on the copy stream while the kernels run:
   // the top halves ([Q0|Q1], final after the row pass) during the column pass
   // and the NMT kernels, the bottom halves ([Q2|Q3]) during the NMT kernels.
@@ -281,6 +289,7 @@ int run_group_host(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* ods, uin
   rc = enqueue_roots(ctx, k, n, (const uint8_t*)ctx->eds.p, res.rr, res.cr, res.dah, res.st, ctx->ws.p, s);
   if (rc) return rc;
   HIP_TRY(ctx, res.download(ctx, s));
+  stage_mark(ctx, DAGPU_STAGE_RESULTS, s);
   if (eds_out) {
     hipStream_t cs = ctx->copy_stream;
     // from here on DMA may be writing into eds_out: every return path waits for it
@@ -293,10 +302,12 @@ int run_group_host(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* ods, uin
     const uint8_t* d = (const uint8_t*)ctx->eds.p;
     for (size_t i = 0; i < n; i++)  // plain 1D copies: the DMA engines' fast path
       HIP_TRY(ctx, hipMemcpyAsync(eds_out + i * eb, d + i * eb, half, hipMemcpyDeviceToHost, cs));
+    stage_mark(ctx, DAGPU_STAGE_EDS_TOP, cs);
     HIP_TRY(ctx, hipStreamWaitEvent(cs, ctx->ev_loaded[1], 0));
     for (size_t i = 0; i < n; i++)
       HIP_TRY(ctx, hipMemcpyAsync(eds_out + i * eb + half, d + i * eb + half, half,
                                   hipMemcpyDeviceToHost, cs));
+    stage_mark(ctx, DAGPU_STAGE_EDS_BOTTOM, cs);
     HIP_TRY(ctx, hipStreamSynchronize(cs));
   }
   HIP_TRY(ctx, hipStreamSynchronize(s));
@@ -326,6 +337,7 @@ int dagpu_init(int device, dagpu_ctx** out) {
   for (int i = 0; ok && i < 2; i++)
     ok = hipEventCreateWithFlags(&c->ev_loaded[i], hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&c->ev_done[i], hipEventDisableTiming) == hipSuccess;
+  for (int i = 0; ok && i < dagpu_ctx::kStages; i++) ok = hipEventCreate(&c->stage_ev[i]) == hipSuccess;
   if (!ok) {
     dagpu_destroy(c);
     return DAGPU_ERR_DEVICE;
@@ -352,6 +364,8 @@ void dagpu_destroy(dagpu_ctx* c) {
     if (c->ev_loaded[i]) (void)hipEventDestroy(c->ev_loaded[i]);
     if (c->ev_done[i]) (void)hipEventDestroy(c->ev_done[i]);
   }
+  for (auto e : c->stage_ev)
+    if (e) (void)hipEventDestroy(e);
   for (auto& cs : c->side) (void)hipStreamSynchronize(cs.second);
   for (auto e : c->ev_pool) (void)hipEventDestroy(e);
   for (auto& cs : c->side) (void)hipStreamDestroy(cs.second);
@@ -1128,7 +1142,21 @@ int dagpu_repair(dagpu_ctx* ctx, uint32_t k, uint8_t* eds, uint8_t* present,
 
 int dagpu_profile_enable(dagpu_ctx* ctx, int on) {
   if (!ctx) return DAGPU_ERR_ARG;
-  ctx->prof = on != 0;
+  ctx->prof = (on & 1) != 0;
+  ctx->stages_on = (on & 2) != 0;
+  return DAGPU_OK;
+}
+
+int dagpu_profile_stages(dagpu_ctx* ctx, float* ms) {
+  if (!ctx || !ms) return DAGPU_ERR_ARG;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  for (int i = 0; i < dagpu_ctx::kStages; i++) ms[i] = -1.0f;
+  if (!(ctx->stage_mask & 1u)) return DAGPU_OK;
+  for (int i = 0; i < dagpu_ctx::kStages; i++) {
+    if (!(ctx->stage_mask & (1u << i))) continue;
+    HIP_TRY(ctx, hipEventSynchronize(ctx->stage_ev[i]));
+    HIP_TRY(ctx, hipEventElapsedTime(&ms[i], ctx->stage_ev[0], ctx->stage_ev[i]));
+  }
   return DAGPU_OK;
 }
 

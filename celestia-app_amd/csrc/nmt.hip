@@ -162,13 +162,21 @@ __global__ __launch_bounds__(256) void nmt_level1_kernel(SquareArgs a, uint8_t* 
   }
   uint32_t st[8];
   const bool lpar = ns_is_parity(nl), rpar = ns_is_parity(nr);
-  if (__all(lpar)) {
+  if (__all(lpar && rpar)) {
+    // both children of every node of this wave carry the parity namespace (3/4
+    // of all nodes): the namespace words of all three blocks are constant and
+    // every block runs fully unrolled so their schedule terms fold as well
+    auto get = [&](int P, int i) -> uint32_t {
+      return P == 2 ? dl[i] : P == 5 ? dr[i] : 0xFFFFFFFFu;
+    };
+    sha_node_msg<true, true, true>(get, st);
+  } else if (__all(lpar)) {
     // every left leaf of this wave carries the parity namespace: the message's
     // first 56 bytes (0x01 | 0xFF*58) are constant and rounds 0..13 of block 0 fold
     auto get = [&](int P, int i) -> uint32_t {
-      return P == 0 || P == 1 ? (i == 7 ? 0xFFu : 0xFFFFFFFFu) : P == 2 ? dl[i] : P == 3 || P == 4 ? nr[i] : dr[i];
+      return P == 0 || P == 1 ? 0xFFFFFFFFu : P == 2 ? dl[i] : P == 3 || P == 4 ? nr[i] : dr[i];
     };
-    sha_node_msg(get, st);
+    sha_node_msg<true>(get, st);
   } else {
     auto get = [&](int P, int i) -> uint32_t {
       return P == 0 || P == 1 ? nl[i] : P == 2 ? dl[i] : P == 3 || P == 4 ? nr[i] : dr[i];
@@ -215,13 +223,20 @@ __global__ __launch_bounds__(256) void nmt_level_kernel(SquareArgs a, const uint
   ns_by_ref(ns_sq, r2.x, rmn);
   ns_by_ref(ns_sq, r2.y, rmx);
   uint32_t st[8];
-  if (__all(l2.x == kParityRef)) {
+  if (__all(l2.x == kParityRef && r2.x == kParityRef)) {
+    // both children all-parity (3/4 of all nodes): constant namespace words in
+    // all three blocks, each fully unrolled so the schedule folds too
+    auto get = [&](int P, int i) -> uint32_t {
+      return P == 2 ? dl[i] : P == 5 ? dr[i] : 0xFFFFFFFFu;
+    };
+    sha_node_msg<true, true, true>(get, st);
+  } else if (__all(l2.x == kParityRef)) {
     // all-parity left children (min PARITY implies max PARITY): constant
     // 0x01 | 0xFF*58 prefix, rounds 0..13 of block 0 fold
     auto get = [&](int P, int i) -> uint32_t {
-      return P <= 1 ? (i == 7 ? 0xFFu : 0xFFFFFFFFu) : P == 2 ? dl[i] : P == 3 ? rmn[i] : P == 4 ? rmx[i] : dr[i];
+      return P <= 1 ? 0xFFFFFFFFu : P == 2 ? dl[i] : P == 3 ? rmn[i] : P == 4 ? rmx[i] : dr[i];
     };
-    sha_node_msg(get, st);
+    sha_node_msg<true>(get, st);
   } else {
     auto get = [&](int P, int i) -> uint32_t {
       return P == 0 ? lmn[i] : P == 1 ? lmx[i] : P == 2 ? dl[i] : P == 3 ? rmn[i] : P == 4 ? rmx[i] : dr[i];

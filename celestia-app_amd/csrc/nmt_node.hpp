@@ -7,6 +7,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+#include <utility>
+
 #include "sha256.hpp"
 
 namespace dagpu {
@@ -51,51 +54,144 @@ __device__ __forceinline__ void put_bytes(uint32_t (&m)[MW], const uint32_t (&sr
   }
 }
 
-// Window form: OR part P (8 dwords fetched through get(P, i)) placed at message
-// byte OFF into the 16-word window of SHA block B.  Only dwords that land in the
-// window are fetched, so each block pulls just the source words it needs.
-template <int OFF, int B, int P, class G>
-__device__ __forceinline__ void put_part_win(uint32_t (&m)[16], const G& get) {
-  constexpr int al = OFF & 3;
-  constexpr int d0 = OFF >> 2;
-  constexpr int lo = 16 * B, hi = 16 * B + 16;
+// v_perm_b32 with a plain-C fallback when both sources are compile-time
+// constants (parity namespace words), so constant message words fold.
+__device__ __forceinline__ uint32_t perm_c(uint32_t s0, uint32_t s1, uint32_t sel) {
+  if (__builtin_constant_p(s0) && __builtin_constant_p(s1)) {
+    const uint64_t v = ((uint64_t)s0 << 32) | s1;
+    uint32_t r = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const int p0 = d0 + i, p1 = d0 + i + 1;
-    const bool in0 = p0 >= lo && p0 < hi;
-    const bool in1 = al != 0 && p1 >= lo && p1 < hi;
-    if (in0 || in1) {
-      const uint32_t v = get(P, i);
-      if (in0) m[p0 - lo] |= al ? (v << (8 * al)) : v;
-      if (in1) m[p1 - lo] |= v >> (32 - 8 * al);
+    for (int i = 0; i < 4; i++) {
+      const uint32_t sb = (sel >> (8 * i)) & 0xFFu;
+      const uint32_t byte = sb < 8 ? (uint32_t)(v >> (8 * sb)) & 0xFFu : sb == 12 ? 0u : 0xFFu;
+      r |= byte << (8 * i);
     }
+    return r;
+  }
+  return __builtin_amdgcn_perm(s0, s1, sel);
+}
+
+// Byte m of the HashNode message 0x01 | L.min(29) | L.max(29) | L.d(32) |
+// R.min(29) | R.max(29) | R.d(32) | SHA padding (181 B, 3 blocks): part 0..5
+// and byte within the part, or part -1 with a constant value.
+struct NodeByte {
+  int part, q, cval;
+};
+constexpr NodeByte node_byte(int m) {
+  constexpr int off[6] = {1, 30, 59, 91, 120, 149}, len[6] = {29, 29, 32, 29, 29, 32};
+  if (m == 0) return {-1, 0, 0x01};
+  for (int p = 0; p < 6; p++)
+    if (m >= off[p] && m < off[p] + len[p]) return {p, m - off[p], 0};
+  if (m == 181) return {-1, 0, 0x80};
+  if (m >= 184 && m < 192) {  // 64-bit big-endian bit length 181 * 8 = 1448
+    const unsigned long long bits = 181ull * 8ull;
+    return {-1, 0, (int)((bits >> (8 * (191 - m))) & 0xFF)};
+  }
+  return {-1, 0, 0};
+}
+
+// Big-endian message word J built with v_perm_b32 straight from the parts'
+// little-endian dwords: one perm when its 4 bytes come from <= 2 source
+// dwords, two when from 3 (a 29-byte namespace's last byte plus its neighbours),
+// plus an OR for the 0x01 / 0x80 bytes.  (Round 2 shifted and OR-ed every
+// dword into place and byte-swapped each word: ~3 ops per word.)
+template <int J, class G>
+__device__ __forceinline__ uint32_t node_word(const G& get) {
+  struct Src {
+    int part, d;
+  };
+  struct Plan {
+    Src src[3];
+    int nsrc;
+    int which[4];  // per output byte (0 = LSB = message byte 4J+3): source slot, -1 = constant
+    int sb[4];     // byte within that source dword
+    uint32_t cword;  // constant bytes
+  };
+  constexpr Plan P = [] {
+    Plan pl{};
+    pl.nsrc = 0;
+    pl.cword = 0;
+    for (int i = 0; i < 4; i++) {
+      const NodeByte nb = node_byte(4 * J + 3 - i);
+      if (nb.part < 0) {
+        pl.which[i] = -1;
+        pl.sb[i] = 0;
+        pl.cword |= (uint32_t)nb.cval << (8 * i);
+        continue;
+      }
+      const int d = nb.q >> 2;
+      int slot = -1;
+      for (int t = 0; t < pl.nsrc; t++)
+        if (pl.src[t].part == nb.part && pl.src[t].d == d) slot = t;
+      if (slot < 0) {
+        slot = pl.nsrc++;
+        pl.src[slot] = {nb.part, d};
+      }
+      pl.which[i] = slot;
+      pl.sb[i] = nb.q & 3;
+    }
+    return pl;
+  }();
+  if constexpr (P.nsrc == 0) {
+    return P.cword;
+  } else if constexpr (P.nsrc <= 2) {
+    // perm(S0 = src[1] (bytes 4..7), S1 = src[0] (bytes 0..3))
+    constexpr uint32_t sel = [] {
+      uint32_t s = 0;
+      for (int i = 0; i < 4; i++) {
+        const uint32_t v = P.which[i] < 0 ? 0x0Cu : (uint32_t)(P.which[i] == 0 ? P.sb[i] : 4 + P.sb[i]);
+        s |= v << (8 * i);
+      }
+      return s;
+    }();
+    const uint32_t s1 = get(P.src[0].part, P.src[0].d);
+    const uint32_t s0 = P.nsrc == 2 ? get(P.src[1].part, P.src[1].d) : s1;
+    const uint32_t w = perm_c(s0, s1, sel);
+    return P.cword ? (w | P.cword) : w;
+  } else {
+    // t = perm(src[1], src[0]) for their bytes; then perm(t, src[2])
+    constexpr uint32_t sel1 = [] {
+      uint32_t s = 0;
+      for (int i = 0; i < 4; i++) {
+        const uint32_t v = (P.which[i] == 0) ? (uint32_t)P.sb[i] : (P.which[i] == 1) ? 4u + P.sb[i] : 0x0Cu;
+        s |= v << (8 * i);
+      }
+      return s;
+    }();
+    constexpr uint32_t sel2 = [] {
+      uint32_t s = 0;
+      for (int i = 0; i < 4; i++) {
+        const uint32_t v = (P.which[i] == 2) ? (uint32_t)P.sb[i] : (P.which[i] < 0) ? 0x0Cu : 4u + i;
+        s |= v << (8 * i);
+      }
+      return s;
+    }();
+    const uint32_t t = perm_c(get(P.src[1].part, P.src[1].d), get(P.src[0].part, P.src[0].d), sel1);
+    const uint32_t w = perm_c(t, get(P.src[2].part, P.src[2].d), sel2);
+    return P.cword ? (w | P.cword) : w;
   }
 }
 
+template <int B, class G, bool F>
+__device__ __forceinline__ void static_for_words(const G& get, uint32_t (&st)[8], std::bool_constant<F>) {
+  uint32_t m[16];
+  [&]<int... I>(std::integer_sequence<int, I...>) {
+    ((m[I] = node_word<16 * B + I>(get)), ...);
+  }(std::make_integer_sequence<int, 16>{});
+  sha256_compress_t<F>(st, m);
+}
+
 // NMT HashNode message 0x01 | L.min | L.max | L.d | R.min | R.max | R.d
-// (181 B, 3 SHA blocks).  get(P, i): P = 0..5 -> Lmn, Lmx, Ld, Rmn, Rmx, Rd.
-template <class G>
+// (181 B, 3 SHA blocks).  get(P, i): P = 0..5 -> Lmn, Lmx, Ld, Rmn, Rmx, Rd
+// (8 little-endian dwords in memory byte order; namespace bytes 29..31 are
+// never read).  FULLn: block n runs fully unrolled, for callers whose get()
+// returns compile-time constants in that block (all-parity children).
+template <bool FULL0 = false, bool FULL1 = false, bool FULL2 = false, class G>
 __device__ __forceinline__ void sha_node_msg(const G& get, uint32_t (&st)[8]) {
   sha256_init(st);
-#pragma unroll
-  for (int blk = 0; blk < 3; blk++) {
-    uint32_t m[16];
-#pragma unroll
-    for (int j = 0; j < 16; j++) m[j] = 0;
-    if (blk == 0) m[0] = 0x01u;
-    if (blk == 0) { put_part_win<1, 0, 0>(m, get); put_part_win<30, 0, 1>(m, get); put_part_win<59, 0, 2>(m, get); }
-    if (blk == 1) {
-      put_part_win<59, 1, 2>(m, get); put_part_win<91, 1, 3>(m, get); put_part_win<120, 1, 4>(m, get);
-    }
-    if (blk == 2) {
-      put_part_win<120, 2, 4>(m, get); put_part_win<149, 2, 5>(m, get);
-      m[45 - 32] |= 0x80u << 8;  // byte 181
-    }
-#pragma unroll
-    for (int j = 0; j < 16; j++) m[j] = bswap32(m[j]);
-    if (blk == 2) { m[14] = 0; m[15] = 181u * 8u; }
-    sha256_compress(st, m);
-  }
+  static_for_words<0>(get, st, std::bool_constant<FULL0>{});
+  static_for_words<1>(get, st, std::bool_constant<FULL1>{});
+  static_for_words<2>(get, st, std::bool_constant<FULL2>{});
 }
 
 __device__ __forceinline__ void load_digest(const uint8_t* p, uint32_t (&d)[8]) {
@@ -170,7 +266,7 @@ __device__ __forceinline__ void share_leaf_sha256(const uint4* src, bool q0, uin
 #pragma unroll
       for (int j = 1; j <= 6; j++) m[j] = 0xFFFFFFFFu;
       m[7] = 0xFFFF0000u | m7lo;
-      sha256_compress(st, m);
+      sha256_compress_t<true>(st, m);
     }
   }
   mid_block(cur[2], cur[3], cur[4], cur[5], cur[6]);  // block 1
@@ -192,7 +288,7 @@ __device__ __forceinline__ void share_leaf_sha256(const uint4* src, bool q0, uin
 #pragma unroll
     for (int j = 8; j < 15; j++) m[j] = 0u;
     m[15] = 542u * 8u;
-    sha256_compress(st, m);
+    sha256_compress_t<true>(st, m);  // words 8..15 constant: their schedule terms fold
   }
 }
 

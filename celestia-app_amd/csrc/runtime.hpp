@@ -93,8 +93,13 @@ struct dagpu_ctx {
   HostBuf h_out;
   // generic forests / commitments / split square (trees.cpp, split.cpp)
   DevBuf t_leaf_data, t_leaves, t_inner, t_meta, t_out, t_status, t_flags;
-  // profiling
+  // profiling: per-kernel brackets (prof) and, for host-path calls, a stage
+  // timeline of the last call (stages_on; dagpu_profile_stages)
   bool prof = false;
+  bool stages_on = false;
+  static constexpr int kStages = DAGPU_STAGES;
+  hipEvent_t stage_ev[kStages] = {};
+  uint32_t stage_mask = 0;  // stages recorded by the last host-path call
   std::mutex prof_mu;
   std::vector<ProfRec> pending;
   std::vector<hipEvent_t> pool;
@@ -167,6 +172,12 @@ inline hipEvent_t pool_get(dagpu_ctx* c) {
   hipEvent_t e = nullptr;
   (void)hipEventCreate(&e);
   return e;
+}
+
+// Stage mark of a host-path call (see DAGPU_STAGE_* in dagpu.h).
+inline void stage_mark(dagpu_ctx* c, int i, hipStream_t s) {
+  if (!c->stages_on || !c->stage_ev[i]) return;
+  if (hipEventRecord(c->stage_ev[i], s) == hipSuccess) c->stage_mask |= 1u << i;
 }
 
 // RAII bracket: records events around one kernel launch when profiling is on.

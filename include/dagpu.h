@@ -190,6 +190,24 @@ int dagpu_repair_batch_device_ex(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* 
 int dagpu_profile_enable(dagpu_ctx* ctx, int on);
 int dagpu_profile_read(dagpu_ctx* ctx, double* total_ms, uint64_t* launches, int reset);
 
+/* Stage timeline of the last host-path extend call (dagpu_extend_shares /
+ * one-chunk dagpu_extend_batch) when dagpu_profile_enable(ctx, 2) is on:
+ * ms[i] = milliseconds from the call's first enqueue to stage i (HIP events on
+ * the compute stream, and on the copy stream for the EDS halves), -1 when the
+ * stage did not run.  For diagnosing single-call latency. */
+#define DAGPU_STAGES 10
+#define DAGPU_STAGE_START 0      /* before the ODS upload */
+#define DAGPU_STAGE_UPLOADED 1
+#define DAGPU_STAGE_ROWS 2       /* RS row pass done */
+#define DAGPU_STAGE_COLS 3       /* RS column pass done */
+#define DAGPU_STAGE_LEAVES 4
+#define DAGPU_STAGE_TREES 5
+#define DAGPU_STAGE_DAH 6
+#define DAGPU_STAGE_RESULTS 7    /* roots + DAH + status downloaded */
+#define DAGPU_STAGE_EDS_TOP 8    /* [Q0|Q1] halves downloaded (copy stream) */
+#define DAGPU_STAGE_EDS_BOTTOM 9 /* [Q2|Q3] halves downloaded (copy stream) */
+int dagpu_profile_stages(dagpu_ctx* ctx, float* ms);
+
 /* RFC-6962 root of rowRoots || colRoots (DataAvailabilityHeader.Hash,
  * pkg/da/data_availability_header.go:92-108), computed on the host side of the
  * boundary for small inputs (w = number of row roots; w == 0 gives the

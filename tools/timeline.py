@@ -18,6 +18,9 @@ rows.sort()
 step = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 per = int(sys.argv[3]) if len(sys.argv) > 3 else 48
 seg = rows[step * per:(step + 1) * per]
+if not seg:
+    n_steps = len(rows) // per if per else 0
+    sys.exit(f"step {step} is past the trace: {len(rows)} DA dispatches = {n_steps} steps of {per}")
 t0 = seg[0][0]
 end = max(r[1] for r in seg)
 busy = {}
