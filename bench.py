@@ -495,7 +495,9 @@ def bench_single(ctx, ks=(64, 128), calls=60, trace=True):
     """Drop-in latency of ONE square per call, as the production callers use it
     (app/process_proposal.go:147-161, app/prepare_proposal.go:95-107):
     dagpu_extend_shares from page-locked host shares, with eds_out NULL (roots +
-    DAH only) and with the whole EDS returned to page-locked host memory.
+    DAH only), with the whole EDS returned to page-locked host memory, and to
+    pageable memory (an ordinary Go slice: the copies then run after the kernel
+    chain is queued, synchronously on the calling thread).
     p50/p99 over `calls` calls after 5 warm-up calls, per k."""
     from celestia_da import _abi, da, synth
 
@@ -513,7 +515,9 @@ def bench_single(ctx, ks=(64, 128), calls=60, trace=True):
         dah = np.empty(32, np.uint8)
         r = {}
         stages = np.zeros(len(_abi.STAGES), np.float32)
-        for mode, eds_ptr in (("roots_only", 0), ("with_eds", edsb.ptr)):
+        pageable = np.empty(w * w * SHARE, np.uint8)  # an ordinary (Go-heap-like) caller buffer
+        pageable.fill(0)
+        for mode, eds_ptr in (("roots_only", 0), ("with_eds", edsb.ptr), ("with_eds_pageable", _abi.addr(pageable))):
             lat, tl = [], []
             for i in range(5 + calls):
                 t0 = time.perf_counter()

@@ -259,6 +259,28 @@ struct HostResults {
   }
 };
 
+// hipHostMalloc / hipHostRegister memory: device->host copies into it are
+// asynchronous DMA.  Into pageable memory they run synchronously on this thread.
+bool host_pinned(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+// Completion wait of a host-path call.  Calls that finish in about a
+// millisecond (single squares, the production callers' shape) spin on the
+// stream: the blocking wait's wake-up added up to 0.25 ms to single-square
+// calls (bench.py single_square stages, r03).
+hipError_t wait_stream(hipStream_t s, bool spin) {
+  if (!spin) return hipStreamSynchronize(s);
+  hipError_t e;
+  while ((e = hipStreamQuery(s)) == hipErrorNotReady) __builtin_ia32_pause();
+  return e;
+}
+
 // Runs one uniform-k group from host memory.  Caller holds ctx->mu.
 int run_group_host(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* ods, uint8_t* eds_out,
                    uint8_t* rr, uint8_t* cr, uint8_t* dah, int32_t* status) {
@@ -266,7 +288,8 @@ int run_group_host(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* ods, uin
   if (rc) return rc;
   const size_t m = pipeline_chunk(k, n);
   if (n > m) return run_group_pipelined(ctx, k, n, m, ods, eds_out, rr, cr, dah, status);
-  hipStream_t s = ctx->stream;
+  hipStream_t s = ctx->stream, cs = ctx->copy_stream;
+  const bool spin = eds_bytes(k) * n <= (size_t(64) << 20);
   HostResults res;
   HIP_TRY(ctx, ctx->ods.ensure(ods_bytes(k) * n));
   HIP_TRY(ctx, ctx->eds.ensure(eds_bytes(k) * n));
@@ -279,24 +302,25 @@ int run_group_host(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* ods, uin
   // An EDS requested back goes down on the copy stream while the kernels run:
   // the top halves ([Q0|Q1], final after the row pass) during the column pass
   // and the NMT kernels, the bottom halves ([Q2|Q3]) during the NMT kernels.
-  // The whole kernel chain and the results download are queued on `s` BEFORE
-  // the EDS copies: a device->host copy into pageable caller memory runs
-  // synchronously on this thread, and must not hold back the NMT launches.
+  // Into page-locked memory the copies are queued right after the RS passes,
+  // so the DMA starts as soon as the rows are final.  Into pageable memory a
+  // device->host copy runs synchronously on this thread, so there the whole
+  // kernel chain and the results download are queued first.
   rc = enqueue_rs(ctx, k, n, (const uint8_t*)ctx->ods.p, (uint8_t*)ctx->eds.p, s,
                   eds_out ? ctx->ev_loaded[0] : nullptr);
   if (rc) return rc;
   if (eds_out) HIP_TRY(ctx, hipEventRecord(ctx->ev_loaded[1], s));
-  rc = enqueue_roots(ctx, k, n, (const uint8_t*)ctx->eds.p, res.rr, res.cr, res.dah, res.st, ctx->ws.p, s);
-  if (rc) return rc;
-  HIP_TRY(ctx, res.download(ctx, s));
-  stage_mark(ctx, DAGPU_STAGE_RESULTS, s);
-  if (eds_out) {
-    hipStream_t cs = ctx->copy_stream;
-    // from here on DMA may be writing into eds_out: every return path waits for it
-    struct CopyJoin {
-      hipStream_t cs;
-      ~CopyJoin() { (void)hipStreamSynchronize(cs); }
-    } join{cs};
+  // from the first EDS copy on, DMA may be writing into eds_out: every return
+  // path waits for the copy stream
+  struct CopyJoin {
+    hipStream_t cs;
+    bool armed = false;
+    ~CopyJoin() {
+      if (armed) (void)hipStreamSynchronize(cs);
+    }
+  } join{cs};
+  auto eds_copies = [&]() -> int {
+    join.armed = true;
     const size_t eb = eds_bytes(k), half = eb / 2;
     HIP_TRY(ctx, hipStreamWaitEvent(cs, ctx->ev_loaded[0], 0));
     const uint8_t* d = (const uint8_t*)ctx->eds.p;
@@ -308,9 +332,20 @@ int run_group_host(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* ods, uin
       HIP_TRY(ctx, hipMemcpyAsync(eds_out + i * eb + half, d + i * eb + half, half,
                                   hipMemcpyDeviceToHost, cs));
     stage_mark(ctx, DAGPU_STAGE_EDS_BOTTOM, cs);
-    HIP_TRY(ctx, hipStreamSynchronize(cs));
+    return DAGPU_OK;
+  };
+  const bool early = eds_out && host_pinned(eds_out);
+  if (early && (rc = eds_copies())) return rc;
+  rc = enqueue_roots(ctx, k, n, (const uint8_t*)ctx->eds.p, res.rr, res.cr, res.dah, res.st, ctx->ws.p, s);
+  if (rc) return rc;
+  HIP_TRY(ctx, res.download(ctx, s));
+  stage_mark(ctx, DAGPU_STAGE_RESULTS, s);
+  if (eds_out && !early && (rc = eds_copies())) return rc;
+  if (eds_out) {
+    HIP_TRY(ctx, wait_stream(cs, spin));
+    join.armed = false;
   }
-  HIP_TRY(ctx, hipStreamSynchronize(s));
+  HIP_TRY(ctx, wait_stream(s, spin));
   std::vector<int32_t> st(n);
   res.deliver(ctx, rr, cr, dah, st.data());
   return finish_status(ctx, st.data(), n, status);

@@ -39,6 +39,9 @@ __device__ uint16_t g_log16[65536];
 __device__ uint16_t g_exp16[65536];
 __device__ uint16_t g_skew16[65536];
 __device__ uint16_t g_walsh16[65536];
+// Folded Walsh weights for the n-point error-locator transform (n = 2k =
+// 512, 1024): g_wfold16[n == 1024][r] = sum_q walsh[q*n + r] mod 65535.
+__device__ uint16_t g_wfold16[2][1024];
 
 __device__ __forceinline__ uint32_t mul16(uint32_t a, uint32_t lm) {
   if (a == 0) return 0;
@@ -227,6 +230,84 @@ __device__ void fwht65536(uint16_t* e) {
     }
     __syncthreads();
   }
+}
+
+// The same locators from n-point transforms (n = 2k <= 1024).  The erasure
+// vector is zero past n, so its 65536-point FWHT is n-periodic (popcount(i & j)
+// only sees the low log2(n) bits of j when i < n), and only the first n
+// outputs of the second transform are used, which sum the products over j = r
+// (mod n): out = FWHT_n(FWHT_n(e) * wfold), wfold[r] = sum_q walsh[q*n + r]
+// (mod 65535; a ring identity, so the values stay congruent to the reference's).
+// One 256-thread workgroup per vector, 2 x log4(n) radix-4 stages in 4 KiB of
+// LDS instead of 2 x 8 over 128 KiB (round 2: ~200 us per launch, set by the
+// one head vector of each square's erasure pattern).
+constexpr int kFoldThreads = 256;
+
+template <int N>
+__device__ __forceinline__ void fwht_n(uint32_t* e) {
+  int dist = 1;
+  if constexpr ((__builtin_ctz(N) & 1) != 0) {  // odd log2: one radix-2 stage first
+    for (int g = threadIdx.x; g < N / 2; g += kFoldThreads) {
+      const int i = 2 * g;
+      const uint32_t t0 = e[i], t1 = e[i + 1];
+      e[i] = add_mod16(t0, t1);
+      e[i + 1] = sub_mod16(t0, t1);
+    }
+    __syncthreads();
+    dist = 2;
+  }
+  for (; dist < N; dist <<= 2) {
+    const int dist4 = dist << 2;
+    for (int g = threadIdx.x; g < N / 4; g += kFoldThreads) {
+      const int r = (g / dist) * dist4;
+      const int i = r + (g % dist);
+      const uint32_t t0 = e[i], t1 = e[i + dist], t2 = e[i + 2 * dist], t3 = e[i + 3 * dist];
+      const uint32_t a0 = add_mod16(t0, t1), a1 = sub_mod16(t0, t1);
+      const uint32_t a2 = add_mod16(t2, t3), a3 = sub_mod16(t2, t3);
+      e[i] = add_mod16(a0, a2);
+      e[i + 2 * dist] = sub_mod16(a0, a2);
+      e[i + dist] = add_mod16(a1, a3);
+      e[i + 3 * dist] = sub_mod16(a1, a3);
+    }
+    __syncthreads();
+  }
+}
+
+template <int N>
+__global__ __launch_bounds__(kFoldThreads) void leo16_errlocs_fold_kernel(DecodeArgs a) {
+  __shared__ uint32_t e[N];
+  __shared__ int cnt_s;
+  const long v = blockIdx.x;
+  const long sq = v / a.nvec, vec = v % a.nvec;
+  constexpr int k = N / 2;
+  const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
+  if (threadIdx.x == 0) cnt_s = 0;
+  __syncthreads();
+  int cnt = 0;
+  for (int i = threadIdx.x; i < N; i += kFoldThreads) {
+    const uint32_t x = i < k ? (pres[(long)(k + i) * a.p_shard_stride] ? 0u : 1u)   // parity k+i -> work i
+                             : (pres[(long)(i - k) * a.p_shard_stride] ? 0u : 1u);  // data i-k -> work i
+    e[i] = x;
+    cnt += (x == 0);
+  }
+  atomicAdd(&cnt_s, cnt);
+  __syncthreads();
+  const int present = cnt_s;
+  const bool decode = present >= k && present < N && vec_selected(a, v);
+  if (threadIdx.x == 0) {
+    a.flags[v] = decode ? 1 : 0;
+    if (present < k && a.too_few) atomicOr(a.too_few, 1);
+    if (decode && a.ndecodable) atomicAdd(a.ndecodable, 1);
+  }
+  if (!decode) return;  // uniform
+  if (err_vec(a, v) != v) return;  // shares an earlier vector's locators
+  fwht_n<N>(e);
+  const uint16_t* wf = g_wfold16[N == 1024];
+  for (int i = threadIdx.x; i < N; i += kFoldThreads) e[i] = (e[i] * (uint32_t)wf[i]) % kMod16;
+  __syncthreads();
+  fwht_n<N>(e);
+  uint16_t* out = (uint16_t*)(a.err + v * (long)rs_err_bytes(k));
+  for (int i = threadIdx.x; i < N; i += kFoldThreads) out[i] = (uint16_t)e[i];
 }
 
 __global__ __launch_bounds__(kErrThreads) void leo16_errlocs_kernel(DecodeArgs a) {
@@ -1051,6 +1132,18 @@ hipError_t ensure_tables() {
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_exp16), t.exp.data(), 65536 * 2)) != hipSuccess) return e;
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_skew16), t.skew.data(), 65536 * 2)) != hipSuccess) return e;
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_walsh16), t.walsh.data(), 65536 * 2)) != hipSuccess) return e;
+  {
+    std::vector<uint16_t> wf(2 * 1024, 0);
+    for (int f = 0; f < 2; f++) {
+      const int n = f ? 1024 : 512;
+      for (int r = 0; r < n; r++) {
+        uint64_t acc = 0;
+        for (int q = 0; q < 65536 / n; q++) acc += t.walsh[(size_t)q * n + r];
+        wf[(size_t)f * 1024 + r] = (uint16_t)(acc % kMod16);
+      }
+    }
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_wfold16), wf.data(), wf.size() * 2)) != hipSuccess) return e;
+  }
   {  // per skew position: products of every 2-bit group value with skew[pos]
     std::vector<uint32_t> pt((size_t)kTabPos * 16, 0u);
     for (int pos = 0; pos < kTabPos; pos++) {
@@ -1117,7 +1210,12 @@ hipError_t launch_leo16_errlocs(const DecodeArgs& a, hipStream_t s) {
   if (e != hipSuccess) return e;
   const long nv = a.nsq * a.nvec;
   if (nv <= 0) return hipSuccess;
-  hipLaunchKernelGGL(leo16_errlocs_kernel, dim3((unsigned)nv), dim3(kErrThreads), kErrLds, s, a);
+  if (a.k == 256 && !getenv("DAGPU_ERRLOC_FULL"))
+    hipLaunchKernelGGL(leo16_errlocs_fold_kernel<512>, dim3((unsigned)nv), dim3(kFoldThreads), 0, s, a);
+  else if (a.k == 512 && !getenv("DAGPU_ERRLOC_FULL"))
+    hipLaunchKernelGGL(leo16_errlocs_fold_kernel<1024>, dim3((unsigned)nv), dim3(kFoldThreads), 0, s, a);
+  else  // DAGPU_ERRLOC_FULL=1: the 65536-point form (A/B and cross-check)
+    hipLaunchKernelGGL(leo16_errlocs_kernel, dim3((unsigned)nv), dim3(kErrThreads), kErrLds, s, a);
   return hipGetLastError();
 }
 
