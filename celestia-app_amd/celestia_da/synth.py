@@ -90,3 +90,24 @@ def tail_padding_square(k: int) -> np.ndarray:
     ns = b"\xff" * 28 + b"\xfe"
     share = ns + b"\x01" + b"\x00" * 4 + b"\x00" * (SHARE - 34)
     return np.tile(np.frombuffer(share, np.uint8), (k * k, 1))
+
+
+def block_txs(n_normal: int, n_blob: int, seed: int, normal_size: int = 300,
+              blob_sizes=(1500, 3000), n_namespaces: int = 64):
+    """A synthetic block for square construction (pkg/square): n_normal random
+    txs of normal_size bytes, then n_blob BlobTx protos (pkg/blob/blob.go wire
+    format) with one blob each, data sizes uniform in blob_sizes, namespaces
+    drawn from n_namespaces version-0 IDs.  The PFB tx inside each BlobTx is a
+    stand-in of the signed MsgPayForBlobs the reference would carry (only its
+    length affects the layout): b"PFB" | 1 | varint(size), zero padded to 330 B."""
+    import random
+
+    from . import blobtx, shares
+    rng = random.Random(seed)
+    txs = [rng.randbytes(normal_size) for _ in range(n_normal)]
+    nss = sorted(shares.new_namespace_v0(rng.randbytes(10)) for _ in range(n_namespaces))
+    for i in range(n_blob):
+        data = rng.randbytes(rng.randrange(blob_sizes[0], blob_sizes[1]))
+        pfb = (b"PFB\x01" + shares.put_uvarint(len(data))).ljust(330, b"\x00")
+        txs.append(blobtx.marshal_blob_tx(pfb, shares.Blob.new(nss[i % n_namespaces], data)))
+    return txs
