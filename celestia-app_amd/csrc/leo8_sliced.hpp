@@ -166,8 +166,117 @@ __host__ __device__ __forceinline__ uint32_t xor_row(uint32_t acc, const uint32_
   }
 }
 template <int C>
-__host__ __device__ __forceinline__ void muladd_ct(uint32_t (&x)[8], const uint32_t (&y)[8]) {
+__host__ __device__ __forceinline__ void muladd_ct_rows(uint32_t (&x)[8], const uint32_t (&y)[8]) {
   static_for<8>([&](auto i) { x[i] = xor_row<kMat.row[C][i], 0>(x[i], y); });
+}
+
+// Shared XOR subexpressions for x ^= C * y (round 3).  Row by row the product
+// costs sum_i ceil(|row_i| / 2) three-input XORs (acc + two planes each): 17.9
+// on average over the encoder's skews.  A plane triple (or pair) that several
+// rows contain can be XOR-ed once into a temporary that those rows then take
+// as one term; make_slp extracts them greedily (largest saving first, temps
+// may contain temps) at compile time: 13.9 per multiply on average.  Symbols
+// 0..7 are the planes y[j], 8.. the temporaries.
+struct Slp {
+  int ntmp;
+  int8_t tmp[8][3];   // operands of temp t (-1 = none: a pair)
+  int nterm[8];
+  int8_t term[8][16];
+};
+// acc: rows accumulate into x (row cost ceil(n / 2)); otherwise they are
+// summed from scratch (cost floor(n / 2): the first term starts the sum).
+constexpr int slp_row_cost(int n, bool acc) { return acc ? (n + 1) / 2 : n / 2; }
+constexpr Slp make_slp(int c, bool acc) {
+  Slp p{};
+  bool has[8][16] = {};
+  for (int i = 0; i < 8; i++)
+    for (int j = 0; j < 8; j++) has[i][j] = (kMat.row[c][i] >> j) & 1;
+  int nsym = 8;
+  auto cnt = [&](int i) {
+    int n = 0;
+    for (int s = 0; s < nsym; s++) n += has[i][s];
+    return n;
+  };
+  while (nsym < 16) {
+    int best = 0, ba = -1, bb = -1, bc = -1;
+    for (int a = 0; a < nsym; a++)
+      for (int b = a + 1; b < nsym; b++)
+        for (int c3 = b; c3 <= nsym; c3++) {  // c3 == nsym: the pair (a, b)
+          const bool pair = c3 == nsym;
+          if (!pair && c3 == b) continue;
+          const int len = pair ? 2 : 3;
+          int sav = -1;  // the temporary's own op
+          for (int i = 0; i < 8; i++) {
+            if (!(has[i][a] && has[i][b] && (pair || has[i][c3]))) continue;
+            const int n = cnt(i);
+            sav += slp_row_cost(n, acc) - slp_row_cost(n - len + 1, acc);
+          }
+          if (sav > best) {
+            best = sav;
+            ba = a;
+            bb = b;
+            bc = pair ? -1 : c3;
+          }
+        }
+    if (best <= 0) break;
+    const int t = nsym - 8;
+    p.tmp[t][0] = (int8_t)ba;
+    p.tmp[t][1] = (int8_t)bb;
+    p.tmp[t][2] = (int8_t)bc;
+    for (int i = 0; i < 8; i++) {
+      if (!(has[i][ba] && has[i][bb] && (bc < 0 || has[i][bc]))) continue;
+      has[i][ba] = has[i][bb] = false;
+      if (bc >= 0) has[i][bc] = false;
+      has[i][nsym] = true;
+    }
+    nsym++;
+  }
+  p.ntmp = nsym - 8;
+  for (int i = 0; i < 8; i++) {
+    p.nterm[i] = 0;
+    for (int s = 0; s < nsym; s++)
+      if (has[i][s]) p.term[i][p.nterm[i]++] = (int8_t)s;
+  }
+  return p;
+}
+template <int C, bool ACC = true>
+struct SlpOf {
+  static constexpr Slp v = make_slp(C, ACC);
+};
+
+#ifndef DAGPU_SLP
+#define DAGPU_SLP 1  // 0: row-by-row products (A/B builds)
+#endif
+template <int C>
+__host__ __device__ __forceinline__ void muladd_ct(uint32_t (&x)[8], const uint32_t (&y)[8]) {
+  if constexpr (!DAGPU_SLP || C == 0) {
+    muladd_ct_rows<C>(x, y);
+  } else {
+    constexpr Slp P = SlpOf<C>::v;
+    uint32_t sym[8 + 8];
+    static_for<8>([&](auto j) { sym[j] = y[j]; });
+    static_for<8>([&](auto t) {
+      if constexpr (t < P.ntmp) {
+        constexpr int a = P.tmp[t][0], b = P.tmp[t][1], c3 = P.tmp[t][2];
+        if constexpr (c3 < 0) sym[8 + t] = sym[a] ^ sym[b];
+        else sym[8 + t] = SL_BOP3(sym[a], sym[b], sym[c3], kXor3);
+      }
+    });
+    static_for<8>([&](auto i) {
+      constexpr int n = P.nterm[i];
+      uint32_t acc = x[i];
+      static_for<(n + 1) / 2>([&](auto q) {
+        constexpr int t0 = P.term[i][2 * q];
+        if constexpr (2 * q + 1 < n) {
+          constexpr int t1 = P.term[i][2 * q + 1];
+          acc = SL_BOP3(acc, sym[t0], sym[t1], kXor3);
+        } else {
+          acc ^= sym[t0];
+        }
+      });
+      x[i] = acc;
+    });
+  }
 }
 
 // x ^= (C ^ W) * y: C compile-time, W given by its 64 masks (wave-uniform)
@@ -306,10 +415,39 @@ __host__ __device__ __forceinline__ uint32_t row_sum(const uint32_t (&y)[8]) {
 // output plane on top of the row sums (cheaper than masking the 8 inputs).
 template <int C>
 __host__ __device__ __forceinline__ void muladd_ct_lane(uint32_t (&x)[8], const uint32_t (&y)[8], uint32_t mask) {
-  static_for<8>([&](auto i) {
-    constexpr int R = kMat.row[C][i];
-    if constexpr (R != 0) x[i] = SL_BOP3(x[i], row_sum<R>(y), mask, kXorAnd);
-  });
+  if constexpr (!DAGPU_SLP || C == 0) {
+    static_for<8>([&](auto i) {
+      constexpr int R = kMat.row[C][i];
+      if constexpr (R != 0) x[i] = SL_BOP3(x[i], row_sum<R>(y), mask, kXorAnd);
+    });
+  } else {  // row sums from scratch over shared temporaries (SlpOf<C, false>)
+    constexpr Slp P = SlpOf<C, false>::v;
+    uint32_t sym[8 + 8];
+    static_for<8>([&](auto j) { sym[j] = y[j]; });
+    static_for<8>([&](auto t) {
+      if constexpr (t < P.ntmp) {
+        constexpr int a = P.tmp[t][0], b = P.tmp[t][1], c3 = P.tmp[t][2];
+        if constexpr (c3 < 0) sym[8 + t] = sym[a] ^ sym[b];
+        else sym[8 + t] = SL_BOP3(sym[a], sym[b], sym[c3], kXor3);
+      }
+    });
+    static_for<8>([&](auto i) {
+      constexpr int n = P.nterm[i];
+      if constexpr (n > 0) {
+        uint32_t sum = sym[P.term[i][0]];
+        static_for<n / 2>([&](auto q) {
+          constexpr int t0 = P.term[i][1 + 2 * q];
+          if constexpr (2 * q + 2 < n) {
+            constexpr int t1 = P.term[i][2 + 2 * q];
+            sum = SL_BOP3(sum, sym[t0], sym[t1], kXor3);
+          } else {
+            sum ^= sym[t0];
+          }
+        });
+        x[i] = SL_BOP3(x[i], sum, mask, kXorAnd);
+      }
+    });
+  }
 }
 
 // IFFT layers 0..NL-1 in the two-vector layout A (K = 128), wave w, lane mask of eb.

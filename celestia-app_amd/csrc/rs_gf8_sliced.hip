@@ -275,6 +275,17 @@ void leo8_encode_sliced2_kernel(EncodeArgs a) {
   __syncthreads();  // other waves' last exchange reads of this wave's quarter are done
   transpose_wave2<false>(v, lds, w, eb, col);
   fft_A2<K, 1>(v, w, ebmask);
+#if defined(DAGPU_RS_PAD) && DAGPU_RS_PAD > 0
+  {  // A/B instrument only: DAGPU_RS_PAD x 128 extra fast-class VALU ops per lane, results unchanged
+    const uint32_t z = __builtin_amdgcn_readfirstlane((uint32_t)(a.nchunk - 1));  // 0 at run time
+#pragma unroll
+    for (int r = 0; r < DAGPU_RS_PAD; r++)
+#pragma unroll
+      for (int j = 0; j < 16; j++)
+#pragma unroll
+        for (int p = 0; p < 8; p++) v[j][p] ^= z * (uint32_t)(2654435761u * (r + 1) + 97u * j + p);
+  }
+#endif
 
 #pragma unroll
   for (int j = 0; j < 16; j++) transpose8(v[j]);
