@@ -450,10 +450,45 @@ __host__ __device__ __forceinline__ void muladd_ct_lane(uint32_t (&x)[8], const 
   }
 }
 
+#ifndef DAGPU_WSPEC
+#define DAGPU_WSPEC 1  // 0: wave terms as uniform branches around extra multiplies (A/B builds)
+#endif
+// f(integral_constant<W>) for the wave-uniform index w in 0..3: the wave bits of
+// a layout-A skew then fold into the compile-time element, one multiply per
+// butterfly on every wave (the branch form costs popcount(w) extra multiplies,
+// and the workgroup waits at its barriers for wave 3).
+template <typename F>
+__host__ __device__ __forceinline__ void wave_switch4(int w, F&& f) {
+  switch (w) {
+    case 0: f(std::integral_constant<int, 0>{}); break;
+    case 1: f(std::integral_constant<int, 1>{}); break;
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    default: f(std::integral_constant<int, 3>{}); break;
+  }
+}
+
 // IFFT layers 0..NL-1 in the two-vector layout A (K = 128), wave w, lane mask of eb.
 template <int K, int NL = 3>
 __host__ __device__ __forceinline__ void ifft_A2(uint32_t (&v)[16][8], int w, uint32_t ebmask) {
   static_assert(K == 128, "two-vector layout: k = 128");
+  if constexpr (DAGPU_WSPEC) {
+    static_for<NL>([&](auto m) {
+      constexpr int D = 1 << m;
+      SL_FENCE();
+      static_for<16>([&](auto j) {
+        if constexpr (!(j & D)) xor8(v[j + D], v[j]);
+      });
+      wave_switch4(w, [&](auto W) {
+        static_for<16>([&](auto j) {
+          if constexpr (!(j & D)) muladd_ct<skew_elem(D - 1 + K + (j & ~(2 * D - 1)) + 32 * W)>(v[j], v[j + D]);
+        });
+      });
+      static_for<16>([&](auto j) {
+        if constexpr (!(j & D)) muladd_ct_lane<skew_elem(D - 1 + 16)>(v[j], v[j + D], ebmask);
+      });
+    });
+    return;
+  }
   static_for<NL>([&](auto m) {
     constexpr int D = 1 << m;
     SL_FENCE();
@@ -484,6 +519,25 @@ __host__ __device__ __forceinline__ void ifft_A2(uint32_t (&v)[16][8], int w, ui
 template <int K, int NL = 3>
 __host__ __device__ __forceinline__ void fft_A2(uint32_t (&v)[16][8], int w, uint32_t ebmask) {
   static_assert(K == 128, "two-vector layout: k = 128");
+  if constexpr (DAGPU_WSPEC) {
+    static_for<NL>([&](auto mm) {
+      constexpr int m = NL - 1 - mm;
+      constexpr int D = 1 << m;
+      SL_FENCE();
+      wave_switch4(w, [&](auto W) {
+        static_for<16>([&](auto j) {
+          if constexpr (!(j & D)) muladd_ct<skew_elem(D - 1 + (j & ~(2 * D - 1)) + 32 * W)>(v[j], v[j + D]);
+        });
+      });
+      static_for<16>([&](auto j) {
+        if constexpr (!(j & D)) muladd_ct_lane<skew_elem(D - 1 + 16)>(v[j], v[j + D], ebmask);
+      });
+      static_for<16>([&](auto j) {
+        if constexpr (!(j & D)) xor8(v[j + D], v[j]);
+      });
+    });
+    return;
+  }
   static_for<NL>([&](auto mm) {
     constexpr int m = NL - 1 - mm;
     constexpr int D = 1 << m;
@@ -518,6 +572,22 @@ __host__ __device__ __forceinline__ void fft_A2(uint32_t (&v)[16][8], int w, uin
 template <int K>
 __host__ __device__ __forceinline__ void ifft_As2(uint32_t (&v)[16][8], int w) {
   static_assert(K == 128, "two-vector layout: k = 128");
+  if constexpr (DAGPU_WSPEC) {
+    static_for<2>([&](auto mm) {
+      constexpr int m = 1 + mm;
+      constexpr int D = 1 << m, R = D >> 1;
+      SL_FENCE();
+      static_for<16>([&](auto r) {
+        if constexpr (!(r & R)) xor8(v[r + R], v[r]);
+      });
+      wave_switch4(w, [&](auto W) {
+        static_for<16>([&](auto r) {
+          if constexpr (!(r & R)) muladd_ct<skew_elem(D - 1 + K + ((2 * r) & ~(2 * D - 1)) + 32 * W)>(v[r], v[r + R]);
+        });
+      });
+    });
+    return;
+  }
   static_for<2>([&](auto mm) {
     constexpr int m = 1 + mm;
     constexpr int D = 1 << m, R = D >> 1;
@@ -545,6 +615,22 @@ __host__ __device__ __forceinline__ void ifft_As2(uint32_t (&v)[16][8], int w) {
 template <int K>
 __host__ __device__ __forceinline__ void fft_As2(uint32_t (&v)[16][8], int w) {
   static_assert(K == 128, "two-vector layout: k = 128");
+  if constexpr (DAGPU_WSPEC) {
+    static_for<2>([&](auto mm) {
+      constexpr int m = 2 - mm;
+      constexpr int D = 1 << m, R = D >> 1;
+      SL_FENCE();
+      wave_switch4(w, [&](auto W) {
+        static_for<16>([&](auto r) {
+          if constexpr (!(r & R)) muladd_ct<skew_elem(D - 1 + ((2 * r) & ~(2 * D - 1)) + 32 * W)>(v[r], v[r + R]);
+        });
+      });
+      static_for<16>([&](auto r) {
+        if constexpr (!(r & R)) xor8(v[r + R], v[r]);
+      });
+    });
+    return;
+  }
   static_for<2>([&](auto mm) {
     constexpr int m = 2 - mm;
     constexpr int D = 1 << m, R = D >> 1;
@@ -586,6 +672,35 @@ __host__ __device__ __forceinline__ void fft_As2(uint32_t (&v)[16][8], int w) {
 // IFFT butterfly (ifftDIT8): y ^= x; x ^= skew * y.  FFT (fftDIT8): x ^= skew * y; y ^= x.
 template <bool IFFT, int NL>
 __host__ __device__ __forceinline__ void dec_A(uint32_t (&v)[16][8], int w, uint32_t eb0mask, uint32_t eb1mask) {
+  if constexpr (DAGPU_WSPEC) {
+    static_for<NL>([&](auto mm) {
+      constexpr int m = IFFT ? (int)mm : NL - 1 - (int)mm;
+      constexpr int D = 1 << m;
+      SL_FENCE();
+      if constexpr (IFFT) {
+        static_for<16>([&](auto j) {
+          if constexpr (!(j & D)) xor8(v[j + D], v[j]);
+        });
+      }
+      wave_switch4(w, [&](auto W) {
+        static_for<16>([&](auto j) {
+          if constexpr (!(j & D)) muladd_ct<skew_elem(D - 1 + (j & ~(2 * D - 1)) + 64 * W)>(v[j], v[j + D]);
+        });
+      });
+      static_for<16>([&](auto j) {
+        if constexpr (!(j & D)) muladd_ct_lane<skew_elem(D - 1 + 16)>(v[j], v[j + D], eb0mask);
+      });
+      static_for<16>([&](auto j) {
+        if constexpr (!(j & D)) muladd_ct_lane<skew_elem(D - 1 + 32)>(v[j], v[j + D], eb1mask);
+      });
+      if constexpr (!IFFT) {
+        static_for<16>([&](auto j) {
+          if constexpr (!(j & D)) xor8(v[j + D], v[j]);
+        });
+      }
+    });
+    return;
+  }
   static_for<NL>([&](auto mm) {
     constexpr int m = IFFT ? (int)mm : NL - 1 - (int)mm;
     constexpr int D = 1 << m;
@@ -626,6 +741,29 @@ __host__ __device__ __forceinline__ void dec_A(uint32_t (&v)[16][8], int w, uint
 // block start b = 4 (r with register bits <= m - 2 cleared) + 64 w.
 template <bool IFFT>
 __host__ __device__ __forceinline__ void dec_Astar(uint32_t (&v)[16][8], int w) {
+  if constexpr (DAGPU_WSPEC) {
+    static_for<2>([&](auto mm) {
+      constexpr int rb = IFFT ? (int)mm : 1 - (int)mm;
+      constexpr int D = 4 << rb, R = 1 << rb;
+      SL_FENCE();
+      if constexpr (IFFT) {
+        static_for<16>([&](auto r) {
+          if constexpr (!(r & R)) xor8(v[r + R], v[r]);
+        });
+      }
+      wave_switch4(w, [&](auto W) {
+        static_for<16>([&](auto r) {
+          if constexpr (!(r & R)) muladd_ct<skew_elem(D - 1 + 4 * (r & ~(2 * R - 1)) + 64 * W)>(v[r], v[r + R]);
+        });
+      });
+      if constexpr (!IFFT) {
+        static_for<16>([&](auto r) {
+          if constexpr (!(r & R)) xor8(v[r + R], v[r]);
+        });
+      }
+    });
+    return;
+  }
   static_for<2>([&](auto mm) {
     constexpr int rb = IFFT ? (int)mm : 1 - (int)mm;
     constexpr int D = 4 << rb, R = 1 << rb;
