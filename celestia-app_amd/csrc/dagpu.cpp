@@ -15,6 +15,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <cmath>
 #include <map>
 #include <mutex>
@@ -401,9 +402,13 @@ void dagpu_destroy(dagpu_ctx* c) {
   }
   for (auto e : c->stage_ev)
     if (e) (void)hipEventDestroy(e);
-  for (auto& cs : c->side) (void)hipStreamSynchronize(cs.second);
+  for (auto& cs : c->side)
+    for (hipStream_t x : {cs.rs, cs.rs_hi, cs.nmt})
+      if (x) (void)hipStreamSynchronize(x);
   for (auto e : c->ev_pool) (void)hipEventDestroy(e);
-  for (auto& cs : c->side) (void)hipStreamDestroy(cs.second);
+  for (auto& cs : c->side)
+    for (hipStream_t x : {cs.rs, cs.rs_hi, cs.nmt})
+      if (x) (void)hipStreamDestroy(x);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -567,21 +572,41 @@ size_t pipe_slices(dagpu_ctx* ctx, uint32_t k, size_t n) {
   return s < 1 ? 1 : s;
 }
 
-// The RS side stream paired with caller stream `s` (created on first use).
-hipStream_t side_stream(dagpu_ctx* ctx, hipStream_t s) {
+// The side streams paired with caller stream `s` (created on first use).
+// which: 0 = RS, 1 = RS at the device's greatest stream priority, 2 = NMT.
+hipStream_t side_stream(dagpu_ctx* ctx, hipStream_t s, int which = 0) {
   std::lock_guard<std::mutex> g(ctx->side_mu);
+  dagpu_ctx::Side* sd = nullptr;
   for (auto& p : ctx->side)
-    if (p.first == s) return p.second;
-  if (ctx->side.size() >= dagpu_ctx::kMaxSideStreams) {
-    // more caller streams than side streams: share them round-robin (the
-    // callers then serialise their RS slices, results are unaffected)
-    const size_t i = (size_t)((((uint64_t)(uintptr_t)s) * 0x9E3779B97F4A7C15ull) >> 32) % ctx->side.size();
-    return ctx->side[i].second;
+    if (p.caller == s) sd = &p;
+  if (!sd) {
+    if (ctx->side.size() >= dagpu_ctx::kMaxSideStreams) {
+      // more caller streams than side streams: share them round-robin (the
+      // callers then serialise their side work, results are unaffected)
+      const size_t i = (size_t)((((uint64_t)(uintptr_t)s) * 0x9E3779B97F4A7C15ull) >> 32) % ctx->side.size();
+      sd = &ctx->side[i];
+    } else {
+      ctx->side.emplace_back();
+      sd = &ctx->side.back();
+      sd->caller = s;
+    }
   }
-  hipStream_t side = nullptr;
-  if (hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess) return nullptr;
-  ctx->side.emplace_back(s, side);
-  return side;
+  hipStream_t* slot = which == 0 ? &sd->rs : which == 1 ? &sd->rs_hi : &sd->nmt;
+  if (!*slot) {
+    hipError_t e;
+    if (which == 1) {
+      int lo = 0, hi = 0;
+      (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+      e = hipStreamCreateWithPriority(slot, hipStreamNonBlocking, hi);
+    } else {
+      e = hipStreamCreateWithFlags(slot, hipStreamNonBlocking);
+    }
+    if (e != hipSuccess) {
+      *slot = nullptr;
+      return nullptr;
+    }
+  }
+  return *slot;
 }
 
 }  // namespace
@@ -612,7 +637,7 @@ int dagpu_extend_batch_device(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_
     for (auto x : ev) ev_give(ctx, x);
     return r;
   };
-  hipStream_t rs = side_stream(ctx, s);
+  hipStream_t rs = side_stream(ctx, s, env_long("DAGPU_RS_PRIO") > 0 ? 1 : 0);
   if (!rs) return done(set_err(ctx, DAGPU_ERR_DEVICE, "hipStreamCreate failed"));
   const size_t w = 2 * (size_t)k;
   if (hipEventRecord(ev[S], s) != hipSuccess || hipStreamWaitEvent(rs, ev[S], 0) != hipSuccess)
@@ -634,17 +659,42 @@ int dagpu_extend_batch_device(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_
     if (rc) return done(rc);
     if (hipEventRecord(ev[i], rs) != hipSuccess) return done(set_err(ctx, DAGPU_ERR_DEVICE, "hipEventRecord failed"));
   }
-  // the slices' NMT work runs in order on the caller's stream and shares the
-  // front of the workspace; waiting on the last slice's event also joins the side stream
+  // NMT work of the slices: in order on the caller's stream, sharing the front
+  // of the workspace; or (DAGPU_PIPE_NMT2) odd slices on a second NMT stream
+  // with the workspace's second half, so the latency-bound tree levels and DAH
+  // of one slice overlap the leaves of the next.  Waiting on the last slice's
+  // event joins the RS stream; the NMT stream is joined with one more event.
+  size_t maxs = 0;
+  for (size_t i = 0; i < S; i++) maxs = std::max(maxs, cut[i + 1] - cut[i]);
+  const size_t ws_half = (nmt_workspace_bytes((int)k, (long)maxs) + 255) & ~(size_t)255;
+  hipStream_t nmt2 = nullptr;
+  if (env_long("DAGPU_PIPE_NMT2") > 0 && 2 * ws_half + 256 <= dagpu_workspace_size(k, n)) {
+    nmt2 = side_stream(ctx, s, 2);
+    if (!nmt2) return done(set_err(ctx, DAGPU_ERR_DEVICE, "hipStreamCreate failed"));
+  }
+  hipEvent_t ev_join = nullptr;
+  if (nmt2 && !(ev_join = ev_take(ctx)))
+    return done(set_err(ctx, DAGPU_ERR_DEVICE, "hipEventCreate failed"));
+  auto done2 = [&](int r) {
+    ev_give(ctx, ev_join);
+    return done(r);
+  };
   for (size_t i = 0; i < S; i++) {
     const size_t a = cut[i], b = cut[i + 1];
-    if (hipStreamWaitEvent(s, ev[i], 0) != hipSuccess)
-      return done(set_err(ctx, DAGPU_ERR_DEVICE, "hipStreamWaitEvent failed"));
+    const bool alt = nmt2 && (i & 1);
+    hipStream_t ns = alt ? nmt2 : s;
+    if (hipStreamWaitEvent(ns, ev[i], 0) != hipSuccess)
+      return done2(set_err(ctx, DAGPU_ERR_DEVICE, "hipStreamWaitEvent failed"));
     rc = enqueue_roots(ctx, k, b - a, d_eds + a * eds_bytes(k), d_row_roots + a * w * kNodeSize,
-                       d_col_roots + a * w * kNodeSize, d_dah + a * 32, d_status + a, d_workspace, s);
-    if (rc) return done(rc);
+                       d_col_roots + a * w * kNodeSize, d_dah + a * 32, d_status + a,
+                       (uint8_t*)d_workspace + (alt ? ws_half : 0), ns);
+    if (rc) return done2(rc);
   }
-  return done(DAGPU_OK);
+  if (nmt2) {
+    if (hipEventRecord(ev_join, nmt2) != hipSuccess || hipStreamWaitEvent(s, ev_join, 0) != hipSuccess)
+      return done2(set_err(ctx, DAGPU_ERR_DEVICE, "pipeline join failed"));
+  }
+  return done2(DAGPU_OK);
 }
 
 int dagpu_roots(dagpu_ctx* ctx, uint32_t k, const uint8_t* eds, uint8_t* row_roots,

@@ -84,9 +84,15 @@ struct dagpu_ctx {
   // stream.  One side stream per caller stream (up to kMaxSideStreams, then
   // callers share them round-robin), so concurrent callers on different streams
   // do not queue their RS slices behind each other.
+  // Each caller stream also gets a second NMT stream (slices alternate between
+  // it and the caller's stream, so the tree levels and DAH of slice i, which
+  // fill few CUs, overlap the leaves of slice i+1) and a high-priority RS stream.
   static constexpr size_t kMaxSideStreams = 16;
+  struct Side {
+    hipStream_t caller = nullptr, rs = nullptr, rs_hi = nullptr, nmt = nullptr;
+  };
   std::mutex side_mu;
-  std::vector<std::pair<hipStream_t, hipStream_t>> side;  // caller -> side stream
+  std::vector<Side> side;
   std::mutex ev_mu;
   std::vector<hipEvent_t> ev_pool;  // timing-disabled events, recycled per call
   hipEvent_t ev_loaded[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
