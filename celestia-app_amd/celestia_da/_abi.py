@@ -85,7 +85,7 @@ PREFIX_SELF = 1
 PREFIX_PARITY = 2
 PREFIX_FLAGS = 3
 
-PROFILE_KERNELS = ("rs_row", "rs_col", "nmt_leaves", "nmt_trees", "dah", "decode")
+PROFILE_KERNELS = ("rs_row", "rs_col", "nmt_leaves", "nmt_trees", "dah", "decode", "repair_fill")
 # dagpu_profile_stages (include/dagpu.h DAGPU_STAGE_*)
 STAGES = ("start", "uploaded", "rs_rows", "rs_cols", "leaves", "trees", "dah", "results", "eds_top", "eds_bottom")
 

@@ -789,7 +789,7 @@ int dagpu_decode(dagpu_ctx* ctx, uint32_t k, size_t nvec, size_t shard_size, uin
   da.err = (uint8_t*)ctx->ws.p;
   da.flags = (int32_t*)((uint8_t*)ctx->ws.p + errb);
   // locator sharing runs one workgroup over all vectors of a "square" (<= 1024)
-  da.err_same = nvec <= 1024 ? da.flags + nvec : nullptr;
+  da.err_key = nvec <= 1024 ? da.flags + nvec : nullptr;
   da.err_head = nvec <= 1024 ? da.flags + 2 * nvec : nullptr;
   da.too_few = (int32_t*)ctx->status.p;
   da.nsq = 1;
@@ -825,7 +825,15 @@ struct RepairWs {
   int32_t* err_share[2][2];  // [axis][same, head]
   int32_t* sel;         // exact-order repair: level of each axis' attempt, [2][w]
   int32_t* bits;
-  int32_t* counters;    // [0] decodable rows, [1] decodable cols
+  int32_t* counters;    // [0] decodable rows, [1] decodable cols, [2] deferred, [3] fill pairs
+  // fill route / deferral (repair.hip PlanArgs)
+  int32_t* fill;        // [sq][idx] of the round's axis
+  int32_t* pair_list;   // k = 128 fill pairs, n * w entries
+  int32_t* known;       // [axis][sq][idx]
+  int32_t* deferred;    // [axis][sq][idx]
+  int32_t* nodefer;     // [sq]
+  int32_t* check;       // [sq]: a deferred axis is not a codeword
+  int32_t* counts[2];   // [axis] vec_counts: present data shards | present shards << 16
 };
 
 size_t a256(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -837,9 +845,11 @@ size_t repair_ws_bytes(uint32_t k, size_t n) {
   t += a256(n * w * w);                                           // p0
   t += 4 * a256(n * 2 * w * 4);                                   // complete before/now, root/parity bad
   t += 2 * a256(n * w * rs_err_bytes((int)k)) + 2 * a256(n * w * 4);  // err, flags
-  t += 4 * a256(n * w * 4);                                             // err_same, err_head per axis
+  t += 4 * a256(n * w * 4);                                             // err_key, err_head per axis
   t += a256(2 * w * 4);                                                 // sel
   t += a256(n * 4) + 256;                                         // bits, counters
+  t += 2 * a256(n * w * 4) + 2 * a256(n * 2 * w * 4) + 2 * a256(n * 4);  // fill, pairs, known, deferred, nodefer, check
+  t += 2 * a256(n * w * 4);                                                 // counts
   return t;
 }
 
@@ -871,7 +881,15 @@ RepairWs carve_repair(uint32_t k, size_t n, void* base) {
     }
   r.sel = (int32_t*)p; p += a256(2 * w * 4);
   r.bits = (int32_t*)p; p += a256(n * 4);
-  r.counters = (int32_t*)p;
+  r.counters = (int32_t*)p; p += 256;
+  r.fill = (int32_t*)p; p += a256(n * w * 4);
+  r.pair_list = (int32_t*)p; p += a256(n * w * 4);
+  r.known = (int32_t*)p; p += a256(n * 2 * w * 4);
+  r.deferred = (int32_t*)p; p += a256(n * 2 * w * 4);
+  r.nodefer = (int32_t*)p; p += a256(n * 4);
+  r.check = (int32_t*)p; p += a256(n * 4);
+  r.counts[0] = (int32_t*)p; p += a256(n * w * 4);
+  r.counts[1] = (int32_t*)p;
   return r;
 }
 
@@ -892,7 +910,7 @@ DecodeArgs axis_decode_args(uint32_t k, size_t n, uint8_t* eds, uint8_t* present
     d.p_vec_stride = 1; d.p_shard_stride = w;
     d.err = r.err_cols; d.flags = r.flags_cols; d.ndecodable = r.counters + 1;
   }
-  d.err_same = r.err_share[axis][0];
+  d.err_key = r.err_share[axis][0];
   d.err_head = r.err_share[axis][1];
   d.nsq = (long)n;
   d.nvec = w;
@@ -1011,7 +1029,7 @@ int exact_repair(dagpu_ctx* ctx, uint32_t k, size_t n, size_t sq, uint8_t* d_eds
     for (int ax = 0; ax < 2; ax++) {
       if (!has[2 * (size_t)L + ax]) continue;
       DecodeArgs d = axis_decode_args(k, 1, eds, pres, ax, r);
-      d.err_same = d.err_head = nullptr;
+      d.err_key = d.err_head = nullptr;
       d.ndecodable = nullptr;
       d.sel_level = r.sel + (size_t)ax * w;
       d.sel_value = L;
@@ -1101,19 +1119,137 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
   }
   // solveCrossword: each round rebuilds every decodable row or every decodable
   // column (whichever set is larger) until no axis can make progress.
+  // Fill route and deferral (repair.hip PlanArgs; DAGPU_REPAIR_FILL=0 turns
+  // them off): a decodable vector whose data half is complete is re-encoded
+  // instead of decoded; when every vector i < k of an axis is decodable or
+  // complete, the decodes of i >= k wait and the next round (the other axis)
+  // fills everything.  For the maximal erasure pattern that is k row decodes,
+  // k column decodes and k row fills instead of k + 2k decodes.  A deferred
+  // vector the decoder would have rebuilt is the same codeword whenever the
+  // square ends up a codeword square, which the known[] bookkeeping proves for
+  // that pattern; otherwise a compare-mode encode checks every deferred vector,
+  // and a square that fails is re-run from its original presence without
+  // deferral (the decoders read present shards only).
+  const char* fill_env = getenv("DAGPU_REPAIR_FILL");  // read per call (tests compare both)
+  const bool shortcut = !(fill_env && fill_env[0] == '0');
+  const bool fill_list = k == 128;
+  if (shortcut) {
+    HIP_TRY(ctx, hipMemcpyAsync(r.known, r.complete_before, n * 2 * w * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+    HIP_TRY(ctx, hipMemsetAsync(r.deferred, 0, n * 2 * w * sizeof(int32_t), s));
+    HIP_TRY(ctx, hipMemsetAsync(r.nodefer, 0, n * sizeof(int32_t), s));
+    HIP_TRY(ctx, hipMemsetAsync(r.counters, 0, 4 * sizeof(int32_t), s));
+  }
   const int max_rounds = 4 * (int)w + 4;
-  for (int round = 0; round < max_rounds; round++) {
-    DecodeArgs dr = axis_decode_args(k, n, d_eds, d_present, 0, r);
-    DecodeArgs dc = axis_decode_args(k, n, d_eds, d_present, 1, r);
-    HIP_TRY(ctx, hipMemsetAsync(r.counters, 0, 2 * sizeof(int32_t), s));
-    HIP_TRY(ctx, launch_rs_errlocs(dr, s));
-    HIP_TRY(ctx, launch_rs_errlocs(dc, s));
-    int32_t cnt[2] = {0, 0};
-    HIP_TRY(ctx, hipMemcpyAsync(cnt, r.counters, sizeof cnt, hipMemcpyDeviceToHost, s));
+  for (int pass = 0; pass < 2; pass++) {
+    long deferred_total = 0;
+    int last_ax = -1;
+    for (int round = 0; round < max_rounds; round++) {
+      DecodeArgs dr = axis_decode_args(k, n, d_eds, d_present, 0, r);
+      DecodeArgs dc = axis_decode_args(k, n, d_eds, d_present, 1, r);
+      // decodable vectors and counts of both axes (no locators yet)
+      dr.vec_counts = r.counts[0];
+      dc.vec_counts = r.counts[1];
+      HIP_TRY(ctx, hipMemsetAsync(r.counters, 0, 2 * sizeof(int32_t), s));
+      HIP_TRY(ctx, launch_vec_count(dr, s));
+      HIP_TRY(ctx, launch_vec_count(dc, s));
+      int32_t cnt[3] = {0, 0, 0};
+      HIP_TRY(ctx, hipMemcpyAsync(cnt, r.counters, sizeof cnt, hipMemcpyDeviceToHost, s));
+      HIP_TRY(ctx, hipStreamSynchronize(s));
+      deferred_total += cnt[2];
+      if (cnt[0] == 0 && cnt[1] == 0) break;
+      int ax = cnt[0] >= cnt[1] ? 0 : 1;
+      // after a deferral the other axis is the one with complete data halves
+      if (cnt[2] > 0 && last_ax >= 0 && cnt[1 - last_ax] > 0) ax = 1 - last_ax;
+      last_ax = ax;
+      DecodeArgs& d = ax == 0 ? dr : dc;
+      if (shortcut) {
+        HIP_TRY(ctx, hipMemsetAsync(r.counters + 2, 0, 2 * sizeof(int32_t), s));
+        const long w_ = w;
+        EncodeArgs e{};
+        e.in = d_eds;
+        e.in_sq_stride = e.out_sq_stride = (long)eds_bytes(k);
+        e.op_sq_stride = w_ * w_;
+        if (ax == 0) {
+          e.in_vec_stride = w_ * kSS; e.in_shard_stride = kSS;
+          e.out = d_eds + (long)k * kSS; e.out_vec_stride = w_ * kSS; e.out_shard_stride = kSS;
+          e.out_present = d_present + k; e.op_vec_stride = w_; e.op_shard_stride = 1;
+        } else {
+          e.in_vec_stride = kSS; e.in_shard_stride = w_ * kSS;
+          e.out = d_eds + (long)k * w_ * kSS; e.out_vec_stride = kSS; e.out_shard_stride = w_ * kSS;
+          e.out_present = d_present + (long)k * w_; e.op_vec_stride = 1; e.op_shard_stride = w_;
+        }
+        e.nsq = (long)n; e.nvec = w_; e.nchunk = 1; e.shard_bytes = kSS;
+        e.redo = d.flags;
+        const bool listed = fill_list && leo8_fill_sliced_applicable(e);
+        PlanArgs pa{};
+        pa.counts = d.vec_counts;
+        pa.flags = d.flags;
+        pa.fill = r.fill;
+        pa.pair_list = listed ? r.pair_list : nullptr;
+        pa.pair_count = r.counters + 3;
+        pa.known = r.known;
+        pa.deferred = r.deferred;
+        pa.nodefer = r.nodefer;
+        pa.ndeferred = r.counters + 2;
+        pa.k = (int)k;
+        pa.nsq = (long)n;
+        pa.axis = ax;
+        HIP_TRY(ctx, launch_repair_plan(pa, s));
+        {
+          ProfScope p(ctx, 6, s);
+          if (listed) {
+            e.pair_list = r.pair_list;
+            e.pair_count = r.counters + 3;
+            HIP_TRY(ctx, launch_leo8_fill_sliced(e, (long)n * w_ / 2, s));
+          } else {
+            e.vec_flags = r.fill;
+            HIP_TRY(ctx, launch_rs_encode((int)k, e, s));
+          }
+        }
+      }
+      // locators of the vectors left to the decoder (fill redos included)
+      d.locators_only = 1;
+      HIP_TRY(ctx, launch_rs_errlocs(d, s));
+      {
+        ProfScope p(ctx, 5, s);
+        HIP_TRY(ctx, launch_rs_decode_only(d, s, false));
+      }
+      HIP_TRY(ctx, launch_rs_mark_present(d, d.flags, s));
+      if (shortcut) HIP_TRY(ctx, launch_rs_mark_present(d, r.fill, s, r.known + (long)ax * n * w));
+    }
+    if (!shortcut || deferred_total == 0) break;
+    // deferred vectors whose codeword property is not implied: compare-mode encodes
+    HIP_TRY(ctx, launch_repair_defer_check(r.deferred, r.known, (int)k, (long)n, r.check, s));
+    for (int axis = 0; axis < 2; axis++) {
+      EncodeArgs e{};
+      e.in = d_eds;
+      e.in_sq_stride = e.out_sq_stride = (long)eds_bytes(k);
+      if (axis == 0) {
+        e.in_vec_stride = w * kSS; e.in_shard_stride = kSS;
+        e.out = d_eds + (long)k * kSS; e.out_vec_stride = w * kSS; e.out_shard_stride = kSS;
+      } else {
+        e.in_vec_stride = kSS; e.in_shard_stride = w * kSS;
+        e.out = d_eds + (long)k * w * kSS; e.out_vec_stride = kSS; e.out_shard_stride = w * kSS;
+      }
+      e.nsq = (long)n; e.nvec = w; e.nchunk = 1; e.shard_bytes = kSS;
+      e.vec_flags = r.deferred + (long)axis * n * w;
+      e.mismatch = r.check;
+      e.mismatch_bit = 1;
+      HIP_TRY(ctx, launch_rs_encode((int)k, e, s));
+    }
+    std::vector<int32_t> chk(n);
+    HIP_TRY(ctx, hipMemcpyAsync(chk.data(), r.check, n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(ctx, hipStreamSynchronize(s));
-    if (cnt[0] == 0 && cnt[1] == 0) break;
-    ProfScope p(ctx, 5, s);
-    HIP_TRY(ctx, launch_rs_decode_only(cnt[0] >= cnt[1] ? dr : dc, s, true));
+    bool rerun = false;
+    for (size_t i = 0; i < n; i++) {
+      if (!chk[i]) continue;
+      rerun = true;
+      const int32_t one = 1;
+      HIP_TRY(ctx, hipMemcpyAsync(d_present + i * w * w, r.p0 + i * w * w, w * w, hipMemcpyDeviceToDevice, s));
+      HIP_TRY(ctx, hipMemcpyAsync(r.nodefer + i, &one, sizeof one, hipMemcpyHostToDevice, s));
+    }
+    HIP_TRY(ctx, hipStreamSynchronize(s));  // (the host-side `one` above)
+    if (!rerun) break;
   }
   // verify every complete axis against the given roots
   HIP_TRY(ctx, launch_axis_complete(d_present, (int)k, (long)n, r.complete_now, s));

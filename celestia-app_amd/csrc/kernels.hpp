@@ -37,13 +37,33 @@ struct EncodeArgs {
   int32_t* mismatch;
   int mismatch_bit;
   int32_t* mismatch_vec;  // optional: mismatch_vec[square * nvec + vec] = 1 on a difference
+  // Fill mode (Repair, dagpu.cpp repair_device): a vector whose data half is
+  // complete is rebuilt by encoding that half.  A parity shard is stored only
+  // where out_present[sq * op_sq_stride + vec * op_vec_stride + j * op_shard_stride]
+  // is 0; a given (present) one that differs from the encoding sets
+  // redo[sq * nvec + vec] = 1, and that vector goes to the decoder instead.
+  // vec_flags selects the vectors; the k = 128 bit-sliced encoder instead takes
+  // pair_list (pairs of same-square vectors, flattened sq * nvec + vec, -1 =
+  // none) with *pair_count pairs.
+  const uint8_t* out_present;
+  long op_sq_stride, op_vec_stride, op_shard_stride;
+  int32_t* redo;
+  const int32_t* pair_list;
+  const int32_t* pair_count;
 };
+
+__device__ __forceinline__ bool fill_given(const EncodeArgs& a, long sq, long vec, long j) {
+  return a.out_present[sq * a.op_sq_stride + vec * a.op_vec_stride + j * a.op_shard_stride] != 0;
+}
 
 hipError_t launch_leo8_encode(int k, const EncodeArgs& a, hipStream_t s);
 // bit-sliced GF(2^8) encode (rs_gf8_sliced.hip); launch_leo8_encode uses it
 // whenever leo8_sliced_applicable() holds
 bool leo8_sliced_applicable(int k, const EncodeArgs& a);
 hipError_t launch_leo8_encode_sliced(int k, const EncodeArgs& a, hipStream_t s);
+// k = 128 Repair fill over EncodeArgs.pair_list (up to max_pairs pairs)
+bool leo8_fill_sliced_applicable(const EncodeArgs& a);
+hipError_t launch_leo8_fill_sliced(const EncodeArgs& a, long max_pairs, hipStream_t s);
 
 // Decode addressing: shard i of vector (s, v) at
 //   data + s*sq_stride + v*vec_stride + i*shard_stride   (2k shards)
@@ -59,15 +79,24 @@ struct DecodeArgs {
   int32_t* progress;   // optional: += number of vectors rebuilt (mark pass)
   int32_t* ndecodable; // optional: += number of decodable vectors (errlocs pass)
   // Optional error-locator sharing: the locators depend only on the erasure
-  // pattern, and neighbouring vectors of a repair pass usually share it (every
-  // row of a square kept by the same column set).  err_same[v] = pattern of v
-  // equals that of v - 1; err_head[v] = first vector of v's run, whose locators
-  // v uses.  Both nsq * nvec int32 of workspace; NULL = one computation per vector.
-  int32_t* err_same;
+  // pattern, and many vectors of a repair pass share it (every row of a square
+  // kept by the same column set).  err_key[v] = 32-bit hash of v's pattern;
+  // err_head[v] = the first vector of v's square with the same pattern
+  // (checked flag by flag), whose locators v uses.  Both nsq * nvec int32 of
+  // workspace; NULL = one computation per vector.
+  int32_t* err_key;
   int32_t* err_head;
+  // Locators only (Repair, after the fill/deferral plan): compute the error
+  // locators of the vectors whose flags[] are already set, leaving flags and
+  // counts alone; a flagged vector whose head is not flagged computes the
+  // head's locators itself (same pattern, same values).
+  int locators_only;
+  // Optional (launch_vec_count): vec_counts[v] = present data shards | present
+  // shards << 16 (Repair plan).
+  int32_t* vec_counts;
   // Optional vector selection (exact-order Repair, dagpu.cpp): only vectors v
   // with sel_level[v] == sel_value are decodable in this pass.  Requires
-  // err_same/err_head = NULL (an unselected run head computes no locators).
+  // err_key/err_head = NULL (an unselected head computes no locators).
   const int32_t* sel_level;
   int sel_value;
   long nsq, nvec, nchunk, shard_bytes;
@@ -80,6 +109,10 @@ __device__ __forceinline__ bool vec_selected(const DecodeArgs& a, long v) {
 
 // vector whose error locators vector v uses
 __device__ __forceinline__ long err_vec(const DecodeArgs& a, long v) { return a.err_head ? a.err_head[v] : v; }
+// does vector v (decodable) compute the locators of its head hv?
+__device__ __forceinline__ bool err_computes(const DecodeArgs& a, long v, long hv) {
+  return hv == v || (a.locators_only && a.flags[hv] == 0);
+}
 
 hipError_t launch_leo8_decode(const DecodeArgs& a, hipStream_t s, bool mark_present);
 hipError_t launch_leo8_errlocs(const DecodeArgs& a, hipStream_t s);
@@ -117,6 +150,43 @@ hipError_t launch_verify_roots(const uint8_t* exp_rr, const uint8_t* exp_cr, con
 // rebuilt index} (-1 = none / not known): the first pre-repair failure in the
 // order i = 0..2k-1 x {row root, col root, row parity, col parity}, else a
 // crossword failure (kRepByz, axis resolved by the host), else unrepairable
+// Repair shortcut plan for one round on one axis (see repair_device): every
+// decodable vector of the axis whose data half is complete moves from the
+// decoder (flags) to the fill encoder (fill, and pair_list when set); when every
+// vector i < k of a square is decodable or complete (and nodefer[sq] is 0), the
+// decodes of its vectors i >= k are deferred: the other axis then has complete
+// data halves everywhere and is filled in the next round.  known[axis][sq][i]
+// records axes that are codewords by construction (rebuilt from exactly k
+// shares, or filled); deferred[axis][sq][i] the deferred ones; *ndeferred counts them.
+struct PlanArgs {
+  const int32_t* counts;  // vec_counts of the axis (launch_vec_count)
+  int32_t* flags;
+  int32_t* fill;
+  int32_t* pair_list;
+  int32_t* pair_count;
+  int32_t* known;
+  int32_t* deferred;
+  const int32_t* nodefer;
+  int32_t* ndeferred;
+  int k;
+  long nsq;
+  int axis;
+};
+hipError_t launch_repair_plan(const PlanArgs& p, hipStream_t s);
+// After the crossword: squares with deferred axes whose codeword property does
+// not follow from the known ones (all rows and the columns < k, or all columns
+// and the rows < k) keep their deferred[] marks for a compare-mode encode;
+// the others' marks are cleared.  check[sq] = 0.
+hipError_t launch_repair_defer_check(int32_t* deferred, const int32_t* known, int k, long nsq, int32_t* check,
+                                     hipStream_t s);
+// Decodable vectors and counts without locators (Repair rounds): one lane per
+// vector; flags[v], vec_counts[v] (when set) and *ndecodable as the locator pass
+// would leave them.
+hipError_t launch_vec_count(const DecodeArgs& a, hipStream_t s);
+// presence += vectors with flags[v] != 0 (axis given by the args); with
+// `known` ([sq][idx] of that axis), known[v] = 0 where a.flags[v] is set too
+hipError_t launch_rs_mark_present(const DecodeArgs& a, const int32_t* flags, hipStream_t s,
+                                  int32_t* known = nullptr);
 hipError_t launch_finalize_repair(const int32_t* bits, const int32_t* complete_before, const int32_t* root_bad,
                                   const int32_t* parity_bad, int k, long nsq, int32_t* status, int32_t* byz,
                                   hipStream_t s);

@@ -148,4 +148,247 @@ hipError_t launch_finalize_repair(const int32_t* bits, const int32_t* complete_b
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Repair shortcut (round 3): fill route and deferral, see kernels.hpp PlanArgs
+// and dagpu.cpp repair_device.  A decode rebuilds a vector as the unique
+// codeword through its >= k given shares; when its data half (indices < k) is
+// complete that codeword is Encode(data half), which the fill encoder computes
+// for a fraction of the decoder's work (IFFT_k + FFT_k against the decoder's
+// n-point transforms and per-element multiplies).  Given shares of the parity
+// half are compared, and a difference sends the vector back to the decoder, so
+// every rebuilt vector gets the decoder's bytes.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int nonzero_bytes(uint32_t x) {
+  const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);  // 0x80 per zero byte
+  return 4 - __builtin_popcount(z);
+}
+
+constexpr int kPlanThreads = 256;
+
+// Present shards per vector (all, and of the data half) -> flags, vec_counts,
+// *ndecodable.  The layouts of the locator-key kernels (rs_gf16.hip): contiguous
+// flags (p_shard_stride == 1, the row axis): one wave per vector, 16 flags per
+// lane load; otherwise (column axis) one lane per vector, the 2k flags split
+// over the 16 waves of the block and summed in LDS.  (One lane per vector
+// throughout took 0.1 ms per launch at k = 512, 2 squares: 2,048 lanes in all.)
+__device__ __forceinline__ void vec_count_finish(const DecodeArgs& a, long v, int sys, int tot, int* blk_cnt) {
+  const int k = a.k, n = 2 * k;
+  const bool decode = tot >= k && tot < n && vec_selected(a, v);
+  a.flags[v] = decode ? 1 : 0;
+  if (a.vec_counts) a.vec_counts[v] = sys | (tot << 16);
+  if (tot < k && a.too_few) atomicOr(a.too_few, 1);
+  if (decode) atomicAdd(blk_cnt, 1);
+}
+
+__global__ __launch_bounds__(1024) void vec_count_rows_kernel(DecodeArgs a) {
+  __shared__ int blk_cnt;
+  if (threadIdx.x == 0) blk_cnt = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long v = (long)blockIdx.x * 16 + wave;  // wave-uniform
+  if (v < a.nsq * a.nvec) {
+    const long sq = v / a.nvec;
+    const uint8_t* pres = a.present + sq * a.p_sq_stride + (v - sq * a.nvec) * a.p_vec_stride;
+    const int k = a.k, n = 2 * k;
+    int sys = 0, tot = 0;
+    if (k >= 8 && ((uintptr_t)pres & 15) == 0) {
+      const uint4* q = (const uint4*)pres;
+      for (int j = lane; j < n / 16; j += 64) {
+        const uint4 x = q[j];
+        const int c = nonzero_bytes(x.x) + nonzero_bytes(x.y) + nonzero_bytes(x.z) + nonzero_bytes(x.w);
+        tot += c;
+        if (16 * j < k) sys += c;
+      }
+    } else {
+      for (int i = lane; i < n; i += 64) {
+        const int c = pres[i] != 0;
+        tot += c;
+        if (i < k) sys += c;
+      }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      sys += __shfl_xor(sys, off);
+      tot += __shfl_xor(tot, off);
+    }
+    if (lane == 0) vec_count_finish(a, v, sys, tot, &blk_cnt);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && blk_cnt && a.ndecodable) atomicAdd(a.ndecodable, blk_cnt);
+}
+
+__global__ __launch_bounds__(1024) void vec_count_cols_kernel(DecodeArgs a) {
+  __shared__ int blk_cnt;
+  __shared__ int acc_sys[64], acc_tot[64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long nb = (a.nvec + 63) / 64;
+  const long sq = blockIdx.x / nb;
+  const long vec = (blockIdx.x - sq * nb) * 64 + lane;
+  if (threadIdx.x < 64) acc_sys[threadIdx.x] = acc_tot[threadIdx.x] = 0;
+  if (threadIdx.x == 0) blk_cnt = 0;
+  __syncthreads();
+  const int k = a.k, n = 2 * k;
+  if (vec < a.nvec) {
+    const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
+    int sys = 0, tot = 0;
+    for (int i = wave; i < n; i += 16) {
+      const int c = pres[(long)i * a.p_shard_stride] != 0;
+      tot += c;
+      if (i < k) sys += c;
+    }
+    if (sys) atomicAdd(&acc_sys[lane], sys);
+    if (tot) atomicAdd(&acc_tot[lane], tot);
+  }
+  __syncthreads();
+  if (wave == 0 && vec < a.nvec) vec_count_finish(a, sq * a.nvec + vec, acc_sys[lane], acc_tot[lane], &blk_cnt);
+  __syncthreads();
+  if (threadIdx.x == 0 && blk_cnt && a.ndecodable) atomicAdd(a.ndecodable, blk_cnt);
+}
+
+hipError_t launch_vec_count(const DecodeArgs& a, hipStream_t s) {
+  const long nv = a.nsq * a.nvec;
+  if (nv <= 0) return hipSuccess;
+  if (a.p_shard_stride == 1)
+    hipLaunchKernelGGL(vec_count_rows_kernel, dim3((unsigned)((nv + 15) / 16)), dim3(1024), 0, s, a);
+  else
+    hipLaunchKernelGGL(vec_count_cols_kernel, dim3((unsigned)(a.nsq * ((a.nvec + 63) / 64))), dim3(1024), 0, s,
+                       a);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(kPlanThreads) void repair_plan_kernel(PlanArgs p) {
+  __shared__ int low_ok;
+  __shared__ int nfill_s[kPlanThreads];
+  __shared__ int base_s, total_s;
+  const long sq = blockIdx.x;
+  const int k = p.k, w = 2 * k;
+  if (threadIdx.x == 0) low_ok = 1;
+  __syncthreads();
+  // vectors i = threadIdx.x + 256 m (w <= 1024)
+  constexpr int kPer = 4;
+  int sys[kPer], tot[kPer];
+  bool dec[kPer];
+#pragma unroll
+  for (int m = 0; m < kPer; m++) {
+    const int i = threadIdx.x + kPlanThreads * m;
+    sys[m] = tot[m] = 0;
+    dec[m] = false;
+    if (i >= w) continue;
+    const int32_t c = p.counts[sq * w + i];
+    sys[m] = c & 0xFFFF;
+    tot[m] = c >> 16;
+    dec[m] = p.flags[sq * w + i] != 0;
+    if (i < k && !dec[m] && tot[m] != w) low_ok = 0;
+  }
+  __syncthreads();
+  const bool defer = low_ok && !p.nodefer[sq];
+  int nf = 0, nd = 0;
+  const long ax0 = (long)p.axis * p.nsq * w + sq * w;  // [axis][sq][idx]
+#pragma unroll
+  for (int m = 0; m < kPer; m++) {
+    const int i = threadIdx.x + kPlanThreads * m;
+    if (i >= w) continue;
+    const long v = sq * w + i;
+    const bool f = dec[m] && sys[m] == k;
+    p.fill[v] = f ? 1 : 0;
+    if (f) {
+      p.flags[v] = 0;
+      p.known[ax0 + i] = 1;
+      nf++;
+    } else if (dec[m]) {
+      if (defer && i >= k) {
+        p.flags[v] = 0;
+        p.deferred[ax0 + i] = 1;
+        nd++;
+      } else {
+        p.known[ax0 + i] = tot[m] == k;
+      }
+    }
+  }
+  if (nd) atomicAdd(p.ndeferred, nd);
+  if (!p.pair_list) return;
+  // pair list: the square's fill vectors in pairs (an odd one paired with -1)
+  nfill_s[threadIdx.x] = nf;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int t = 0; t < kPlanThreads; t++) {
+      const int c = nfill_s[t];
+      nfill_s[t] = acc;
+      acc += c;
+    }
+    total_s = acc;
+    base_s = acc ? atomicAdd(p.pair_count, (acc + 1) / 2) : 0;
+  }
+  __syncthreads();
+  int32_t* out = p.pair_list + 2L * base_s;
+  int o = nfill_s[threadIdx.x];
+#pragma unroll
+  for (int m = 0; m < kPer; m++) {
+    const int i = threadIdx.x + kPlanThreads * m;
+    if (i < w && p.fill[sq * w + i]) out[o++] = (int32_t)(sq * w + i);
+  }
+  if (threadIdx.x == 0 && (total_s & 1)) out[total_s] = -1;
+}
+
+hipError_t launch_repair_plan(const PlanArgs& p, hipStream_t s) {
+  if (p.nsq <= 0) return hipSuccess;
+  if (2 * p.k > 4 * kPlanThreads) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(repair_plan_kernel, dim3((unsigned)p.nsq), dim3(kPlanThreads), 0, s, p);
+  return hipGetLastError();
+}
+
+// One workgroup per square: the deferred axes need a codeword check unless
+// every row and every column < k is known to be a codeword (then the square is
+// G A G^T: every column is one) or every column and every row < k is.
+__global__ __launch_bounds__(256) void repair_defer_check_kernel(int32_t* deferred, const int32_t* known, int k,
+                                                                  long nsq, int32_t* check) {
+  __shared__ int any_def, rows_all, cols_low, cols_all, rows_low;
+  const long sq = blockIdx.x;
+  const int w = 2 * k;
+  if (threadIdx.x == 0) {
+    any_def = 0;
+    rows_all = cols_low = cols_all = rows_low = 1;
+    check[sq] = 0;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < w; i += 256) {
+    const long r = sq * w + i, c = (nsq + sq) * w + i;
+    if (deferred[r] || deferred[c]) any_def = 1;
+    if (!known[r]) { rows_all = 0; if (i < k) rows_low = 0; }
+    if (!known[c]) { cols_all = 0; if (i < k) cols_low = 0; }
+  }
+  __syncthreads();
+  if (!any_def || !((rows_all && cols_low) || (cols_all && rows_low))) return;
+  for (int i = threadIdx.x; i < w; i += 256) {
+    deferred[sq * w + i] = 0;
+    deferred[(nsq + sq) * w + i] = 0;
+  }
+}
+
+hipError_t launch_repair_defer_check(int32_t* deferred, const int32_t* known, int k, long nsq, int32_t* check,
+                                     hipStream_t s) {
+  if (nsq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(repair_defer_check_kernel, dim3((unsigned)nsq), dim3(256), 0, s, deferred, known, k, nsq,
+                     check);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void mark_flagged_kernel(DecodeArgs a, const int32_t* flags, int32_t* known) {
+  const long v = blockIdx.x;
+  if (flags[v] == 0) return;
+  // a filled vector the decoder redid (a given parity shard differed): not a codeword by construction
+  if (known && a.flags[v] && threadIdx.x == 0) known[v] = 0;
+  const long sq = v / a.nvec, vec = v % a.nvec;
+  uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
+  for (int i = threadIdx.x; i < 2 * a.k; i += 256) pres[(long)i * a.p_shard_stride] = 1;
+}
+
+hipError_t launch_rs_mark_present(const DecodeArgs& a, const int32_t* flags, hipStream_t s, int32_t* known) {
+  const long nv = a.nsq * a.nvec;
+  if (nv <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mark_flagged_kernel, dim3((unsigned)nv), dim3(256), 0, s, a, flags, known);
+  return hipGetLastError();
+}
+
 }  // namespace dagpu

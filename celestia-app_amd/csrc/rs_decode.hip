@@ -79,7 +79,9 @@ __global__ __launch_bounds__(64 * kErrVecs) void leo8_errlocs_kernel(DecodeArgs 
   if (threadIdx.x == 0) blk_cnt = 0;
   __syncthreads();
   const long v = (long)blockIdx.x * kErrVecs + wave;  // flattened (square, vector)
-  if (v < a.nsq * a.nvec) {
+  // locators_only: flagged vectors that compute their head's locators (uniform per wave)
+  const bool skip = v >= a.nsq * a.nvec || (a.locators_only && (!a.flags[v] || !err_computes(a, v, err_vec(a, v))));
+  if (!skip) {
     uint32_t* e = e_all[wave];
     const long sq = v / a.nvec, vec = v % a.nvec;
     const int k = a.k, n = 2 * k;
@@ -92,23 +94,27 @@ __global__ __launch_bounds__(64 * kErrVecs) void leo8_errlocs_kernel(DecodeArgs 
       e[i] = x;
       if (i < n) cnt += (x == 0);
     }
+    bool decode = true;
+    if (!a.locators_only) {
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);  // present shards
-    const bool decode = cnt >= k && cnt < n && vec_selected(a, v);
-    if (lane == 0) {
-      a.flags[v] = decode ? 1 : 0;
-      if (cnt < k && a.too_few) atomicOr(a.too_few, 1);
-      if (decode) atomicAdd(&blk_cnt, 1);
+      for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);  // present shards
+      decode = cnt >= k && cnt < n && vec_selected(a, v);
+      if (lane == 0) {
+        a.flags[v] = decode ? 1 : 0;
+        if (cnt < k && a.too_few) atomicOr(a.too_few, 1);
+        if (decode) atomicAdd(&blk_cnt, 1);
+      }
     }
     // uniform per wave; a vector sharing an earlier vector's erasure pattern
     // uses that vector's locators
-    if (decode && err_vec(a, v) == v) {
+    const long hv = err_vec(a, v);
+    if (decode && err_computes(a, v, hv)) {
       wave_sync();
       fwht256_wave(e, n, lane);
       for (int i = lane; i < 256; i += 64) e[i] = (e[i] * kGf8.walsh[i]) % 255u;
       wave_sync();
       fwht256_wave(e, 256, lane);
-      uint8_t* out = a.err + v * 256;
+      uint8_t* out = a.err + hv * 256;
       for (int i = lane; i < n; i += 64) out[i] = (uint8_t)e[i];
     }
   }

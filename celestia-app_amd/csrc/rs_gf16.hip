@@ -191,7 +191,7 @@ __global__ __launch_bounds__(kThreads16) void leo16_encode_kernel(EncodeArgs a, 
     uint32_t lo, hi;
     lds_to_block(w16 + e * 32, lo, hi, q);
     uint32_t* dst = (uint32_t*)(out + (long)e * a.out_shard_stride);
-    if (a.mismatch) {
+    if (a.mismatch || (a.out_present && fill_given(a, sq, vec, e))) {
       diff |= (dst[q] != lo) || (dst[q + 8] != hi);
     } else {
       dst[q] = lo;
@@ -202,6 +202,7 @@ __global__ __launch_bounds__(kThreads16) void leo16_encode_kernel(EncodeArgs a, 
     atomicOr(a.mismatch + sq, a.mismatch_bit);
     if (a.mismatch_vec) a.mismatch_vec[sq * a.nvec + vec] = 1;
   }
+  if (a.out_present && !a.mismatch && diff) a.redo[v] = 1;  // Repair fill: a given shard differs
 }
 
 // ---------------------------------------------------------------------------
@@ -281,6 +282,7 @@ __global__ __launch_bounds__(kFoldThreads) void leo16_errlocs_fold_kernel(Decode
   const long sq = v / a.nvec, vec = v % a.nvec;
   constexpr int k = N / 2;
   const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
+  if (a.locators_only && (!a.flags[v] || !err_computes(a, v, err_vec(a, v)))) return;  // uniform
   if (threadIdx.x == 0) cnt_s = 0;
   __syncthreads();
   int cnt = 0;
@@ -293,20 +295,24 @@ __global__ __launch_bounds__(kFoldThreads) void leo16_errlocs_fold_kernel(Decode
   atomicAdd(&cnt_s, cnt);
   __syncthreads();
   const int present = cnt_s;
-  const bool decode = present >= k && present < N && vec_selected(a, v);
-  if (threadIdx.x == 0) {
-    a.flags[v] = decode ? 1 : 0;
-    if (present < k && a.too_few) atomicOr(a.too_few, 1);
-    if (decode && a.ndecodable) atomicAdd(a.ndecodable, 1);
+  bool decode = true;
+  if (!a.locators_only) {
+    decode = present >= k && present < N && vec_selected(a, v);
+    if (threadIdx.x == 0) {
+      a.flags[v] = decode ? 1 : 0;
+      if (present < k && a.too_few) atomicOr(a.too_few, 1);
+      if (decode && a.ndecodable) atomicAdd(a.ndecodable, 1);
+    }
   }
   if (!decode) return;  // uniform
-  if (err_vec(a, v) != v) return;  // shares an earlier vector's locators
+  const long hv = err_vec(a, v);
+  if (!err_computes(a, v, hv)) return;  // shares an earlier vector's locators
   fwht_n<N>(e);
   const uint16_t* wf = g_wfold16[N == 1024];
   for (int i = threadIdx.x; i < N; i += kFoldThreads) e[i] = (e[i] * (uint32_t)wf[i]) % kMod16;
   __syncthreads();
   fwht_n<N>(e);
-  uint16_t* out = (uint16_t*)(a.err + v * (long)rs_err_bytes(k));
+  uint16_t* out = (uint16_t*)(a.err + hv * (long)rs_err_bytes(k));
   for (int i = threadIdx.x; i < N; i += kFoldThreads) out[i] = (uint16_t)e[i];
 }
 
@@ -317,6 +323,7 @@ __global__ __launch_bounds__(kErrThreads) void leo16_errlocs_kernel(DecodeArgs a
   const long sq = v / a.nvec, vec = v % a.nvec;
   const int k = a.k, n = 2 * k;
   const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
+  if (a.locators_only && (!a.flags[v] || !err_computes(a, v, err_vec(a, v)))) return;  // uniform
   if (threadIdx.x == 0) cnt_s = 0;
   __syncthreads();
   int cnt = 0;
@@ -330,20 +337,24 @@ __global__ __launch_bounds__(kErrThreads) void leo16_errlocs_kernel(DecodeArgs a
   atomicAdd(&cnt_s, cnt);
   __syncthreads();
   const int present = cnt_s;
-  const bool decode = present >= k && present < n && vec_selected(a, v);
-  if (threadIdx.x == 0) {
-    a.flags[v] = decode ? 1 : 0;
-    if (present < k && a.too_few) atomicOr(a.too_few, 1);
-    if (decode && a.ndecodable) atomicAdd(a.ndecodable, 1);
+  bool decode = true;
+  if (!a.locators_only) {
+    decode = present >= k && present < n && vec_selected(a, v);
+    if (threadIdx.x == 0) {
+      a.flags[v] = decode ? 1 : 0;
+      if (present < k && a.too_few) atomicOr(a.too_few, 1);
+      if (decode && a.ndecodable) atomicAdd(a.ndecodable, 1);
+    }
   }
   if (!decode) return;  // uniform
-  if (err_vec(a, v) != v) return;  // shares an earlier vector's locators
+  const long hv = err_vec(a, v);
+  if (!err_computes(a, v, hv)) return;  // shares an earlier vector's locators
   fwht65536(e16);
   for (int i = threadIdx.x; i < 65536; i += kErrThreads)
     e16[i] = (uint16_t)(((uint32_t)e16[i] * (uint32_t)g_walsh16[i]) % kMod16);
   __syncthreads();
   fwht65536(e16);
-  uint16_t* out = (uint16_t*)(a.err + v * (long)rs_err_bytes(k));
+  uint16_t* out = (uint16_t*)(a.err + hv * (long)rs_err_bytes(k));
   for (int i = threadIdx.x; i < n; i += kErrThreads) out[i] = e16[i];
 }
 
@@ -653,6 +664,22 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(3, 8))) void 
       atomicOr(&a.mismatch[sq], a.mismatch_bit);
       if (a.mismatch_vec) a.mismatch_vec[sq * a.nvec + vec] = 1;
     }
+    return;
+  }
+  if (a.out_present) {  // Repair fill: store missing parity shards, compare given ones
+    uint32_t diff = 0;
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+      const uint32_t so = (uint32_t)(64 * q + j) * os;
+      if (fill_given(a, sq, vec, 64 * q + j)) {  // wave-uniform
+        diff |= w.lo[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, col, so, 0);
+        diff |= w.hi[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, col + 32u, so, 0);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b32(w.lo[j], out_rsrc, col, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(w.hi[j], out_rsrc, col + 32u, so, 0);
+      }
+    }
+    if (diff) a.redo[sv] = 1;
     return;
   }
 #pragma unroll
@@ -1249,87 +1276,147 @@ hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mar
   return e;
 }
 
-// Error-locator sharing.  err_same[v] = vector v's erasure pattern (its 2k
-// presence flags) equals vector v - 1's; err_head[v] = the last u <= v of v's
-// square whose pattern differs from u - 1's (a run never crosses a square),
-// whose locators v then uses.
+// Error-locator sharing.  err_key[v] = 32-bit hash of vector v's erasure
+// pattern (its 2k presence flags, as 64-flag masks mixed with their index);
+// err_head[v] = the first u <= v of v's square with the same key whose flags
+// equal v's one by one (a key collision falls back to v itself), whose
+// locators v then uses.  (Rounds 2-3 shared locators only along runs of equal
+// neighbours: under the maximal erasure pattern the kept rows are scattered, so
+// about half of them computed their own.)
 //
-// Two launches: the neighbour compare over a grid of (square, vector) blocks,
-// so a few large squares (k = 512 Repair: 2 squares x 1024 vectors x 1024
-// flags per axis) still fill the chip, then one scan workgroup per square.
-// (Round 2 ran both in one workgroup per square: at 2 squares that was 2 of
-// 256 CUs walking 1 M strided flags per axis and round, 182 -> 137 squares/s.)
+// Two launches: the keys over a grid of (square, vector) blocks, so a few
+// large squares (k = 512 Repair: 2 squares x 1024 vectors x 1024 flags per
+// axis) still fill the chip, then one workgroup per square finds the heads.
 // Flag layouts: p_shard_stride == 1 (row axis, codec API): one wave per
-// vector, lanes over its contiguous flags; otherwise (column axis, where
-// adjacent vectors are adjacent bytes) one lane per vector, the 2k flags split
-// over the 16 waves of the block and OR-ed in LDS.
-__global__ __launch_bounds__(1024) void errloc_same_rows_kernel(DecodeArgs a) {
+// vector, 64 flags per ballot; otherwise (column axis, where adjacent vectors
+// are adjacent bytes) one lane per vector, its 64-flag groups split over the
+// 16 waves of the block and XOR-ed in LDS.
+__device__ __forceinline__ uint32_t key_mix(uint64_t m, int g) {
+  uint64_t x = m + 0x9E3779B97F4A7C15ull * (uint64_t)(g + 1);
+  x ^= x >> 31;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 29;
+  x *= 0x94D049BB133111EBull;
+  x ^= x >> 32;
+  return (uint32_t)x;
+}
+
+__global__ __launch_bounds__(1024) void errloc_key_rows_kernel(DecodeArgs a) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long gv = (long)blockIdx.x * 16 + wave;  // wave-uniform
   if (gv >= a.nsq * a.nvec) return;
   const long sq = gv / a.nvec;
   const long v = gv - sq * a.nvec;
-  bool diff = v == 0;  // the first vector of a square starts a run
-  if (v > 0) {
-    const uint8_t* pv = a.present + sq * a.p_sq_stride + v * a.p_vec_stride;
-    const uint8_t* pu = pv - a.p_vec_stride;
-    for (int i = lane; i < 2 * a.k; i += 64) diff |= (pv[i] != 0) != (pu[i] != 0);
+  const uint8_t* pv = a.present + sq * a.p_sq_stride + v * a.p_vec_stride;
+  const int n = 2 * a.k;
+  uint32_t key = 0;
+  for (int g = 0; 64 * g < n; g++) {
+    const int i = 64 * g + lane;
+    const uint64_t m = __builtin_amdgcn_ballot_w64(i < n && pv[i] != 0);
+    key ^= key_mix(m, g);
   }
-  const bool any = __builtin_amdgcn_ballot_w64(diff) != 0;
-  if (lane == 0) a.err_same[gv] = any ? 0 : 1;
+  if (lane == 0) a.err_key[gv] = (int32_t)key;
 }
 
-__global__ __launch_bounds__(1024) void errloc_same_cols_kernel(DecodeArgs a) {
-  __shared__ int32_t acc[64];
+__global__ __launch_bounds__(1024) void errloc_key_cols_kernel(DecodeArgs a) {
+  __shared__ uint32_t acc[64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long nb = (a.nvec + 63) / 64;
   const long sq = blockIdx.x / nb;
   const long v = (blockIdx.x - sq * nb) * 64 + lane;
+  const int n = 2 * a.k;
   if (threadIdx.x < 64) acc[threadIdx.x] = 0;
   __syncthreads();
-  if (v > 0 && v < a.nvec) {
+  if (v < a.nvec) {
     const uint8_t* pv = a.present + sq * a.p_sq_stride + v * a.p_vec_stride;
-    const uint8_t* pu = pv - a.p_vec_stride;
-    bool diff = false;
-    for (int i = wave; i < 2 * a.k; i += 16)
-      diff |= (pv[(long)i * a.p_shard_stride] != 0) != (pu[(long)i * a.p_shard_stride] != 0);
-    if (diff) acc[lane] = 1;  // every writer stores the same value
+    uint32_t key = 0;
+    for (int g = wave; 64 * g < n; g += 16) {
+      uint64_t m = 0;
+      for (int j = 0; j < 64 && 64 * g + j < n; j++)
+        m |= (uint64_t)(pv[(long)(64 * g + j) * a.p_shard_stride] != 0) << j;
+      key ^= key_mix(m, g);
+    }
+    if (key) atomicXor(&acc[lane], key);
   }
   __syncthreads();
-  if (wave == 0 && v < a.nvec) a.err_same[sq * a.nvec + v] = (v == 0 || acc[lane]) ? 0 : 1;
+  if (wave == 0 && v < a.nvec) a.err_key[sq * a.nvec + v] = (int32_t)acc[lane];
 }
 
-// Prefix max of (same ? -1 : index) per square in LDS (Hillis-Steele, nvec <= 1024).
+// One workgroup per square (nvec <= 1024): keys in LDS, candidate head = the
+// first vector with an equal key.
 __global__ __launch_bounds__(1024) void errloc_heads_kernel(DecodeArgs a) {
-  __shared__ int32_t h[1024];
+  __shared__ int32_t key[1024];
   const long sq = blockIdx.x;
   const int t = threadIdx.x;
   const int nvec = (int)a.nvec;
   const long v0 = sq * a.nvec;
-  if (t < nvec) h[t] = a.err_same[v0 + t] ? -1 : t;
+  if (t < nvec) key[t] = a.err_key[v0 + t];
   __syncthreads();
-  for (int off = 1; off < nvec; off <<= 1) {
-    const int x = (t < nvec && t >= off) ? h[t - off] : -1;
-    __syncthreads();
-    if (t < nvec && x > h[t]) h[t] = x;
-    __syncthreads();
+  if (t >= nvec) return;
+  const int32_t kt = key[t];
+  int u = 0;
+  while (key[u] != kt) u++;  // ends at t at the latest
+  a.err_head[v0 + t] = (int32_t)(v0 + u);
+}
+
+// Candidate heads checked flag by flag (a key collision falls back to the
+// vector itself); the same two layouts as the key kernels.
+__global__ __launch_bounds__(1024) void errloc_verify_rows_kernel(DecodeArgs a) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long gv = (long)blockIdx.x * 16 + wave;  // wave-uniform
+  if (gv >= a.nsq * a.nvec) return;
+  const long hv = a.err_head[gv];
+  if (hv == gv) return;
+  const long sq = gv / a.nvec;
+  const uint8_t* pv = a.present + sq * a.p_sq_stride + (gv - sq * a.nvec) * a.p_vec_stride;
+  const uint8_t* pu = a.present + sq * a.p_sq_stride + (hv - sq * a.nvec) * a.p_vec_stride;
+  bool diff = false;
+  for (int i = lane; i < 2 * a.k; i += 64) diff |= (pv[i] != 0) != (pu[i] != 0);
+  if (__builtin_amdgcn_ballot_w64(diff) != 0 && lane == 0) a.err_head[gv] = (int32_t)gv;
+}
+
+__global__ __launch_bounds__(1024) void errloc_verify_cols_kernel(DecodeArgs a) {
+  __shared__ int32_t bad[64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long nb = (a.nvec + 63) / 64;
+  const long sq = blockIdx.x / nb;
+  const long v = (blockIdx.x - sq * nb) * 64 + lane;
+  if (threadIdx.x < 64) bad[threadIdx.x] = 0;
+  __syncthreads();
+  const long gv = sq * a.nvec + v;
+  const long hv = v < a.nvec ? a.err_head[gv] : gv;
+  if (v < a.nvec && hv != gv) {
+    const uint8_t* pv = a.present + sq * a.p_sq_stride + v * a.p_vec_stride;
+    const uint8_t* pu = a.present + sq * a.p_sq_stride + (hv - sq * a.nvec) * a.p_vec_stride;
+    bool diff = false;
+    for (int i = wave; i < 2 * a.k; i += 16)
+      diff |= (pv[(long)i * a.p_shard_stride] != 0) != (pu[(long)i * a.p_shard_stride] != 0);
+    if (diff) bad[lane] = 1;  // every writer stores the same value
   }
-  if (t < nvec) a.err_head[v0 + t] = (int32_t)(v0 + h[t]);
+  __syncthreads();
+  if (wave == 0 && v < a.nvec && bad[lane]) a.err_head[gv] = (int32_t)gv;
 }
 
 hipError_t launch_errloc_heads(const DecodeArgs& a, hipStream_t s) {
-  if (!a.err_same || !a.err_head) return hipSuccess;
+  if (!a.err_key || !a.err_head) return hipSuccess;
   const long nv = a.nsq * a.nvec;
   if (nv <= 0) return hipSuccess;
   if (a.nvec > 1024) return hipErrorInvalidValue;
   if (a.p_shard_stride == 1)
-    hipLaunchKernelGGL(errloc_same_rows_kernel, dim3((unsigned)((nv + 15) / 16)), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(errloc_key_rows_kernel, dim3((unsigned)((nv + 15) / 16)), dim3(1024), 0, s, a);
   else
-    hipLaunchKernelGGL(errloc_same_cols_kernel, dim3((unsigned)(a.nsq * ((a.nvec + 63) / 64))), dim3(1024), 0,
+    hipLaunchKernelGGL(errloc_key_cols_kernel, dim3((unsigned)(a.nsq * ((a.nvec + 63) / 64))), dim3(1024), 0,
                        s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(errloc_heads_kernel, dim3((unsigned)a.nsq), dim3(1024), 0, s, a);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if (a.p_shard_stride == 1)
+    hipLaunchKernelGGL(errloc_verify_rows_kernel, dim3((unsigned)((nv + 15) / 16)), dim3(1024), 0, s, a);
+  else
+    hipLaunchKernelGGL(errloc_verify_cols_kernel, dim3((unsigned)(a.nsq * ((a.nvec + 63) / 64))), dim3(1024), 0,
+                       s, a);
   return hipGetLastError();
 }
 

@@ -178,6 +178,18 @@ __device__ __forceinline__ void encode_half(const EncodeArgs& a, long sq, long v
     }
     return;
   }
+  if (a.out_present) {  // Repair fill: store missing parity shards, compare given ones
+    uint32_t diff = 0;
+#pragma unroll
+    for (int j = 0; j < E; j++) {
+      if (fill_given(a, sq, vec, HH * E + j))  // wave-uniform
+        diff |= w[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, col, (HH * E + j) * out_stride, 0);
+      else
+        __builtin_amdgcn_raw_buffer_store_b32(w[j], out_rsrc, col, (HH * E + j) * out_stride, 0);
+    }
+    if (diff) a.redo[sq * a.nvec + vec] = 1;
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < E; j++)
     __builtin_amdgcn_raw_buffer_store_b32(w[j], out_rsrc, col, (HH * E + j) * out_stride, 0);

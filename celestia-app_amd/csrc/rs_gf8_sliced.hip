@@ -210,31 +210,51 @@ __device__ __forceinline__ void transpose_wave2(uint32_t (&v)[16][8], u32x4* lds
   }
 }
 
+// FILL (Repair fill mode, EncodeArgs): block = (pair of same-square vectors
+// from pair_list, chunk); each half of the lanes takes its own vector (a -1
+// entry: the lanes load the partner's data and store nothing); a parity shard
+// is stored where it is missing, a given one is compared (redo on a difference).
+template <bool FILL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void leo8_encode_sliced2_kernel(EncodeArgs a) {
   constexpr int K = 128;
   __shared__ u32x4 lds[K * 32];  // 64 KB
-  const long ngrp = a.nvec >> 1;
-  const long nblk = a.nsq * ngrp * a.nchunk;
-  long blk = blockIdx.x;
-  if ((nblk & 7) == 0) blk = (blk & 7) * (nblk >> 3) + (blk >> 3);  // one eighth per XCD
-  const long chunk = blk % a.nchunk;
-  const long sg = blk / a.nchunk;
-  const long grp = sg % ngrp;
-  const long sq = sg / ngrp;
-  constexpr int st_aux = 2;  // non-temporal stores
   const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int t = lane & 15, vv = (lane >> 4) & 1, eb = lane >> 5;
+  long chunk, sq, vbase, vlane;  // vector = vbase (block-uniform) + vlane (this lane)
+  int fill_v = -1;               // FILL: this lane's flattened vector, -1 = none
+  if constexpr (FILL) {
+    chunk = blockIdx.x % a.nchunk;
+    const long g = blockIdx.x / a.nchunk;
+    if (g >= *a.pair_count) return;  // uniform
+    const int v0 = a.pair_list[2 * g], v1 = a.pair_list[2 * g + 1];
+    sq = v0 / a.nvec;
+    fill_v = vv ? v1 : v0;
+    vbase = 0;
+    vlane = (fill_v >= 0 ? fill_v : v0) - sq * a.nvec;
+  } else {
+    const long ngrp = a.nvec >> 1;
+    const long nblk = a.nsq * ngrp * a.nchunk;
+    long blk = blockIdx.x;
+    if ((nblk & 7) == 0) blk = (blk & 7) * (nblk >> 3) + (blk >> 3);  // one eighth per XCD
+    chunk = blk % a.nchunk;
+    const long sg = blk / a.nchunk;
+    const long grp = sg % ngrp;
+    sq = sg / ngrp;
+    vbase = grp * 2;
+    vlane = vv;
+  }
+  constexpr int st_aux = 2;  // non-temporal stores
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t ebmask = eb ? 0xFFFFFFFFu : 0u;
 
   // layout A: register j holds element j + 16 eb + 32 w; the lane part of the
   // element offset (16 eb) goes into voffset, the wave part into soffset
   uint32_t v[16][8];
   {
-    const auto rsrc = make_rsrc(a.in + sq * a.in_sq_stride + grp * 2 * a.in_vec_stride + chunk * 512);
+    const auto rsrc = make_rsrc(a.in + sq * a.in_sq_stride + vbase * a.in_vec_stride + chunk * 512);
     const uint32_t sstride = (uint32_t)a.in_shard_stride;
-    const uint32_t voff = (uint32_t)(vv * a.in_vec_stride) + (uint32_t)(16 * eb) * sstride + 16u * t;
+    const uint32_t voff = (uint32_t)(vlane * a.in_vec_stride) + (uint32_t)(16 * eb) * sstride + 16u * t;
 #pragma unroll
     for (int j = 0; j < 16; j++) {
       const uint32_t soff = (uint32_t)(j + 32 * w) * sstride;
@@ -244,10 +264,10 @@ void leo8_encode_sliced2_kernel(EncodeArgs a) {
       v[j][4] = hi.x; v[j][5] = hi.y; v[j][6] = hi.z; v[j][7] = hi.w;
     }
   }
-  if (a.copy) {  // row pass: the data shards also go to Q0 of the EDS
-    const auto rsrc = make_rsrc(a.copy + sq * a.copy_sq_stride + grp * 2 * a.copy_vec_stride + chunk * 512);
+  if (!FILL && a.copy) {  // row pass: the data shards also go to Q0 of the EDS
+    const auto rsrc = make_rsrc(a.copy + sq * a.copy_sq_stride + vbase * a.copy_vec_stride + chunk * 512);
     const uint32_t sstride = (uint32_t)a.copy_shard_stride;
-    const uint32_t voff = (uint32_t)(vv * a.copy_vec_stride) + (uint32_t)(16 * eb) * sstride + 16u * t;
+    const uint32_t voff = (uint32_t)(vlane * a.copy_vec_stride) + (uint32_t)(16 * eb) * sstride + 16u * t;
 #pragma unroll
     for (int j = 0; j < 16; j++) {
       const uint32_t soff = (uint32_t)(j + 32 * w) * sstride;
@@ -289,9 +309,29 @@ void leo8_encode_sliced2_kernel(EncodeArgs a) {
 
 #pragma unroll
   for (int j = 0; j < 16; j++) transpose8(v[j]);
-  const auto rsrc = make_rsrc(a.out + sq * a.out_sq_stride + grp * 2 * a.out_vec_stride + chunk * 512);
+  const auto rsrc = make_rsrc(a.out + sq * a.out_sq_stride + vbase * a.out_vec_stride + chunk * 512);
   const uint32_t sstride = (uint32_t)a.out_shard_stride;
-  const uint32_t voff = (uint32_t)(vv * a.out_vec_stride) + (uint32_t)(16 * eb) * sstride + 16u * t;
+  const uint32_t voff = (uint32_t)(vlane * a.out_vec_stride) + (uint32_t)(16 * eb) * sstride + 16u * t;
+  if constexpr (FILL) {
+    if (fill_v < 0) return;
+    uint32_t diff = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint32_t soff = (uint32_t)(j + 32 * w) * sstride;
+      if (fill_given(a, sq, vlane, j + 16 * eb + 32 * w)) {
+        const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, soff, 0);
+        const u32x4 hi = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 256u, soff, 0);
+        diff |= (lo.x ^ v[j][0]) | (lo.y ^ v[j][1]) | (lo.z ^ v[j][2]) | (lo.w ^ v[j][3]);
+        diff |= (hi.x ^ v[j][4]) | (hi.y ^ v[j][5]) | (hi.z ^ v[j][6]) | (hi.w ^ v[j][7]);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128((u32x4){v[j][0], v[j][1], v[j][2], v[j][3]}, rsrc, voff, soff, 0);
+        __builtin_amdgcn_raw_buffer_store_b128((u32x4){v[j][4], v[j][5], v[j][6], v[j][7]}, rsrc, voff + 256u, soff,
+                                               0);
+      }
+    }
+    if (diff) a.redo[fill_v] = 1;
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 16; j++) {
     const uint32_t soff = (uint32_t)(j + 32 * w) * sstride;
@@ -320,7 +360,8 @@ bool leo8_sliced_applicable(int k, const EncodeArgs& a) {
     return !(e && e[0] == '0');
   }();
   if (!enabled || k < 16 || k > 128) return false;
-  if (a.shard_bytes <= 0 || a.shard_bytes % 512 || a.nvec % 4 || a.vec_flags || a.mismatch) return false;
+  if (a.shard_bytes <= 0 || a.shard_bytes % 512 || a.nvec % 4 || a.vec_flags || a.mismatch || a.out_present)
+    return false;
   if (a.nchunk * 512 != a.shard_bytes) return false;
   const long strides[] = {a.in_sq_stride, a.in_vec_stride, a.in_shard_stride, a.out_sq_stride,
                           a.out_vec_stride, a.out_shard_stride};
@@ -351,7 +392,7 @@ hipError_t launch_leo8_encode_sliced(int k, const EncodeArgs& a, hipStream_t s) 
   if (k == 128 && sliced2_enabled()) {
     const long blocks = a.nsq * (a.nvec / 2) * a.nchunk;
     if (blocks <= 0) return hipSuccess;
-    hipLaunchKernelGGL(leo8_encode_sliced2_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(leo8_encode_sliced2_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, a);
     return hipGetLastError();
   }
   switch (k) {
@@ -361,6 +402,28 @@ hipError_t launch_leo8_encode_sliced(int k, const EncodeArgs& a, hipStream_t s) 
     case 128: return launch_sliced_k<128>(a, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+// Repair fill at k = 128 over a pair list (EncodeArgs fill fields; grid for the
+// worst case, blocks past *pair_count return).  Same shape limits as the
+// sliced encoder: whole 512-B chunks, 16-B aligned strides, offsets < 2^31.
+bool leo8_fill_sliced_applicable(const EncodeArgs& a) {
+  if (a.shard_bytes <= 0 || a.shard_bytes % 512 || a.nchunk * 512 != a.shard_bytes) return false;
+  const long strides[] = {a.in_sq_stride, a.in_vec_stride, a.in_shard_stride, a.out_sq_stride,
+                          a.out_vec_stride, a.out_shard_stride};
+  for (long st : strides)
+    if (st % 16) return false;
+  if (!aligned16(a.in) || !aligned16(a.out)) return false;
+  const long lim = 1L << 31;
+  return (a.nvec - 1) * a.in_vec_stride + 512 + 128L * a.in_shard_stride < lim &&
+         (a.nvec - 1) * a.out_vec_stride + 512 + 128L * a.out_shard_stride < lim;
+}
+
+hipError_t launch_leo8_fill_sliced(const EncodeArgs& a, long max_pairs, hipStream_t s) {
+  const long blocks = max_pairs * a.nchunk;
+  if (blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(leo8_encode_sliced2_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s, a);
+  return hipGetLastError();
 }
 
 }  // namespace dagpu

@@ -183,10 +183,10 @@ int dagpu_repair_batch_device_ex(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* 
 /* Per-kernel timing with HIP events recorded on the launch stream around each
  * kernel the pipeline enqueues (for bench.py's roofline; off by default).
  * Kernel ids: 0 RS row pass, 1 RS column pass, 2 NMT leaves, 3 NMT trees,
- * 4 DAH, 5 decode.  dagpu_profile_read synchronises the recorded events and
+ * 4 DAH, 5 decode, 6 Repair fill encode.  dagpu_profile_read synchronises the recorded events and
  * returns, per kernel id, the summed milliseconds and launch count since the
  * last reset (arrays of DAGPU_PROFILE_KERNELS entries). */
-#define DAGPU_PROFILE_KERNELS 6
+#define DAGPU_PROFILE_KERNELS 7
 int dagpu_profile_enable(dagpu_ctx* ctx, int on);
 int dagpu_profile_read(dagpu_ctx* ctx, double* total_ms, uint64_t* launches, int reset);
 

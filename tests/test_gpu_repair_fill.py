@@ -1,0 +1,154 @@
+"""Repair fill route and deferral (dagpu.cpp repair_device, repair.hip
+repair_plan_kernel): with DAGPU_REPAIR_FILL on (the default) a decodable axis
+whose data half is complete is re-encoded instead of decoded, and decodes of
+axes i >= k wait when every axis i < k is being rebuilt.  Both must leave
+exactly what the plain decoder schedule leaves -- status, every EDS byte and
+the presence map -- for consistent squares, corrupted given shares (also in
+the parity half of a filled axis, which sends it back to the decoder),
+unrepairable patterns and a committed square that is not a codeword square
+(the deferred-axis check and the re-run without deferral).  Statuses are also
+checked against the oracle's rsmt2d restatement."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from celestia_da import _abi, da, synth
+from celestia_da.device import DeviceSquares
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = da.Context(0)
+    yield c
+    c.close()
+
+
+def _pattern(kind, k, rng):
+    w = 2 * k
+    p = np.zeros((w, w), bool)
+    if kind == "subgrid":  # the maximal erasure pattern (configs[3])
+        p[np.ix_(rng.choice(w, k, replace=False), rng.choice(w, k, replace=False))] = True
+    elif kind == "subgrid_top":  # kept rows are the data rows
+        p[np.ix_(np.arange(k), rng.choice(w, k, replace=False))] = True
+    elif kind == "q0":  # the original data only: every axis is filled
+        p[:k, :k] = True
+    elif kind == "left_half":  # every row decodable by its data half, some parity given
+        p[:, :k] = True
+        p[:, k:] = rng.random((w, k)) < 0.3
+    elif kind == "rows_plus":  # data rows over-determined, parity rows exactly k: deferral + check
+        for r in range(w):
+            p[r, rng.choice(w, k + max(1, min(5, k // 2)) if r < k else k, replace=False)] = True
+    elif kind == "unrepairable":
+        p[np.ix_(rng.choice(w, k, replace=False), rng.choice(w, k, replace=False))] = True
+        r, c = np.argwhere(p)[0]
+        p[r, :] = False
+        p[:, c] = False
+    else:  # random density
+        p = rng.random((w, w)) < float(kind)
+    return p
+
+
+def _corrupt(eds, p, how, rng, k):
+    """Flip one byte of a given share: any, or one in the parity half of a row
+    whose data half is complete (the fill route compares it)."""
+    if how is None:
+        return
+    cells = np.argwhere(p)
+    if how == "parity_half":
+        cells = [(r, c) for r, c in cells if c >= k and p[r, :k].all()] or list(cells)
+    r, c = cells[rng.integers(len(cells))]
+    eds[r, c, rng.integers(512)] ^= 1 << int(rng.integers(8))
+
+
+def _run(ctx, k, eds_dmg, pres, rr, cr, monkeypatch, fill):
+    monkeypatch.setenv("DAGPU_REPAIR_FILL", "1" if fill else "0")
+    n = len(eds_dmg)
+    w = 2 * k
+    ds = DeviceSquares(k, n, ctx=ctx)
+    ds.eds.copy_(torch.from_numpy(eds_dmg.reshape(n, -1)))
+    ds.row_roots.copy_(torch.from_numpy(rr))
+    ds.col_roots.copy_(torch.from_numpy(cr))
+    present = torch.from_numpy(pres.reshape(n, -1).astype(np.uint8)).cuda()
+    status = torch.full((n,), -99, dtype=torch.int32, device="cuda")
+    ds.repair(present, status, ds.repair_workspace())
+    torch.cuda.synchronize()
+    out = (status.cpu().numpy(), ds.eds.cpu().numpy().reshape(n, w, w, 512), present.cpu().numpy().reshape(n, w, w))
+    del ds
+    torch.cuda.empty_cache()
+    return out
+
+
+def _case(ctx, monkeypatch, k, specs, seed, oracle_check=True, bad_encoding=()):
+    rng = np.random.default_rng(seed)
+    n = len(specs)
+    w = 2 * k
+    ods = synth.blob_squares(k, seed, 0, n, threads=16)
+    eds_l, rr_l, cr_l, dmg_l, pres_l = [], [], [], [], []
+    for i, (kind, corrupt) in enumerate(specs):
+        eds, rr, cr, _ = oracle.extend_and_dah(ods[i].reshape(k * k, 512), k, nthreads=16)
+        p = _pattern(kind, k, rng)
+        if i in bad_encoding:
+            # commit to a square that is not a codeword square: garbage in the
+            # cells of Q3 that are missing, roots computed over it
+            q3 = np.zeros((w, w), bool)
+            q3[k:, k:] = True
+            eds = eds.copy()
+            eds[q3 & ~p] = rng.integers(0, 256, (int((q3 & ~p).sum()), 512), dtype=np.uint8)
+            rr, cr = oracle.compute_roots(eds, k, nthreads=16)
+        dmg = eds * p[:, :, None]
+        _corrupt(dmg, p, corrupt, rng, k)
+        eds_l.append(eds); rr_l.append(rr); cr_l.append(cr); dmg_l.append(dmg); pres_l.append(p)
+    dmg = np.stack(dmg_l)
+    pres = np.stack(pres_l)
+    rr, cr = np.stack(rr_l), np.stack(cr_l)
+    st1, e1, p1 = _run(ctx, k, dmg, pres, rr, cr, monkeypatch, True)
+    st0, e0, p0 = _run(ctx, k, dmg, pres, rr, cr, monkeypatch, False)
+    for i, spec in enumerate(specs):
+        assert st1[i] == st0[i], (i, spec, st1[i], st0[i])
+        assert (p1[i] == p0[i]).all(), (i, spec)
+        assert (e1[i] == e0[i]).all(), (i, spec)
+        if st1[i] == 0:
+            assert (e1[i] == eds_l[i]).all() and p1[i].all(), (i, spec)
+        if oracle_check:
+            orc, _ = oracle.repair(dmg_l[i], pres_l[i], k, rr_l[i], cr_l[i])
+            assert st1[i] == orc, (i, spec, st1[i], orc)
+    return st1
+
+
+@pytest.mark.parametrize("k", [4, 16, 64])
+def test_fill_equals_decoder_small(ctx, monkeypatch, k):
+    specs = [("subgrid", None), ("subgrid_top", None), ("q0", None), ("left_half", None),
+             ("rows_plus", None), ("0.5", None), ("0.65", None), ("0.8", None),
+             ("subgrid", "any"), ("left_half", "parity_half"), ("rows_plus", "any"),
+             ("unrepairable", None), ("unrepairable", "any"), ("q0", "any")]
+    st = _case(ctx, monkeypatch, k, specs, 300 + k)
+    assert st[0] == 0 and st[2] == 0 and st[9] == _abi.ERR_BYZANTINE
+
+
+def test_fill_equals_decoder_k128(ctx, monkeypatch):
+    """The bit-sliced k = 128 fill (pair list) and decoder."""
+    specs = [("subgrid", None), ("subgrid", None), ("subgrid_top", None), ("q0", None),
+             ("left_half", None), ("rows_plus", None), ("0.6", None), ("subgrid", "any"),
+             ("left_half", "parity_half"), ("rows_plus", "any"), ("unrepairable", None)]
+    st = _case(ctx, monkeypatch, 128, specs, 1280, oracle_check=False)
+    assert (st[:7] == 0).all() and st[8] == _abi.ERR_BYZANTINE
+
+
+@pytest.mark.parametrize("k", [16, 128])
+def test_fill_bad_encoding(ctx, monkeypatch, k):
+    """Committed squares that are not codeword squares (garbage in the missing
+    Q3 cells, roots over it): the same outcome with and without the shortcut,
+    including the deferred-axis check and the re-run without deferral."""
+    specs = [("subgrid", None), ("rows_plus", None), ("rows_plus", "any"), ("left_half", None),
+             ("subgrid_top", None), ("0.6", None)]
+    _case(ctx, monkeypatch, k, specs, 4400 + k, oracle_check=(k <= 16), bad_encoding=range(len(specs)))
+
+
+def test_fill_equals_decoder_gf16(ctx, monkeypatch):
+    """GF(2^16) (k = 256): the register-resident fill encoder and decoder."""
+    specs = [("subgrid", None), ("left_half", "parity_half"), ("rows_plus", None)]
+    st = _case(ctx, monkeypatch, 256, specs, 2560, oracle_check=False)
+    assert st[0] == 0 and st[1] == _abi.ERR_BYZANTINE and st[2] == 0
