@@ -372,6 +372,46 @@ __host__ __device__ __forceinline__ void fft_B(uint32_t (&v)[16][8]) {
   });
 }
 
+// ifft_B then fft_B with their adjacent middle layers fused (round 3): the
+// IFFT's last layer and the FFT's first act on the same pairs (i, i + 8), so
+//   y ^= x; x ^= c1 y;  x ^= c2 y; y ^= x   ==   y ^= x; x ^= (c1 ^ c2) y; y ^= x
+// (multiplication distributes over field addition; a "skip" skew is element 0):
+// one constant multiply per pair instead of two.
+template <int K>
+__host__ __device__ __forceinline__ void ifft_fft_B(uint32_t (&v)[16][8]) {
+  constexpr int NB = Geo<K>::NB, NW = Geo<K>::NW;
+  static_for<3>([&](auto rb) {  // IFFT layers n-4 .. n-2
+    constexpr int D = 1 << (rb + NB), R = 1 << rb;
+    static_for<16>([&](auto i) {
+      if constexpr (!(i & R)) {
+        constexpr int c = skew_elem(D - 1 + K + NW * (i & ~(2 * R - 1)));
+        xor8(v[i + R], v[i]);
+        muladd_ct<c>(v[i], v[i + R]);
+      }
+    });
+  });
+  {  // IFFT layer n-1 + FFT layer n-1 (pairs (i, i + 8); block start 0 for i < 8)
+    constexpr int D = 1 << (3 + NB);
+    static_for<8>([&](auto i) {
+      constexpr int c = skew_elem(D - 1 + K) ^ skew_elem(D - 1);
+      xor8(v[i + 8], v[i]);
+      muladd_ct<c>(v[i], v[i + 8]);
+      xor8(v[i + 8], v[i]);
+    });
+  }
+  static_for<3>([&](auto rr) {  // FFT layers n-2 .. n-4
+    constexpr int rb = 2 - rr;
+    constexpr int D = 1 << (rb + NB), R = 1 << rb;
+    static_for<16>([&](auto i) {
+      if constexpr (!(i & R)) {
+        constexpr int c = skew_elem(D - 1 + NW * (i & ~(2 * R - 1)));
+        muladd_ct<c>(v[i], v[i + R]);
+        xor8(v[i + R], v[i]);
+      }
+    });
+  });
+}
+
 // ---------------------------------------------------------------------------
 // Two-vector layout for k = 128 (rs_gf8_sliced.hip leo8_encode_sliced2_kernel).
 // A 4-wave workgroup holds 2 vectors (128 KB) instead of 4 (256 KB), so two

@@ -120,8 +120,7 @@ void leo8_encode_sliced_kernel(EncodeArgs a) {
 
   ifft_A<K>(v, &kWMasksIfft.m[0][wave][0], kMaxWav * 64);
   if constexpr (NW > 1) exchange<K, true>(v, lds, wave, lane);
-  ifft_B<K>(v);
-  fft_B<K>(v);
+  ifft_fft_B<K>(v);
   if constexpr (NW > 1) {
     __syncthreads();
     exchange<K, false>(v, lds, wave, lane);
@@ -287,8 +286,7 @@ void leo8_encode_sliced2_kernel(EncodeArgs a) {
   ifft_As2<K>(v, w);
   __syncthreads();  // every wave's wave-local reads are done before the exchange writes
   exchange2s<true>(v, lds, w, eb, col);
-  ifft_B<K>(v);
-  fft_B<K>(v);
+  ifft_fft_B<K>(v);
   __syncthreads();
   exchange2s<false>(v, lds, w, eb, col);
   fft_As2<K>(v, w);

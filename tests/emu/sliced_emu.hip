@@ -36,8 +36,7 @@ void encode_chunk_lane(const uint8_t* data, uint8_t* parity, long shard, long co
       memcpy(tmp[wb][i], st[e >> 4][e & 15], 32);
     }
   for (int wb = 0; wb < NW; wb++) {
-    ifft_B<K>(tmp[wb]);
-    fft_B<K>(tmp[wb]);
+    ifft_fft_B<K>(tmp[wb]);
   }
   for (int wb = 0; wb < NW; wb++)  // B -> A
     for (int i = 0; i < 16; i++) {
@@ -93,8 +92,7 @@ void encode2_chunk_lane(const uint8_t* data, uint8_t* parity, long shard, long c
       }
   for (int w = 0; w < 4; w++)
     for (int eb = 0; eb < 2; eb++) {
-      ifft_B<K>(tmp[w][eb]);
-      fft_B<K>(tmp[w][eb]);
+      ifft_fft_B<K>(tmp[w][eb]);
     }
   for (int w = 0; w < 4; w++)  // B -> A*
     for (int eb = 0; eb < 2; eb++)
