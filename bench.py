@@ -826,7 +826,8 @@ MIXED_SEED = 4096
 def mixed_batch(ctx, dev=0):
     """configs[2] input: 4096 squares, k = 2^u with u ~ U{0..7} (seeded), every
     square distinct (seeded run MIXED_SEED + k, csrc/synth.cpp), grouped by k
-    into device-resident batches.  Returns (ks, {k: DeviceSquares}, {k: host ODS})."""
+    into device-resident batches, each ODS in Q0 of its EDS buffer (the layout
+    of the headline step).  Returns (ks, {k: DeviceSquares}, {k: host ODS})."""
     from celestia_da import synth
     from celestia_da.device import DeviceSquares
 
@@ -835,9 +836,9 @@ def mixed_batch(ctx, dev=0):
     groups, hosts = {}, {}
     for k in sorted(set(ks)):
         n = ks.count(k)
-        ds = DeviceSquares(k, n, device=dev, ctx=ctx)
+        ds = DeviceSquares(k, n, device=dev, ctx=ctx, in_place=True)
         hosts[k] = synth.blob_squares(k, MIXED_SEED + k, 0, n, threads=host_threads())
-        ds.ods.copy_(torch.from_numpy(hosts[k]))
+        ds.load_ods(hosts[k])
         groups[k] = ds
     return ks, groups, hosts
 
