@@ -164,7 +164,10 @@ int dagpu_repair_ex(dagpu_ctx* ctx, uint32_t k, uint8_t* eds, uint8_t* present,
  * d_present = n * (2k)^2 flags (updated in place), expected roots as produced by
  * dagpu_extend_batch_device.  d_status gets one dagpu_status per square.
  * d_workspace: dagpu_repair_workspace_size(k, n) bytes.  Enqueued on `stream`;
- * the call synchronises once per crossword round to read two counters.
+ * the call synchronises once per crossword round to read its counters (and
+ * once more when deferred axes need their codeword check).  Axes whose data
+ * half is complete are re-encoded instead of decoded (same bytes);
+ * DAGPU_REPAIR_FILL=0 in the environment selects the plain decoder schedule.
  * The _ex form also writes d_byz (n * 4 int32, device memory, as byz of
  * dagpu_repair_ex); a square whose crossword fails is then re-run in rsmt2d's
  * sequential order on the device to name its axis (synchronises `stream`).
