@@ -1137,12 +1137,12 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
     HIP_TRY(ctx, hipMemcpyAsync(r.known, r.complete_before, n * 2 * w * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
     HIP_TRY(ctx, hipMemsetAsync(r.deferred, 0, n * 2 * w * sizeof(int32_t), s));
     HIP_TRY(ctx, hipMemsetAsync(r.nodefer, 0, n * sizeof(int32_t), s));
-    HIP_TRY(ctx, hipMemsetAsync(r.counters, 0, 4 * sizeof(int32_t), s));
   }
   const int max_rounds = 4 * (int)w + 4;
   for (int pass = 0; pass < 2; pass++) {
     long deferred_total = 0;
     int last_ax = -1;
+    HIP_TRY(ctx, hipMemsetAsync(r.counters, 0, 4 * sizeof(int32_t), s));  // [2] is read every round
     for (int round = 0; round < max_rounds; round++) {
       DecodeArgs dr = axis_decode_args(k, n, d_eds, d_present, 0, r);
       DecodeArgs dc = axis_decode_args(k, n, d_eds, d_present, 1, r);
