@@ -96,6 +96,7 @@ int enqueue_rs(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_ods, uint8
   return DAGPU_OK;
 }
 
+// d_dah = NULL: roots only (Repair's verification needs no DAH)
 int enqueue_roots(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_eds, uint8_t* d_rr,
                   uint8_t* d_cr, uint8_t* d_dah, int32_t* d_status, void* d_ws, hipStream_t s) {
   SquareArgs sa{};
@@ -121,7 +122,7 @@ int enqueue_roots(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_eds, ui
     HIP_TRY(ctx, launch_nmt_trees(sa, s));
   }
   stage_mark(ctx, DAGPU_STAGE_TREES, s);
-  {
+  if (d_dah) {
     ProfScope p(ctx, 4, s);
     HIP_TRY(ctx, launch_dah(sa, s));
   }
@@ -1037,7 +1038,7 @@ int exact_repair(dagpu_ctx* ctx, uint32_t k, size_t n, size_t sq, uint8_t* d_eds
       HIP_TRY(ctx, launch_rs_decode_only(d, s, true));
     }
   }
-  int rc = enqueue_roots(ctx, k, 1, eds, r.sa.row_roots, r.sa.col_roots, r.sa.dah, r.sa.status, r.sa.digests, s);
+  int rc = enqueue_roots(ctx, k, 1, eds, r.sa.row_roots, r.sa.col_roots, nullptr, r.sa.status, r.sa.digests, s);
   if (rc) return rc;
   std::vector<uint8_t> got(2 * w * kNodeSize), want(2 * w * kNodeSize);
   HIP_TRY(ctx, hipMemcpyAsync(got.data(), r.sa.row_roots, w * kNodeSize, hipMemcpyDeviceToHost, s));
@@ -1255,7 +1256,7 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
   HIP_TRY(ctx, launch_axis_complete(d_present, (int)k, (long)n, r.complete_now, s));
   r.sa.eds = d_eds;
   r.sa.eds_sq_stride = (long)eds_bytes(k);
-  int rc = enqueue_roots(ctx, k, n, d_eds, r.sa.row_roots, r.sa.col_roots, r.sa.dah, r.sa.status,
+  int rc = enqueue_roots(ctx, k, n, d_eds, r.sa.row_roots, r.sa.col_roots, nullptr, r.sa.status,
                          r.sa.digests, s);
   if (rc) return rc;
   HIP_TRY(ctx, launch_verify_roots(d_rr, d_cr, r.sa.row_roots, r.sa.col_roots, r.complete_now,
