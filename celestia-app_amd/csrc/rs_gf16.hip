@@ -698,10 +698,9 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(3, 8))) void 
 //   work = shard * errLocs (0 where missing) -> ifftDITDecoder (skew index
 //   iend - 1) -> formal derivative -> fftDIT -> erased shards = work *
 //   (65535 - errLocs).
-// Runtime multiplies (errLocs are per element, wave-uniform) build their
-// 16-dword product table on the fly: lane 4g + e2 computes (e2 << 2g) * exp(lm)
-// from the log/exp tables (16 elements' gathers in flight), a quad DPP OR
-// packs the four bytes, v_readlane moves the 16 dwords to SGPRs.
+// Runtime multiplies (errLocs are per element) use 16-dword product tables that
+// the workgroup builds in LDS, one element per thread (mul16_table_to), and
+// every lane of a wave reads for its elements (mul16_table_from).
 // The formal derivative D(x)_e = x_e ^ XOR_{s: bit s of e == 0} x_{e | 2^s}
 // runs in the transposed layout (element bits 3-5 = wave): slot bits are
 // applied in place in ascending slot order (a read of slot e | 2^t > e sees
@@ -710,33 +709,14 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(3, 8))) void 
 // ---------------------------------------------------------------------------
 constexpr int kDecN = 512;
 
-// Lane 4g + e2 (lanes 32..63 repeat 0..31) owns the product (e2 << 2g) * exp(lm):
-// log(e2 << 2g) is per lane (mul16_logx, hoisted), exp() is one gather per
-// table; mul16_pack turns the 32 products into 16 wave-uniform dwords.
-__device__ __forceinline__ uint32_t mul16_x() {
-  const int lane = threadIdx.x & 63;
-  return (uint32_t)(lane & 3) << (2 * ((lane >> 2) & 7));
-}
+// x * exp(lm) for a field element x with log logx (0 for x = 0)
 __device__ __forceinline__ uint32_t mul16_prod(uint32_t x, uint32_t logx, uint32_t lm) {
   uint32_t sidx = logx + lm;
   sidx = (sidx + (sidx >> 16)) & 0xFFFFu;
   return x ? (uint32_t)g_exp16[sidx] : 0u;
 }
-__device__ __forceinline__ void mul16_pack(uint32_t prod, uint32_t (&t)[16]) {
-  const int e2 = threadIdx.x & 3;
-  uint32_t vlo = (prod & 0xFFu) << (8 * e2), vhi = ((prod >> 8) & 0xFFu) << (8 * e2);
-  vlo |= (uint32_t)__builtin_amdgcn_mov_dpp((int)vlo, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-  vhi |= (uint32_t)__builtin_amdgcn_mov_dpp((int)vhi, 0xB1, 0xF, 0xF, false);
-  vlo |= (uint32_t)__builtin_amdgcn_mov_dpp((int)vlo, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-  vhi |= (uint32_t)__builtin_amdgcn_mov_dpp((int)vhi, 0x4E, 0xF, 0xF, false);
-#pragma unroll
-  for (int gg = 0; gg < 8; gg++) {
-    t[gg] = __builtin_amdgcn_readlane(vlo, 4 * gg);
-    t[8 + gg] = __builtin_amdgcn_readlane(vhi, 4 * gg);
-  }
-}
 
-// (xlo, xhi) = (xlo, xhi) * exp(lm) with the table of mul16_pack
+// (xlo, xhi) = (xlo, xhi) * exp(lm) with its 16-dword product table (mul16_table_to)
 __device__ __forceinline__ void mul16_by(uint32_t& xlo, uint32_t& xhi, const uint32_t (&t)[16]) {
   uint32_t pl[8], ph[8];
 #pragma unroll
@@ -750,6 +730,43 @@ __device__ __forceinline__ void mul16_by(uint32_t& xlo, uint32_t& xhi, const uin
   }
   xlo = xor3(xor3(xor3(pl[0], pl[1], pl[2]), pl[3], pl[4]), xor3(pl[5], pl[6], pl[7]), 0u);
   xhi = xor3(xor3(xor3(ph[0], ph[1], ph[2]), ph[3], ph[4]), xor3(ph[5], ph[6], ph[7]), 0u);
+}
+
+// The decoders' per-element tables are built in LDS, one element per thread
+// with all its gathers in flight at once (round 3; rounds 1-2 built them per
+// wave -- one exp() gather per lane, 4 DPP ORs and 16 v_readlane per element --
+// and the k = 512 decoder waited on memory half of its cycles).
+// out[G] byte e2 = low byte of (e2 << 2G) * exp(lm), out[8 + G] its high byte.
+__device__ __forceinline__ void mul16_table_to(uint32_t* out, uint32_t lm) {
+  uint32_t lo[8], hi[8];
+#pragma unroll
+  for (int G = 0; G < 8; G++) {
+    lo[G] = hi[G] = 0u;
+#pragma unroll
+    for (int e2 = 1; e2 < 4; e2++) {
+      const uint32_t x = (uint32_t)e2 << (2 * G);
+      const uint32_t p = mul16_prod(x, (uint32_t)g_log16[x], lm);
+      lo[G] |= (p & 0xFFu) << (8 * e2);
+      hi[G] |= (p >> 8) << (8 * e2);
+    }
+  }
+  uint4* o = (uint4*)out;
+  o[0] = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+  o[1] = make_uint4(lo[4], lo[5], lo[6], lo[7]);
+  o[2] = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+  o[3] = make_uint4(hi[4], hi[5], hi[6], hi[7]);
+}
+// the table of element e from LDS (every lane of the wave reads the same 64 B)
+__device__ __forceinline__ void mul16_table_from(const uint32_t* tab, int e, uint32_t (&t)[16]) {
+  const uint4* q = (const uint4*)(tab + e * 16);
+#pragma unroll
+  for (int h = 0; h < 4; h++) {
+    const uint4 v = q[h];
+    t[4 * h] = v.x;
+    t[4 * h + 1] = v.y;
+    t[4 * h + 2] = v.z;
+    t[4 * h + 3] = v.w;
+  }
 }
 
 // Formal derivative in the transposed layout (wave c: element bits 3-5 = c,
@@ -790,7 +807,11 @@ __device__ __forceinline__ void derivative16_xposed(W16& w, uint32_t* lds, int c
 __global__ __launch_bounds__(kDecN) __attribute__((amdgpu_waves_per_eu(2, 2))) void leo16_decode_reg_kernel(
     DecodeArgs a) {
   constexpr int M = kDecN, P = 8, S = 1, K = M / 2;
-  __shared__ uint32_t lds[P * 16 * 2 * 64];  // derivative staging (64 KiB) >= transpose (32 KiB)
+  // dynamic LDS (kDecLds): derivative staging (64 KiB) >= transpose (32 KiB),
+  // then the erased elements' product tables (32 KiB), built up front
+  extern __shared__ __attribute__((aligned(16))) uint32_t dyn_lds[];
+  uint32_t* lds = dyn_lds;
+  uint32_t* post_tab = dyn_lds + P * 16 * 2 * 64;
   const long blk = blockIdx.x;
   const int chunk = (int)(blk % a.nchunk);
   const long v = blk / a.nchunk;
@@ -821,26 +842,23 @@ __global__ __launch_bounds__(kDecN) __attribute__((amdgpu_waves_per_eu(2, 2))) v
     w.lo[j] = p ? lo : 0u;
     w.hi[j] = p ? hi : 0u;
   }
-  // work *= errLocs: one product table per element, the exp() gathers of 16
-  // elements in flight at a time
-  const uint32_t mx = mul16_x();
-  const uint32_t mlogx = mx ? (uint32_t)g_log16[mx] : 0u;
+  // work *= errLocs: thread i builds element i's tables in LDS (the premultiply
+  // one in the transpose buffer, free until the first transpose; the erasure
+  // one kept to the end), each wave then reads its 64 elements' tables
+  mul16_table_to(lds + threadIdx.x * 16, my_err);
+  mul16_table_to(post_tab + threadIdx.x * 16, kMod16 - my_err);
+  __syncthreads();
 #pragma unroll
-  for (int j0 = 0; j0 < 64; j0 += 16) {
-    uint32_t prod[16];
-#pragma unroll
-    for (int u = 0; u < 16; u++) prod[u] = mul16_prod(mx, mlogx, __builtin_amdgcn_readlane(my_err, j0 + u));
-#pragma unroll
-    for (int u = 0; u < 16; u++) {
-      uint32_t t[16];
-      mul16_pack(prod[u], t);
-      uint32_t xl = w.lo[j0 + u], xh = w.hi[j0 + u];
-      mul16_by(xl, xh, t);
-      w.lo[j0 + u] = xl;
-      w.hi[j0 + u] = xh;
-    }
-    __builtin_amdgcn_sched_barrier(0);
+  for (int j = 0; j < 64; j++) {
+    uint32_t t[16];
+    mul16_table_from(lds, 64 * q + j, t);
+    uint32_t xl = w.lo[j], xh = w.hi[j];
+    mul16_by(xl, xh, t);
+    w.lo[j] = xl;
+    w.hi[j] = xh;
+    __builtin_amdgcn_sched_barrier(0);  // one element's table live at a time
   }
+  __syncthreads();  // the transpose reuses lds
   // ---- IFFT (ifftDITDecoder, skew index iend - 1) ----
   ifft16_block<1>(w, -1 + 64 * q);  // bits 0-5
   xpose16<P, S>(w, lds, q, lane);
@@ -875,30 +893,20 @@ __global__ __launch_bounds__(kDecN) __attribute__((amdgpu_waves_per_eu(2, 2))) v
 #pragma unroll
   for (int j = 0; j < 32; j++) fft2_16(w, j, j + 32, 64 * q + 31);  // second sub-layer (bit 5)
   fft16_block<8>(w, 64 * q);                                         // bits 4 .. 0
-  // erased shards = work * (65535 - errLocs); every lane builds the tables
-  // (mul16_table reads lanes 0..31), only active lanes store
+  // erased shards = work * (65535 - errLocs); only active lanes store
 #pragma unroll
-  for (int j0 = 0; j0 < 64; j0 += 16) {
-    if (((pm >> j0) & 0xFFFFull) == 0xFFFFull) continue;  // uniform: no erasure among these 16
-    uint32_t prod[16];
-#pragma unroll
-    for (int u = 0; u < 16; u++)
-      prod[u] = mul16_prod(mx, mlogx, kMod16 - __builtin_amdgcn_readlane(my_err, j0 + u));
-#pragma unroll
-    for (int u = 0; u < 16; u++) {
-    const int j = j0 + u;
+  for (int j = 0; j < 64; j++) {
     if ((pm >> j) & 1) continue;  // uniform
     const int i = 64 * q + j;
     const int shard = i < K ? K + i : i - K;
     uint32_t t[16];
-    mul16_pack(prod[u], t);
+    mul16_table_from(post_tab, i, t);
     uint32_t xl = w.lo[j], xh = w.hi[j];
     mul16_by(xl, xh, t);
     const uint32_t so = (uint32_t)shard * (uint32_t)a.shard_stride;
     if (active) {
       __builtin_amdgcn_raw_buffer_store_b32(xl, rsrc, col, so, 0);
       __builtin_amdgcn_raw_buffer_store_b32(xh, rsrc, col + 32u, so, 0);
-    }
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -1027,7 +1035,11 @@ __device__ __forceinline__ void derivativep(W1k& w, uint32_t* lds, int c, int la
 __global__ __launch_bounds__(kDec1k) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_decode_reg1k_kernel(
     DecodeArgs a) {
   constexpr int K = kDec1k / 2;
-  __shared__ uint32_t lds[16 * 16 * 64];  // 64 KiB: transpose rounds and derivative staging
+  // dynamic LDS (kDec1kLds): transpose rounds and derivative staging (64 KiB),
+  // then the erased elements' product tables (64 KiB), built up front
+  extern __shared__ __attribute__((aligned(16))) uint32_t dyn_lds[];
+  uint32_t* lds = dyn_lds;
+  uint32_t* post_tab = dyn_lds + 16 * 16 * 64;
   const long blk = blockIdx.x;
   const int half = (int)(blk % a.nchunk);  // nchunk = 256-B pieces of the shard
   const long v = blk / a.nchunk;
@@ -1054,22 +1066,20 @@ __global__ __launch_bounds__(kDec1k) __attribute__((amdgpu_waves_per_eu(4, 4))) 
     const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b16(rsrc, col + 32u, so, 0);
     w.v[j] = ((pm >> j) & 1) ? (lo | (hi << 16)) : 0u;
   }
-  // work *= errLocs (per-element tables, 16 elements' gathers in flight)
-  const uint32_t mx = mul16_x();
-  const uint32_t mlogx = mx ? (uint32_t)g_log16[mx] : 0u;
+  // work *= errLocs: thread i builds element i's tables in LDS (the premultiply
+  // one in the transpose buffer, free until the first transpose; the erasure
+  // one kept to the end), each wave then reads its 64 elements' tables
+  mul16_table_to(lds + threadIdx.x * 16, my_err);
+  mul16_table_to(post_tab + threadIdx.x * 16, kMod16 - my_err);
+  __syncthreads();
 #pragma unroll
-  for (int j0 = 0; j0 < 64; j0 += 8) {
-    uint32_t prod[8];
-#pragma unroll
-    for (int u = 0; u < 8; u++) prod[u] = mul16_prod(mx, mlogx, __builtin_amdgcn_readlane(my_err, j0 + u));
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      uint32_t t[16];
-      mul16_pack(prod[u], t);
-      w.v[j0 + u] = mulp(w.v[j0 + u], t);
-    }
-    __builtin_amdgcn_sched_barrier(0);
+  for (int j = 0; j < 64; j++) {
+    uint32_t t[16];
+    mul16_table_from(lds, 64 * q + j, t);
+    w.v[j] = mulp(w.v[j], t);
+    __builtin_amdgcn_sched_barrier(0);  // one element's table live at a time
   }
+  __syncthreads();  // the transpose reuses lds
   // ---- IFFT (ifftDITDecoder, skew index iend - 1) ----
   ifftp_block<1>(w, -1 + 64 * q);  // bits 0-5
   xposep(w, lds, q, lane);
@@ -1121,24 +1131,16 @@ __global__ __launch_bounds__(kDec1k) __attribute__((amdgpu_waves_per_eu(4, 4))) 
   fftp_block<16>(w, 64 * q);  // dist 16, 4, 1 (bits 5 .. 0)
   // erased shards = work * (65535 - errLocs)
 #pragma unroll
-  for (int j0 = 0; j0 < 64; j0 += 8) {
-    if (((pm >> j0) & 0xFFull) == 0xFFull) continue;  // uniform
-    uint32_t prod[8];
-#pragma unroll
-    for (int u = 0; u < 8; u++) prod[u] = mul16_prod(mx, mlogx, kMod16 - __builtin_amdgcn_readlane(my_err, j0 + u));
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const int j = j0 + u;
-      if ((pm >> j) & 1) continue;  // uniform
-      const int i = 64 * q + j;
-      const int shard = i < K ? K + i : i - K;
-      uint32_t t[16];
-      mul16_pack(prod[u], t);
-      const uint32_t r = mulp(w.v[j], t);
-      const uint32_t so = (uint32_t)shard * (uint32_t)a.shard_stride;
-      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(r & 0xFFFFu), rsrc, col, so, 0);
-      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(r >> 16), rsrc, col + 32u, so, 0);
-    }
+  for (int j = 0; j < 64; j++) {
+    if ((pm >> j) & 1) continue;  // uniform
+    const int i = 64 * q + j;
+    const int shard = i < K ? K + i : i - K;
+    uint32_t t[16];
+    mul16_table_from(post_tab, i, t);
+    const uint32_t r = mulp(w.v[j], t);
+    const uint32_t so = (uint32_t)shard * (uint32_t)a.shard_stride;
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(r & 0xFFFFu), rsrc, col, so, 0);
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(r >> 16), rsrc, col + 32u, so, 0);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -1246,6 +1248,22 @@ hipError_t launch_leo16_errlocs(const DecodeArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// dynamic LDS of the register-resident decoders: staging + erasure tables
+constexpr size_t kDecLds = (8 * 16 * 2 * 64 + kDecN * 16) * sizeof(uint32_t);    // 96 KiB
+constexpr size_t kDec1kLds = (16 * 16 * 64 + kDec1k * 16) * sizeof(uint32_t);     // 128 KiB
+static hipError_t dec_lds_attr() {  // above the 64 KiB default: once per process
+  static std::once_flag once;
+  static hipError_t err = hipSuccess;
+  std::call_once(once, [] {
+    err = hipFuncSetAttribute((const void*)leo16_decode_reg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kDecLds);
+    if (err == hipSuccess)
+      err = hipFuncSetAttribute((const void*)leo16_decode_reg1k_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDec1kLds);
+  });
+  return err;
+}
+
 hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mark_present) {
   if (!gf16_k_ok(a.k) || a.shard_bytes % 64) return hipErrorInvalidValue;
   hipError_t e = ensure_tables();
@@ -1256,11 +1274,13 @@ hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mar
   if (a.k == kDecN / 2) {  // register-resident decoder; nchunk = 512-B chunks of the shard
     DecodeArgs b = a;
     b.nchunk = (a.shard_bytes + 511) / 512;
-    hipLaunchKernelGGL(leo16_decode_reg_kernel, dim3((unsigned)(nv * b.nchunk)), dim3(kDecN), 0, s, b);
+    if ((e = dec_lds_attr()) != hipSuccess) return e;
+    hipLaunchKernelGGL(leo16_decode_reg_kernel, dim3((unsigned)(nv * b.nchunk)), dim3(kDecN), kDecLds, s, b);
   } else if (a.k == kDec1k / 2 && a.shard_bytes % 256 == 0) {  // k = 512: 256-B pieces
     DecodeArgs b = a;
     b.nchunk = a.shard_bytes / 256;
-    hipLaunchKernelGGL(leo16_decode_reg1k_kernel, dim3((unsigned)(nv * b.nchunk)), dim3(kDec1k), 0, s, b);
+    if ((e = dec_lds_attr()) != hipSuccess) return e;
+    hipLaunchKernelGGL(leo16_decode_reg1k_kernel, dim3((unsigned)(nv * b.nchunk)), dim3(kDec1k), kDec1kLds, s, b);
   } else
 #endif
   {

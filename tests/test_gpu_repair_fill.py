@@ -152,3 +152,18 @@ def test_fill_equals_decoder_gf16(ctx, monkeypatch):
     specs = [("subgrid", None), ("left_half", "parity_half"), ("rows_plus", None)]
     st = _case(ctx, monkeypatch, 256, specs, 2560, oracle_check=False)
     assert st[0] == 0 and st[1] == _abi.ERR_BYZANTINE and st[2] == 0
+
+
+@pytest.mark.parametrize("k", [8, 32])
+def test_fill_random_sweep(ctx, monkeypatch, k):
+    """48 squares, each a random pattern kind and density, a third of them with
+    one corrupted given share: the shortcut equals the plain schedule byte for
+    byte, and every status equals the oracle's."""
+    rng = np.random.default_rng(9000 + k)
+    kinds = ["subgrid", "subgrid_top", "q0", "left_half", "rows_plus", "unrepairable"]
+    specs = []
+    for i in range(48):
+        kind = kinds[i % len(kinds)] if i < 24 else f"{rng.uniform(0.35, 0.9):.2f}"
+        corrupt = ("any", "parity_half", None)[i % 3]
+        specs.append((kind, corrupt))
+    _case(ctx, monkeypatch, k, specs, 9100 + k)
