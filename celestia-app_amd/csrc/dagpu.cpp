@@ -407,6 +407,7 @@ void dagpu_destroy(dagpu_ctx* c) {
     for (hipStream_t x : {cs.rs, cs.rs_hi, cs.nmt})
       if (x) (void)hipStreamSynchronize(x);
   for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+  for (void* m : c->mailboxes) (void)hipHostFree(m);
   for (auto& cs : c->side)
     for (hipStream_t x : {cs.rs, cs.rs_hi, cs.nmt})
       if (x) (void)hipStreamDestroy(x);
@@ -1086,6 +1087,40 @@ int exact_repair(dagpu_ctx* ctx, uint32_t k, size_t n, size_t sq, uint8_t* d_eds
   return DAGPU_OK;
 }
 
+// A page-locked mailbox for the round counters (RAII; back to the context's pool).
+struct Mailbox {
+  dagpu_ctx* c;
+  void* p = nullptr;
+  explicit Mailbox(dagpu_ctx* c_) : c(c_) {
+    {
+      std::lock_guard<std::mutex> g(c->mb_mu);
+      if (!c->mailboxes.empty()) {
+        p = c->mailboxes.back();
+        c->mailboxes.pop_back();
+        return;
+      }
+    }
+    if (hipHostMalloc(&p, dagpu_ctx::kMailbox, hipHostMallocDefault) != hipSuccess) p = nullptr;
+  }
+  ~Mailbox() {
+    if (!p) return;
+    std::lock_guard<std::mutex> g(c->mb_mu);
+    c->mailboxes.push_back(p);
+  }
+};
+
+// Small device->host read that the next host decision waits for: into the
+// mailbox when there is one (a direct DMA), then a spin on the stream (the
+// blocking wait's wake-up cost 50-200 us per Repair round, profiles/
+// repair_timeline_r03.txt).
+hipError_t read_small(void* dst, const void* src, size_t bytes, Mailbox& mb, hipStream_t s) {
+  void* via = (mb.p && bytes <= dagpu_ctx::kMailbox) ? mb.p : dst;
+  hipError_t e = hipMemcpyAsync(via, src, bytes, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = wait_stream(s, true);
+  if (e == hipSuccess && via != dst) memcpy(dst, via, bytes);
+  return e;
+}
+
 // rsmt2d Repair for n same-k squares resident on the device (see repair.hip).
 // d_byz (optional, n * 4 int32): failing axis per square; asking for it makes
 // the call resolve crossword failures in rsmt2d's order (exact_repair).
@@ -1140,6 +1175,7 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
     HIP_TRY(ctx, hipMemsetAsync(r.nodefer, 0, n * sizeof(int32_t), s));
   }
   const int max_rounds = 4 * (int)w + 4;
+  Mailbox mb(ctx);
   for (int pass = 0; pass < 2; pass++) {
     long deferred_total = 0;
     int last_ax = -1;
@@ -1154,8 +1190,7 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
       HIP_TRY(ctx, launch_vec_count(dr, s));
       HIP_TRY(ctx, launch_vec_count(dc, s));
       int32_t cnt[3] = {0, 0, 0};
-      HIP_TRY(ctx, hipMemcpyAsync(cnt, r.counters, sizeof cnt, hipMemcpyDeviceToHost, s));
-      HIP_TRY(ctx, hipStreamSynchronize(s));
+      HIP_TRY(ctx, read_small(cnt, r.counters, sizeof cnt, mb, s));
       deferred_total += cnt[2];
       if (cnt[0] == 0 && cnt[1] == 0) break;
       int ax = cnt[0] >= cnt[1] ? 0 : 1;
@@ -1239,8 +1274,7 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
       HIP_TRY(ctx, launch_rs_encode((int)k, e, s));
     }
     std::vector<int32_t> chk(n);
-    HIP_TRY(ctx, hipMemcpyAsync(chk.data(), r.check, n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY(ctx, hipStreamSynchronize(s));
+    HIP_TRY(ctx, read_small(chk.data(), r.check, n * sizeof(int32_t), mb, s));
     bool rerun = false;
     for (size_t i = 0; i < n; i++) {
       if (!chk[i]) continue;

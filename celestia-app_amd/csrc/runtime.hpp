@@ -95,6 +95,11 @@ struct dagpu_ctx {
   std::vector<Side> side;
   std::mutex ev_mu;
   std::vector<hipEvent_t> ev_pool;  // timing-disabled events, recycled per call
+  // page-locked 4 KiB mailboxes for the small device->host reads of Repair's
+  // rounds (counters, check flags), one per concurrent call, recycled
+  static constexpr size_t kMailbox = 4096;
+  std::mutex mb_mu;
+  std::vector<void*> mailboxes;
   hipEvent_t ev_loaded[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
   HostBuf h_out;
   // generic forests / commitments / split square (trees.cpp, split.cpp)
