@@ -167,3 +167,48 @@ def test_fill_random_sweep(ctx, monkeypatch, k):
         corrupt = ("any", "parity_half", None)[i % 3]
         specs.append((kind, corrupt))
     _case(ctx, monkeypatch, k, specs, 9100 + k)
+
+
+def test_two_threads_repair_one_context(ctx):
+    """Two host threads repairing their own k = 64 batches on their own streams
+    through ONE context (each call takes its own page-locked mailbox for the
+    round counters): both batches come back bit-exact."""
+    import threading
+
+    k, n = 64, 16
+    w = 2 * k
+    sets, out, errors = {}, {}, []
+    for name, seed in (("a", 1700), ("b", 1701)):
+        rng = np.random.default_rng(seed)
+        ds = DeviceSquares(k, n, ctx=ctx, in_place=True)
+        ds.load_ods(synth.blob_squares(k, seed, 0, n, threads=16))
+        ds.extend()
+        torch.cuda.synchronize()
+        ref = ds.eds.clone()
+        pres = np.stack([_pattern("subgrid", k, rng) for _ in range(n)]).reshape(n, -1).astype(np.uint8)
+        present = torch.from_numpy(pres).cuda()
+        ds.eds.copy_((ds.eds.view(n, w * w, 512) * present.view(n, w * w, 1)).view(n, -1))
+        status = torch.full((n,), -99, dtype=torch.int32, device="cuda")
+        sets[name] = (ds, ref, present, status, ds.repair_workspace(), torch.cuda.Stream())
+    torch.cuda.synchronize()
+
+    def worker(name):
+        ds, _, present, status, ws, st = sets[name]
+        try:
+            ds.repair(present, status, ws, stream=st)
+            st.synchronize()
+            out[name] = status.cpu().numpy().copy()
+        except Exception as e:  # pragma: no cover
+            errors.append((name, repr(e)))
+
+    ts = [threading.Thread(target=worker, args=(x,)) for x in sets]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=100)
+    assert not errors, errors
+    for name, (ds, ref, present, _, _, _) in sets.items():
+        assert (out[name] == 0).all(), name
+        assert torch.equal(ds.eds, ref) and bool((present == 1).all()), name
+    del sets
+    torch.cuda.empty_cache()
