@@ -827,10 +827,11 @@ struct RepairWs {
   int32_t* err_share[2][2];  // [axis][same, head]
   int32_t* sel;         // exact-order repair: level of each axis' attempt, [2][w]
   int32_t* bits;
-  int32_t* counters;    // [0] decodable rows, [1] decodable cols, [2] deferred, [3] fill pairs
+  int32_t* counters;    // [0] decodable rows, [1] decodable cols, [2] deferred, [3] / [4] fill / reverse fill pairs
   // fill route / deferral (repair.hip PlanArgs)
   int32_t* fill;        // [sq][idx] of the round's axis
   int32_t* pair_list;   // k = 128 fill pairs, n * w entries
+  int32_t* pair_list_rev;  // k = 128 reverse fill pairs, n * w entries
   int32_t* known;       // [axis][sq][idx]
   int32_t* deferred;    // [axis][sq][idx]
   int32_t* nodefer;     // [sq]
@@ -850,7 +851,8 @@ size_t repair_ws_bytes(uint32_t k, size_t n) {
   t += 4 * a256(n * w * 4);                                             // err_key, err_head per axis
   t += a256(2 * w * 4);                                                 // sel
   t += a256(n * 4) + 256;                                         // bits, counters
-  t += 2 * a256(n * w * 4) + 2 * a256(n * 2 * w * 4) + 2 * a256(n * 4);  // fill, pairs, known, deferred, nodefer, check
+  t += 3 * a256(n * w * 4);                                                 // fill, pairs, reverse pairs
+  t += 2 * a256(n * 2 * w * 4) + 2 * a256(n * 4);                           // known, deferred, nodefer, check
   t += 2 * a256(n * w * 4);                                                 // counts
   return t;
 }
@@ -886,6 +888,7 @@ RepairWs carve_repair(uint32_t k, size_t n, void* base) {
   r.counters = (int32_t*)p; p += 256;
   r.fill = (int32_t*)p; p += a256(n * w * 4);
   r.pair_list = (int32_t*)p; p += a256(n * w * 4);
+  r.pair_list_rev = (int32_t*)p; p += a256(n * w * 4);
   r.known = (int32_t*)p; p += a256(n * 2 * w * 4);
   r.deferred = (int32_t*)p; p += a256(n * 2 * w * 4);
   r.nodefer = (int32_t*)p; p += a256(n * 4);
@@ -1157,10 +1160,14 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
   // column (whichever set is larger) until no axis can make progress.
   // Fill route and deferral (repair.hip PlanArgs; DAGPU_REPAIR_FILL=0 turns
   // them off): a decodable vector whose data half is complete is re-encoded
-  // instead of decoded; when every vector i < k of an axis is decodable or
+  // instead of decoded, and one whose parity half is complete is rebuilt by the
+  // reverse transform (EncodeArgs.reverse); both give the decoder's bytes
+  // whenever the vector's given shards agree with them, and a vector whose
+  // given shards disagree goes to the decoder; when every vector i < k of an axis is decodable or
   // complete, the decodes of i >= k wait and the next round (the other axis)
-  // fills everything.  For the maximal erasure pattern that is k row decodes,
-  // k column decodes and k row fills instead of k + 2k decodes.  A deferred
+  // fills everything.  For the maximal erasure pattern (Q3 given) that is k
+  // reverse row fills, k reverse column fills and k row fills instead of
+  // k + 2k decodes.  A deferred
   // vector the decoder would have rebuilt is the same codeword whenever the
   // square ends up a codeword square, which the known[] bookkeeping proves for
   // that pattern; otherwise a compare-mode encode checks every deferred vector,
@@ -1199,7 +1206,7 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
       last_ax = ax;
       DecodeArgs& d = ax == 0 ? dr : dc;
       if (shortcut) {
-        HIP_TRY(ctx, hipMemsetAsync(r.counters + 2, 0, 2 * sizeof(int32_t), s));
+        HIP_TRY(ctx, hipMemsetAsync(r.counters + 2, 0, 3 * sizeof(int32_t), s));
         const long w_ = w;
         EncodeArgs e{};
         e.in = d_eds;
@@ -1223,6 +1230,8 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
         pa.fill = r.fill;
         pa.pair_list = listed ? r.pair_list : nullptr;
         pa.pair_count = r.counters + 3;
+        pa.pair_list_rev = listed ? r.pair_list_rev : nullptr;
+        pa.pair_count_rev = r.counters + 4;
         pa.known = r.known;
         pa.deferred = r.deferred;
         pa.nodefer = r.nodefer;
@@ -1233,13 +1242,25 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
         HIP_TRY(ctx, launch_repair_plan(pa, s));
         {
           ProfScope p(ctx, 6, s);
+          // reverse fills: parity half in, data half out (its presence k shards before)
+          EncodeArgs er = e;
+          er.in = e.out;
+          er.out = (uint8_t*)e.in;
+          er.out_present = e.out_present - (long)k * e.op_shard_stride;
+          er.reverse = 1;
           if (listed) {
             e.pair_list = r.pair_list;
             e.pair_count = r.counters + 3;
             HIP_TRY(ctx, launch_leo8_fill_sliced(e, (long)n * w_ / 2, s));
+            er.pair_list = r.pair_list_rev;
+            er.pair_count = r.counters + 4;
+            HIP_TRY(ctx, launch_leo8_fill_sliced(er, (long)n * w_ / 2, s));
           } else {
-            e.vec_flags = r.fill;
+            e.vec_flags = er.vec_flags = r.fill;
+            e.vec_flag_match = 1;
+            er.vec_flag_match = 2;
             HIP_TRY(ctx, launch_rs_encode((int)k, e, s));
+            HIP_TRY(ctx, launch_rs_encode((int)k, er, s));
           }
         }
       }

@@ -50,10 +50,26 @@ struct EncodeArgs {
   int32_t* redo;
   const int32_t* pair_list;
   const int32_t* pair_count;
+  // Reverse transform (Repair reverse fill): `in` holds the parity half of each
+  // vector and `out` receives its data half.  Leopard's encode is
+  // parity = FFT(skew offset 0) of IFFT(skew offset k) of the data, both over
+  // the same polynomial of degree < k (k = m, a power of two), so
+  // data = FFT(offset k) of IFFT(offset 0) of the parity.  Fill mode only.
+  int reverse;
+  // With vec_flags: 0 = every nonzero entry selects its vector; otherwise only
+  // entries equal to vec_flag_match do (Repair fill: 1 forward, 2 reverse).
+  int vec_flag_match;
 };
 
 __device__ __forceinline__ bool fill_given(const EncodeArgs& a, long sq, long vec, long j) {
   return a.out_present[sq * a.op_sq_stride + vec * a.op_vec_stride + j * a.op_shard_stride] != 0;
+}
+
+// vector v (flattened sq * nvec + vec) not selected by vec_flags (wave-uniform)
+__device__ __forceinline__ bool vec_skipped(const EncodeArgs& a, long v) {
+  if (!a.vec_flags) return false;
+  const int32_t f = a.vec_flags[v];
+  return a.vec_flag_match ? f != a.vec_flag_match : f == 0;
 }
 
 hipError_t launch_leo8_encode(int k, const EncodeArgs& a, hipStream_t s);
@@ -152,7 +168,9 @@ hipError_t launch_verify_roots(const uint8_t* exp_rr, const uint8_t* exp_cr, con
 // crossword failure (kRepByz, axis resolved by the host), else unrepairable
 // Repair shortcut plan for one round on one axis (see repair_device): every
 // decodable vector of the axis whose data half is complete moves from the
-// decoder (flags) to the fill encoder (fill, and pair_list when set); when every
+// decoder (flags) to the fill encoder (fill[v] = 1, forward), and one whose
+// parity half is complete to the reverse fill (fill[v] = 2); pair_list /
+// pair_list_rev (when set) pair each square's forward / reverse fills; when every
 // vector i < k of a square is decodable or complete (and nodefer[sq] is 0), the
 // decodes of its vectors i >= k are deferred: the other axis then has complete
 // data halves everywhere and is filled in the next round.  known[axis][sq][i]
@@ -164,6 +182,8 @@ struct PlanArgs {
   int32_t* fill;
   int32_t* pair_list;
   int32_t* pair_count;
+  int32_t* pair_list_rev;
+  int32_t* pair_count_rev;
   int32_t* known;
   int32_t* deferred;
   const int32_t* nodefer;

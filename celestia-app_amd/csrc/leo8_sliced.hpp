@@ -305,7 +305,7 @@ struct Geo {
 // IFFT layers m = 0 .. n-5 in layout A (wave wa), distance D = 2^m:
 // ifftDIT28 y ^= x; x ^= skew * y.  Compile-time part of the skew: element
 // k + (register block start); runtime part: W(m, wa) from wm_base[m * wstride].
-template <int K>
+template <int K, int IO = K>
 __host__ __device__ __forceinline__ void ifft_A(uint32_t (&v)[16][8], const uint32_t* wm_base, int wstride) {
   static_for<Geo<K>::NB>([&](auto m) {
     constexpr int D = 1 << m;
@@ -313,7 +313,7 @@ __host__ __device__ __forceinline__ void ifft_A(uint32_t (&v)[16][8], const uint
     const uint32_t* wm = wm_base + m * wstride;
     static_for<16>([&](auto j) {
       if constexpr (!(j & D)) {
-        constexpr int c = skew_elem(D - 1 + K + (j & ~(2 * D - 1)));
+        constexpr int c = skew_elem(D - 1 + IO + (j & ~(2 * D - 1)));
         xor8(v[j + D], v[j]);
         muladd_rt<c>(v[j], v[j + D], wm);
       }
@@ -322,7 +322,7 @@ __host__ __device__ __forceinline__ void ifft_A(uint32_t (&v)[16][8], const uint
 }
 
 // FFT layers m = n-5 .. 0 in layout A: fftDIT28 x ^= skew * y; y ^= x.
-template <int K>
+template <int K, int FO = 0>
 __host__ __device__ __forceinline__ void fft_A(uint32_t (&v)[16][8], const uint32_t* wm_base, int wstride) {
   static_for<Geo<K>::NB>([&](auto mm) {
     constexpr int m = Geo<K>::NB - 1 - mm;
@@ -331,7 +331,7 @@ __host__ __device__ __forceinline__ void fft_A(uint32_t (&v)[16][8], const uint3
     const uint32_t* wm = wm_base + m * wstride;
     static_for<16>([&](auto j) {
       if constexpr (!(j & D)) {
-        constexpr int c = skew_elem(D - 1 + (j & ~(2 * D - 1)));
+        constexpr int c = skew_elem(D - 1 + FO + (j & ~(2 * D - 1)));
         muladd_rt<c>(v[j], v[j + D], wm);
         xor8(v[j + D], v[j]);
       }
@@ -341,14 +341,14 @@ __host__ __device__ __forceinline__ void fft_A(uint32_t (&v)[16][8], const uint3
 
 // IFFT layers m = n-4 .. n-1 in layout B: element e = wb + NW * i, the block
 // start b = NW * (i with register bits <= m - NB cleared) -- compile-time.
-template <int K>
+template <int K, int IO = K>
 __host__ __device__ __forceinline__ void ifft_B(uint32_t (&v)[16][8]) {
   constexpr int NB = Geo<K>::NB, NW = Geo<K>::NW;
   static_for<4>([&](auto rb) {
     constexpr int D = 1 << (rb + NB), R = 1 << rb;
     static_for<16>([&](auto i) {
       if constexpr (!(i & R)) {
-        constexpr int c = skew_elem(D - 1 + K + NW * (i & ~(2 * R - 1)));
+        constexpr int c = skew_elem(D - 1 + IO + NW * (i & ~(2 * R - 1)));
         xor8(v[i + R], v[i]);
         muladd_ct<c>(v[i], v[i + R]);
       }
@@ -356,7 +356,7 @@ __host__ __device__ __forceinline__ void ifft_B(uint32_t (&v)[16][8]) {
   });
 }
 
-template <int K>
+template <int K, int FO = 0>
 __host__ __device__ __forceinline__ void fft_B(uint32_t (&v)[16][8]) {
   constexpr int NB = Geo<K>::NB, NW = Geo<K>::NW;
   static_for<4>([&](auto rr) {
@@ -364,7 +364,7 @@ __host__ __device__ __forceinline__ void fft_B(uint32_t (&v)[16][8]) {
     constexpr int D = 1 << (rb + NB), R = 1 << rb;
     static_for<16>([&](auto i) {
       if constexpr (!(i & R)) {
-        constexpr int c = skew_elem(D - 1 + NW * (i & ~(2 * R - 1)));
+        constexpr int c = skew_elem(D - 1 + FO + NW * (i & ~(2 * R - 1)));
         muladd_ct<c>(v[i], v[i + R]);
         xor8(v[i + R], v[i]);
       }
@@ -376,15 +376,16 @@ __host__ __device__ __forceinline__ void fft_B(uint32_t (&v)[16][8]) {
 // IFFT's last layer and the FFT's first act on the same pairs (i, i + 8), so
 //   y ^= x; x ^= c1 y;  x ^= c2 y; y ^= x   ==   y ^= x; x ^= (c1 ^ c2) y; y ^= x
 // (multiplication distributes over field addition; a "skip" skew is element 0):
-// one constant multiply per pair instead of two.
-template <int K>
+// one constant multiply per pair instead of two.  Skew offsets IO (IFFT) and
+// FO (FFT): K and 0 for the encode, 0 and K for the reverse fill.
+template <int K, int IO = K, int FO = 0>
 __host__ __device__ __forceinline__ void ifft_fft_B(uint32_t (&v)[16][8]) {
   constexpr int NB = Geo<K>::NB, NW = Geo<K>::NW;
   static_for<3>([&](auto rb) {  // IFFT layers n-4 .. n-2
     constexpr int D = 1 << (rb + NB), R = 1 << rb;
     static_for<16>([&](auto i) {
       if constexpr (!(i & R)) {
-        constexpr int c = skew_elem(D - 1 + K + NW * (i & ~(2 * R - 1)));
+        constexpr int c = skew_elem(D - 1 + IO + NW * (i & ~(2 * R - 1)));
         xor8(v[i + R], v[i]);
         muladd_ct<c>(v[i], v[i + R]);
       }
@@ -393,7 +394,7 @@ __host__ __device__ __forceinline__ void ifft_fft_B(uint32_t (&v)[16][8]) {
   {  // IFFT layer n-1 + FFT layer n-1 (pairs (i, i + 8); block start 0 for i < 8)
     constexpr int D = 1 << (3 + NB);
     static_for<8>([&](auto i) {
-      constexpr int c = skew_elem(D - 1 + K) ^ skew_elem(D - 1);
+      constexpr int c = skew_elem(D - 1 + IO) ^ skew_elem(D - 1 + FO);
       xor8(v[i + 8], v[i]);
       muladd_ct<c>(v[i], v[i + 8]);
       xor8(v[i + 8], v[i]);
@@ -404,7 +405,7 @@ __host__ __device__ __forceinline__ void ifft_fft_B(uint32_t (&v)[16][8]) {
     constexpr int D = 1 << (rb + NB), R = 1 << rb;
     static_for<16>([&](auto i) {
       if constexpr (!(i & R)) {
-        constexpr int c = skew_elem(D - 1 + NW * (i & ~(2 * R - 1)));
+        constexpr int c = skew_elem(D - 1 + FO + NW * (i & ~(2 * R - 1)));
         muladd_ct<c>(v[i], v[i + R]);
         xor8(v[i + R], v[i]);
       }
@@ -508,7 +509,7 @@ __host__ __device__ __forceinline__ void wave_switch4(int w, F&& f) {
 }
 
 // IFFT layers 0..NL-1 in the two-vector layout A (K = 128), wave w, lane mask of eb.
-template <int K, int NL = 3>
+template <int K, int NL = 3, int IO = K>
 __host__ __device__ __forceinline__ void ifft_A2(uint32_t (&v)[16][8], int w, uint32_t ebmask) {
   static_assert(K == 128, "two-vector layout: k = 128");
   if constexpr (DAGPU_WSPEC) {
@@ -520,7 +521,7 @@ __host__ __device__ __forceinline__ void ifft_A2(uint32_t (&v)[16][8], int w, ui
       });
       wave_switch4(w, [&](auto W) {
         static_for<16>([&](auto j) {
-          if constexpr (!(j & D)) muladd_ct<skew_elem(D - 1 + K + (j & ~(2 * D - 1)) + 32 * W)>(v[j], v[j + D]);
+          if constexpr (!(j & D)) muladd_ct<skew_elem(D - 1 + IO + (j & ~(2 * D - 1)) + 32 * W)>(v[j], v[j + D]);
         });
       });
       static_for<16>([&](auto j) {
@@ -534,7 +535,7 @@ __host__ __device__ __forceinline__ void ifft_A2(uint32_t (&v)[16][8], int w, ui
     SL_FENCE();
     static_for<16>([&](auto j) {
       if constexpr (!(j & D)) {
-        constexpr int c = skew_elem(D - 1 + K + (j & ~(2 * D - 1)));
+        constexpr int c = skew_elem(D - 1 + IO + (j & ~(2 * D - 1)));
         xor8(v[j + D], v[j]);
         muladd_ct<c>(v[j], v[j + D]);
       }
@@ -556,7 +557,7 @@ __host__ __device__ __forceinline__ void ifft_A2(uint32_t (&v)[16][8], int w, ui
 }
 
 // FFT layers NL-1..0 in the two-vector layout A.
-template <int K, int NL = 3>
+template <int K, int NL = 3, int FO = 0>
 __host__ __device__ __forceinline__ void fft_A2(uint32_t (&v)[16][8], int w, uint32_t ebmask) {
   static_assert(K == 128, "two-vector layout: k = 128");
   if constexpr (DAGPU_WSPEC) {
@@ -566,7 +567,7 @@ __host__ __device__ __forceinline__ void fft_A2(uint32_t (&v)[16][8], int w, uin
       SL_FENCE();
       wave_switch4(w, [&](auto W) {
         static_for<16>([&](auto j) {
-          if constexpr (!(j & D)) muladd_ct<skew_elem(D - 1 + (j & ~(2 * D - 1)) + 32 * W)>(v[j], v[j + D]);
+          if constexpr (!(j & D)) muladd_ct<skew_elem(D - 1 + FO + (j & ~(2 * D - 1)) + 32 * W)>(v[j], v[j + D]);
         });
       });
       static_for<16>([&](auto j) {
@@ -583,7 +584,7 @@ __host__ __device__ __forceinline__ void fft_A2(uint32_t (&v)[16][8], int w, uin
     constexpr int D = 1 << m;
     SL_FENCE();
     static_for<16>([&](auto j) {
-      if constexpr (!(j & D)) muladd_ct<skew_elem(D - 1 + (j & ~(2 * D - 1)))>(v[j], v[j + D]);
+      if constexpr (!(j & D)) muladd_ct<skew_elem(D - 1 + FO + (j & ~(2 * D - 1)))>(v[j], v[j + D]);
     });
     if (w & 1) {
       static_for<16>([&](auto j) {
@@ -609,7 +610,7 @@ __host__ __device__ __forceinline__ void fft_A2(uint32_t (&v)[16][8], int w, uin
 // bit 0 (a wave-local transpose of A).  Layers 1..2 pair register bits 0..1 of
 // r; their skews depend on element bits above the pair bit only, so the lane
 // bit drops out: C(register bits) ^ w0 S32 ^ w1 S64, no lane term.
-template <int K>
+template <int K, int IO = K>
 __host__ __device__ __forceinline__ void ifft_As2(uint32_t (&v)[16][8], int w) {
   static_assert(K == 128, "two-vector layout: k = 128");
   if constexpr (DAGPU_WSPEC) {
@@ -622,7 +623,7 @@ __host__ __device__ __forceinline__ void ifft_As2(uint32_t (&v)[16][8], int w) {
       });
       wave_switch4(w, [&](auto W) {
         static_for<16>([&](auto r) {
-          if constexpr (!(r & R)) muladd_ct<skew_elem(D - 1 + K + ((2 * r) & ~(2 * D - 1)) + 32 * W)>(v[r], v[r + R]);
+          if constexpr (!(r & R)) muladd_ct<skew_elem(D - 1 + IO + ((2 * r) & ~(2 * D - 1)) + 32 * W)>(v[r], v[r + R]);
         });
       });
     });
@@ -634,7 +635,7 @@ __host__ __device__ __forceinline__ void ifft_As2(uint32_t (&v)[16][8], int w) {
     SL_FENCE();
     static_for<16>([&](auto r) {
       if constexpr (!(r & R)) {
-        constexpr int c = skew_elem(D - 1 + K + ((2 * r) & ~(2 * D - 1)));
+        constexpr int c = skew_elem(D - 1 + IO + ((2 * r) & ~(2 * D - 1)));
         xor8(v[r + R], v[r]);
         muladd_ct<c>(v[r], v[r + R]);
       }
@@ -652,7 +653,7 @@ __host__ __device__ __forceinline__ void ifft_As2(uint32_t (&v)[16][8], int w) {
   });
 }
 
-template <int K>
+template <int K, int FO = 0>
 __host__ __device__ __forceinline__ void fft_As2(uint32_t (&v)[16][8], int w) {
   static_assert(K == 128, "two-vector layout: k = 128");
   if constexpr (DAGPU_WSPEC) {
@@ -662,7 +663,7 @@ __host__ __device__ __forceinline__ void fft_As2(uint32_t (&v)[16][8], int w) {
       SL_FENCE();
       wave_switch4(w, [&](auto W) {
         static_for<16>([&](auto r) {
-          if constexpr (!(r & R)) muladd_ct<skew_elem(D - 1 + ((2 * r) & ~(2 * D - 1)) + 32 * W)>(v[r], v[r + R]);
+          if constexpr (!(r & R)) muladd_ct<skew_elem(D - 1 + FO + ((2 * r) & ~(2 * D - 1)) + 32 * W)>(v[r], v[r + R]);
         });
       });
       static_for<16>([&](auto r) {
@@ -676,7 +677,7 @@ __host__ __device__ __forceinline__ void fft_As2(uint32_t (&v)[16][8], int w) {
     constexpr int D = 1 << m, R = D >> 1;
     SL_FENCE();
     static_for<16>([&](auto r) {
-      if constexpr (!(r & R)) muladd_ct<skew_elem(D - 1 + ((2 * r) & ~(2 * D - 1)))>(v[r], v[r + R]);
+      if constexpr (!(r & R)) muladd_ct<skew_elem(D - 1 + FO + ((2 * r) & ~(2 * D - 1)))>(v[r], v[r + R]);
     });
     if (w & 1) {
       static_for<16>([&](auto r) {

@@ -258,8 +258,8 @@ hipError_t launch_vec_count(const DecodeArgs& a, hipStream_t s) {
 
 __global__ __launch_bounds__(kPlanThreads) void repair_plan_kernel(PlanArgs p) {
   __shared__ int low_ok;
-  __shared__ int nfill_s[kPlanThreads];
-  __shared__ int base_s, total_s;
+  __shared__ int nfill_s[kPlanThreads], nrev_s[kPlanThreads];
+  __shared__ int base_s, rbase_s, total_s, rtotal_s;
   const long sq = blockIdx.x;
   const int k = p.k, w = 2 * k;
   if (threadIdx.x == 0) low_ok = 1;
@@ -282,19 +282,22 @@ __global__ __launch_bounds__(kPlanThreads) void repair_plan_kernel(PlanArgs p) {
   }
   __syncthreads();
   const bool defer = low_ok && !p.nodefer[sq];
-  int nf = 0, nd = 0;
+  int nf = 0, nr = 0, nd = 0;
   const long ax0 = (long)p.axis * p.nsq * w + sq * w;  // [axis][sq][idx]
 #pragma unroll
   for (int m = 0; m < kPer; m++) {
     const int i = threadIdx.x + kPlanThreads * m;
     if (i >= w) continue;
     const long v = sq * w + i;
+    // forward fill: data half complete; reverse fill: parity half complete
     const bool f = dec[m] && sys[m] == k;
-    p.fill[v] = f ? 1 : 0;
-    if (f) {
+    const bool r = dec[m] && !f && tot[m] - sys[m] == k;
+    p.fill[v] = f ? 1 : (r ? 2 : 0);
+    if (f || r) {
       p.flags[v] = 0;
       p.known[ax0 + i] = 1;
-      nf++;
+      if (f) nf++;
+      else nr++;
     } else if (dec[m]) {
       if (defer && i >= k) {
         p.flags[v] = 0;
@@ -307,28 +310,39 @@ __global__ __launch_bounds__(kPlanThreads) void repair_plan_kernel(PlanArgs p) {
   }
   if (nd) atomicAdd(p.ndeferred, nd);
   if (!p.pair_list) return;
-  // pair list: the square's fill vectors in pairs (an odd one paired with -1)
+  // pair lists: the square's forward fills in pairs, its reverse fills in
+  // pairs in the second list; an odd one is paired with -1
   nfill_s[threadIdx.x] = nf;
+  nrev_s[threadIdx.x] = nr;
   __syncthreads();
   if (threadIdx.x == 0) {
-    int acc = 0;
+    int acc = 0, racc = 0;
     for (int t = 0; t < kPlanThreads; t++) {
-      const int c = nfill_s[t];
+      const int c = nfill_s[t], rc = nrev_s[t];
       nfill_s[t] = acc;
+      nrev_s[t] = racc;
       acc += c;
+      racc += rc;
     }
     total_s = acc;
+    rtotal_s = racc;
     base_s = acc ? atomicAdd(p.pair_count, (acc + 1) / 2) : 0;
+    rbase_s = racc ? atomicAdd(p.pair_count_rev, (racc + 1) / 2) : 0;
   }
   __syncthreads();
   int32_t* out = p.pair_list + 2L * base_s;
-  int o = nfill_s[threadIdx.x];
+  int32_t* rout = p.pair_list_rev + 2L * rbase_s;
+  int o = nfill_s[threadIdx.x], ro = nrev_s[threadIdx.x];
 #pragma unroll
   for (int m = 0; m < kPer; m++) {
     const int i = threadIdx.x + kPlanThreads * m;
-    if (i < w && p.fill[sq * w + i]) out[o++] = (int32_t)(sq * w + i);
+    if (i >= w) continue;
+    const int32_t fv = p.fill[sq * w + i];
+    if (fv == 1) out[o++] = (int32_t)(sq * w + i);
+    else if (fv == 2) rout[ro++] = (int32_t)(sq * w + i);
   }
   if (threadIdx.x == 0 && (total_s & 1)) out[total_s] = -1;
+  if (threadIdx.x == 0 && (rtotal_s & 1)) rout[rtotal_s] = -1;
 }
 
 hipError_t launch_repair_plan(const PlanArgs& p, hipStream_t s) {

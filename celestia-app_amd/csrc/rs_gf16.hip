@@ -128,8 +128,9 @@ __device__ void ifft16(uint16_t* w, int m, int base) {
   }
 }
 
-// fftDIT over m elements (mtrunc = m), skew index iend - 1.
-__device__ void fft16(uint16_t* w, int m) {
+// fftDIT over m elements (mtrunc = m), skew index fo + iend - 1 (encode:
+// fo = 0; reverse fill: fo = m).
+__device__ void fft16(uint16_t* w, int m, int fo) {
   int dist4 = m, dist = m >> 2;
   while (dist != 0) {
     const int d = dist, d4 = dist4;
@@ -137,12 +138,12 @@ __device__ void fft16(uint16_t* w, int m) {
       const int r = (p / (2 * d)) * d4, q = p % (2 * d), iend = r + d;
       i = r + q;
       j = i + 2 * d;
-      lm = g_skew16[iend + d - 1];
+      lm = g_skew16[fo + iend + d - 1];
     });
     step16<false>(w, m / 2, [&](int p, int& i, int& j, uint32_t& lm) {
       const int r = (p / (2 * d)) * d4, q = p % (2 * d), iend = r + d;
-      if (q < d) { i = r + q; lm = g_skew16[iend - 1]; }
-      else { i = r + d + q; lm = g_skew16[iend + 2 * d - 1]; }
+      if (q < d) { i = r + q; lm = g_skew16[fo + iend - 1]; }
+      else { i = r + d + q; lm = g_skew16[fo + iend + 2 * d - 1]; }
       j = i + d;
     });
     dist4 = dist;
@@ -152,14 +153,15 @@ __device__ void fft16(uint16_t* w, int m) {
     step16<false>(w, m / 2, [&](int p, int& i, int& j, uint32_t& lm) {
       i = 2 * p;
       j = i + 1;
-      lm = g_skew16[i];
+      lm = g_skew16[fo + i];
     });
   }
 }
 
 // ---------------------------------------------------------------------------
 // Encode: parity = FFT_m(IFFT_m(data)), m = k.  Same EncodeArgs addressing as
-// the GF(2^8) encoder, including Q0 placement and compare mode.
+// the GF(2^8) encoder, including Q0 placement, compare mode and the reverse
+// fill (IFFT at skew offset 0, FFT at offset m).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kThreads16) void leo16_encode_kernel(EncodeArgs a, int k) {
   extern __shared__ __attribute__((aligned(16))) uint16_t w16[];  // k rows of 32 symbols
@@ -167,7 +169,7 @@ __global__ __launch_bounds__(kThreads16) void leo16_encode_kernel(EncodeArgs a, 
   const long blk = blockIdx.x % nblk;
   const long v = blockIdx.x / nblk;
   const long sq = v / a.nvec, vec = v % a.nvec;
-  if (a.vec_flags && a.vec_flags[v] == 0) return;  // uniform
+  if (vec_skipped(a, v)) return;  // uniform
   const uint8_t* in = a.in + sq * a.in_sq_stride + vec * a.in_vec_stride + blk * 64;
   for (int t = threadIdx.x; t < k * 8; t += kThreads16) {
     const int e = t >> 3, q = t & 7;
@@ -182,8 +184,8 @@ __global__ __launch_bounds__(kThreads16) void leo16_encode_kernel(EncodeArgs a, 
     }
   }
   __syncthreads();
-  ifft16(w16, k, k - 1);
-  fft16(w16, k);
+  ifft16(w16, k, a.reverse ? -1 : k - 1);
+  fft16(w16, k, a.reverse ? k : 0);
   uint8_t* out = a.out + sq * a.out_sq_stride + vec * a.out_vec_stride + blk * 64;
   bool diff = false;
   for (int t = threadIdx.x; t < k * 8; t += kThreads16) {
@@ -404,7 +406,7 @@ __global__ __launch_bounds__(kThreads16) void leo16_decode_kernel(DecodeArgs a) 
     der[t] = (uint16_t)acc;
   }
   __syncthreads();
-  fft16(der, n);
+  fft16(der, n, 0);
   // reveal erasures: shard = work[pos] * (65535 - errLocs[pos])
   for (int t = threadIdx.x; t < n * 32; t += kThreads16) {
     const int i = t >> 5;
@@ -507,7 +509,7 @@ __device__ __forceinline__ void ifft16_block(W16& w, int base) {
 }
 
 // Block layout, fftDIT radix-4 step with dist DIST (dist4 = 4 DIST) and the
-// ones below it; base = 64 q (skew index iend - 1).  The final radix-2 layer
+// ones below it; base = FO + 64 q (skew index FO + iend - 1).  The final radix-2 layer
 // exists when the last dist4 is 2.
 template <int DIST>
 __device__ __forceinline__ void fft16_block(W16& w, int base) {
@@ -561,8 +563,11 @@ __device__ __forceinline__ void xpose16(W16& w, uint32_t* lds, int q, int lane) 
   }
 }
 
-template <int M>
+// REV: the reverse fill (EncodeArgs.reverse): skew offsets IO = 0 for the IFFT
+// and FO = M for the FFT instead of M and 0 (positions stay below kTabPos).
+template <int M, bool REV>
 __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(3, 8))) void leo16_encode_reg_kernel(EncodeArgs a) {
+  constexpr int IO = REV ? 0 : M, FO = REV ? M : 0;
   constexpr int P = M / 64;
   constexpr int S = P == 8 ? 1 : 2;
   __shared__ uint32_t lds[P * P * S * 2 * 64];
@@ -571,7 +576,7 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(3, 8))) void 
   const long sv = blk / a.nchunk;
   const long vec = sv % a.nvec;
   const long sq = sv / a.nvec;
-  if (a.vec_flags && a.vec_flags[sv] == 0) return;  // uniform
+  if (vec_skipped(a, sv)) return;  // uniform
   const int lane = threadIdx.x & 63;
   const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t col = (uint32_t)chunk * 512u + (uint32_t)(lane >> 3) * 64u + (uint32_t)(lane & 7) * 4u;
@@ -596,13 +601,13 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(3, 8))) void 
       __builtin_amdgcn_raw_buffer_store_b32(w.hi[j], cp, col + 32u, so, 0);
     }
   }
-  // ---- IFFT (ifftDITEncoder, skew index M - 1 + iend) ----
-  ifft16_block<1>(w, M - 1 + 64 * q);  // bits 0-5
+  // ---- IFFT (ifftDITEncoder, skew index IO - 1 + iend) ----
+  ifft16_block<1>(w, IO - 1 + 64 * q);  // bits 0-5
   xpose16<P, S>(w, lds, q, lane);
   if constexpr (M == 512) {  // slot 8h + b: h = bits 6-8, b = bits 0-2
 #pragma unroll
     for (int hr = 0; hr < 8; hr += 4) {  // radix-4 dist 64 (bits 6, 7), groups r = 64 hr
-      const int p01 = M - 1 + 64 * hr + 64, p02 = p01 + 64, p23 = p01 + 128;
+      const int p01 = IO - 1 + 64 * hr + 64, p02 = p01 + 64, p23 = p01 + 128;
 #pragma unroll
       for (int b = 0; b < 8; b++) {
         const int s0 = hr * 8 + b;
@@ -613,25 +618,25 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(3, 8))) void 
       }
     }
 #pragma unroll
-    for (int s0 = 0; s0 < 32; s0++) ifft2_16(w, s0, s0 + 32, M - 1 + 256);  // last layer, dist 256
-    // ---- FFT (fftDIT, skew index iend - 1) ----
+    for (int s0 = 0; s0 < 32; s0++) ifft2_16(w, s0, s0 + 32, IO - 1 + 256);  // last layer, dist 256
+    // ---- FFT (fftDIT, skew index FO + iend - 1) ----
 #pragma unroll
     for (int s0 = 0; s0 < 16; s0++) {  // dist4 = 512, dist = 128 (bits 8, 7)
-      fft2_16(w, s0, s0 + 32, 255);
-      fft2_16(w, s0 + 16, s0 + 48, 255);
-      fft2_16(w, s0, s0 + 16, 127);
-      fft2_16(w, s0 + 32, s0 + 48, 383);
+      fft2_16(w, s0, s0 + 32, FO + 255);
+      fft2_16(w, s0 + 16, s0 + 48, FO + 255);
+      fft2_16(w, s0, s0 + 16, FO + 127);
+      fft2_16(w, s0 + 32, s0 + 48, FO + 383);
     }
 #pragma unroll
     for (int g2 = 0; g2 < 4; g2++)  // dist4 = 128 step, first sub-layer (bit 6)
 #pragma unroll
-      for (int b = 0; b < 8; b++) fft2_16(w, 16 * g2 + b, 16 * g2 + b + 8, 128 * g2 + 63);
+      for (int b = 0; b < 8; b++) fft2_16(w, 16 * g2 + b, 16 * g2 + b + 8, FO + 128 * g2 + 63);
     xpose16<P, S>(w, lds, q, lane);
 #pragma unroll
-    for (int j = 0; j < 32; j++) fft2_16(w, j, j + 32, 64 * q + 31);  // its second sub-layer (bit 5)
-    fft16_block<8>(w, 64 * q);                                         // bits 4 .. 0
+    for (int j = 0; j < 32; j++) fft2_16(w, j, j + 32, FO + 64 * q + 31);  // its second sub-layer (bit 5)
+    fft16_block<8>(w, FO + 64 * q);                                         // bits 4 .. 0
   } else {  // M == 256: slot 16a + b: a = bits 6-7, b = bits 0-3
-    constexpr int p01 = M - 1 + 64, p02 = p01 + 64, p23 = p01 + 128;
+    constexpr int p01 = IO - 1 + 64, p02 = p01 + 64, p23 = p01 + 128;
 #pragma unroll
     for (int b = 0; b < 16; b++) {  // radix-4 dist 64 (bits 6, 7)
       ifft2_16(w, b, 16 + b, p01);
@@ -641,13 +646,13 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(3, 8))) void 
     }
 #pragma unroll
     for (int b = 0; b < 16; b++) {  // FFT dist4 = 256, dist = 64 (bits 7, 6)
-      fft2_16(w, b, 32 + b, 127);
-      fft2_16(w, 16 + b, 48 + b, 127);
-      fft2_16(w, b, 16 + b, 63);
-      fft2_16(w, 32 + b, 48 + b, 191);
+      fft2_16(w, b, 32 + b, FO + 127);
+      fft2_16(w, 16 + b, 48 + b, FO + 127);
+      fft2_16(w, b, 16 + b, FO + 63);
+      fft2_16(w, 32 + b, 48 + b, FO + 191);
     }
     xpose16<P, S>(w, lds, q, lane);
-    fft16_block<16>(w, 64 * q);  // bits 5 .. 0
+    fft16_block<16>(w, FO + 64 * q);  // bits 5 .. 0
   }
   if (!active) return;
   const auto out_rsrc = make_rsrc(a.out + sq * a.out_sq_stride + vec * a.out_vec_stride);
@@ -666,7 +671,7 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(3, 8))) void 
     }
     return;
   }
-  if (a.out_present) {  // Repair fill: store missing parity shards, compare given ones
+  if (a.out_present) {  // Repair fill: store the missing shards of the out half, compare given ones
     uint32_t diff = 0;
 #pragma unroll
     for (int j = 0; j < 64; j++) {
@@ -1213,6 +1218,7 @@ bool gf16_k_ok(int k) { return k >= 256 && k <= kMaxK && (k & (k - 1)) == 0; }
 
 hipError_t launch_leo16_encode(int k, const EncodeArgs& a, hipStream_t s) {
   if (!gf16_k_ok(k) || a.shard_bytes % 64) return hipErrorInvalidValue;
+  if (a.reverse && !a.out_present) return hipErrorInvalidValue;  // reverse transform: Repair fill only
   hipError_t e = ensure_tables();
   if (e != hipSuccess) return e;
 #ifndef DAGPU_GF16_LDS_ENCODE
@@ -1221,8 +1227,13 @@ hipError_t launch_leo16_encode(int k, const EncodeArgs& a, hipStream_t s) {
     b.nchunk = (a.shard_bytes + 511) / 512;
     const long blocks = b.nsq * b.nvec * b.nchunk;
     if (blocks <= 0) return hipSuccess;
-    if (k == 256) hipLaunchKernelGGL(leo16_encode_reg_kernel<256>, dim3((unsigned)blocks), dim3(256), 0, s, b);
-    else hipLaunchKernelGGL(leo16_encode_reg_kernel<512>, dim3((unsigned)blocks), dim3(512), 0, s, b);
+    if (k == 256) {
+      if (a.reverse) hipLaunchKernelGGL((leo16_encode_reg_kernel<256, true>), dim3((unsigned)blocks), dim3(256), 0, s, b);
+      else hipLaunchKernelGGL((leo16_encode_reg_kernel<256, false>), dim3((unsigned)blocks), dim3(256), 0, s, b);
+    } else {
+      if (a.reverse) hipLaunchKernelGGL((leo16_encode_reg_kernel<512, true>), dim3((unsigned)blocks), dim3(512), 0, s, b);
+      else hipLaunchKernelGGL((leo16_encode_reg_kernel<512, false>), dim3((unsigned)blocks), dim3(512), 0, s, b);
+    }
     return hipGetLastError();
   }
 #endif

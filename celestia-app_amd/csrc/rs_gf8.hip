@@ -44,19 +44,19 @@
 
 namespace dagpu {
 
-// ifftDITEncoder8 (m = mtrunc = K, skewLUT = fftSkew8[m-1:]) restricted to the
-// E elements [BASE, BASE+E) one thread holds: every radix-4 group that fits
-// inside the slice; the trailing radix-2 layer only when the slice is the
-// whole vector.
-template <int K, int E, int BASE, int DIST>
+// ifftDITEncoder8 (m = mtrunc = K, skewLUT = fftSkew8[m-1:], i.e. skew offset
+// IO = K; the reverse fill's IFFT has IO = 0) restricted to the E elements
+// [BASE, BASE+E) one thread holds: every radix-4 group that fits inside the
+// slice; the trailing radix-2 layer only when the slice is the whole vector.
+template <int K, int IO, int E, int BASE, int DIST>
 __device__ __forceinline__ void ifft_enc_local(uint32_t (&w)[E]) {
   if constexpr (DIST * 4 <= E) {
 #pragma unroll
     for (int r = 0; r < E; r += DIST * 4) {
       const int iend = BASE + r + DIST;  // global index
-      const int l01 = kGf8.skew[K - 1 + iend];
-      const int l02 = kGf8.skew[K - 1 + iend + DIST];
-      const int l23 = kGf8.skew[K - 1 + iend + 2 * DIST];
+      const int l01 = kGf8.skew[IO - 1 + iend];
+      const int l02 = kGf8.skew[IO - 1 + iend + DIST];
+      const int l23 = kGf8.skew[IO - 1 + iend + 2 * DIST];
 #pragma unroll
       for (int i = r; i < r + DIST; i++) {
         ifft2(w[i], w[i + DIST], l01);
@@ -66,27 +66,28 @@ __device__ __forceinline__ void ifft_enc_local(uint32_t (&w)[E]) {
       }
       if constexpr (K >= 128) ENC_FENCE();
     }
-    ifft_enc_local<K, E, BASE, DIST * 4>(w);
+    ifft_enc_local<K, IO, E, BASE, DIST * 4>(w);
   } else if constexpr (E == K && DIST < K) {
-    const int lm = kGf8.skew[K - 1 + DIST];
+    const int lm = kGf8.skew[IO - 1 + DIST];
 #pragma unroll
     for (int i = 0; i < DIST; i++) ifft2(w[i], w[i + DIST], lm);
   }
 }
 
-// fftDIT8 (mtrunc = m, skewLUT = fftSkew8[:], index iend-1) restricted to the
-// slice [BASE, BASE+E): radix-4 steps with dist4 <= E, then the final radix-2
-// layer when the transform size is 2 * 4^j.
-template <int E, int BASE, int DIST4>
+// fftDIT8 (mtrunc = m, skewLUT = fftSkew8[:], index iend-1: skew offset FO = 0;
+// the reverse fill's FFT has FO = K) restricted to the slice [BASE, BASE+E):
+// radix-4 steps with dist4 <= E, then the final radix-2 layer when the
+// transform size is 2 * 4^j.
+template <int FO, int E, int BASE, int DIST4>
 __device__ __forceinline__ void fft_local(uint32_t (&w)[E]) {
   constexpr int DIST = DIST4 >> 2;
   if constexpr (DIST != 0) {
 #pragma unroll
     for (int r = 0; r < E; r += DIST4) {
       const int iend = BASE + r + DIST;
-      const int l01 = kGf8.skew[iend - 1];
-      const int l02 = kGf8.skew[iend + DIST - 1];
-      const int l23 = kGf8.skew[iend + 2 * DIST - 1];
+      const int l01 = kGf8.skew[FO + iend - 1];
+      const int l02 = kGf8.skew[FO + iend + DIST - 1];
+      const int l23 = kGf8.skew[FO + iend + 2 * DIST - 1];
 #pragma unroll
       for (int i = r; i < r + DIST; i++) {
         fft2(w[i], w[i + 2 * DIST], l02);
@@ -96,10 +97,10 @@ __device__ __forceinline__ void fft_local(uint32_t (&w)[E]) {
       }
       if constexpr (E >= 128) ENC_FENCE();
     }
-    fft_local<E, BASE, DIST>(w);
+    fft_local<FO, E, BASE, DIST>(w);
   } else if constexpr (DIST4 == 2) {
 #pragma unroll
-    for (int r = 0; r < E; r += 2) fft2(w[r], w[r + 1], kGf8.skew[BASE + r]);
+    for (int r = 0; r < E; r += 2) fft2(w[r], w[r + 1], kGf8.skew[FO + BASE + r]);
   }
 }
 
@@ -110,7 +111,7 @@ __device__ __forceinline__ void fft_local(uint32_t (&w)[E]) {
 // IFFT's last radix-2 layer (distance 64) and the FFT's first sub-layer
 // (distance 64); they are adjacent, so one chunked LDS exchange gives each half
 // both operands and each computes the pair result it keeps.
-template <int K, int H, int HH>
+template <int K, int H, int HH, bool REV>
 __device__ __forceinline__ void encode_half(const EncodeArgs& a, long sq, long vec, int t, bool active,
                                             uint32_t (*xch)[16][128]) {
   constexpr int E = K / H;
@@ -133,11 +134,11 @@ __device__ __forceinline__ void encode_half(const EncodeArgs& a, long sq, long v
   }
 
   if constexpr (H == 1) {
-    ifft_enc_local<K, K, 0, 1>(w);
-    fft_local<K, 0, K>(w);
+    ifft_enc_local<K, REV ? 0 : K, K, 0, 1>(w);
+    fft_local<REV ? K : 0, K, 0, K>(w);
   } else {
-    static_assert(K == 128 && H == 2, "split encode is specialised for k = 128");
-    ifft_enc_local<K, E, HH * E, 1>(w);  // distances 1..32 (radix-4 dist 1, 4, 16)
+    static_assert(K == 128 && H == 2 && !REV, "split encode is specialised for the k = 128 forward encode");
+    ifft_enc_local<K, K, E, HH * E, 1>(w);  // distances 1..32 (radix-4 dist 1, 4, 16)
     constexpr int L1 = kGf8.skew[K - 1 + 64];  // IFFT trailing layer, pairs (i, i+64)
     constexpr int L2 = kGf8.skew[63];          // FFT first radix-4 (dist 32), sub-layer (i, i+64)
 #pragma unroll
@@ -161,7 +162,7 @@ __device__ __forceinline__ void encode_half(const EncodeArgs& a, long sq, long v
     constexpr int LA = HH == 0 ? kGf8.skew[31] : kGf8.skew[95];
 #pragma unroll
     for (int i = 0; i < 32; i++) fft2(w[i], w[i + 32], LA);
-    fft_local<E, HH * E, 32>(w);  // radix-4 dist 8, 2 (dist4 32, 8) + final radix-2
+    fft_local<0, E, HH * E, 32>(w);  // radix-4 dist 8, 2 (dist4 32, 8) + final radix-2
   }
 
   if (!active) return;
@@ -178,7 +179,7 @@ __device__ __forceinline__ void encode_half(const EncodeArgs& a, long sq, long v
     }
     return;
   }
-  if (a.out_present) {  // Repair fill: store missing parity shards, compare given ones
+  if (a.out_present) {  // Repair fill: store the missing shards of the out half, compare given ones
     uint32_t diff = 0;
 #pragma unroll
     for (int j = 0; j < E; j++) {
@@ -202,16 +203,16 @@ struct EncOcc { static constexpr int waves = K >= 128 ? DAGPU_ENC_WAVES128 : (K 
 
 // One block = 128*H threads = 512 bytes (128 dword columns) of one vector.
 // Block index (flattened) = (square * nvec + vec) * nchunk + chunk.
-template <int K>
+template <int K, bool REV>
 __global__ __launch_bounds__(128 * EncSplit<K>::H)
 __attribute__((amdgpu_waves_per_eu(EncOcc<K>::waves, 8))) void leo8_encode_kernel(EncodeArgs a) {
-  constexpr int H = EncSplit<K>::H;
+  constexpr int H = REV ? 1 : EncSplit<K>::H;
   const long blk = blockIdx.x;
   const int chunk = (int)(blk % a.nchunk);
   const long sv = blk / a.nchunk;
   const long vec = sv % a.nvec;
   const long sq = sv / a.nvec;
-  if (a.vec_flags && a.vec_flags[sv] == 0) return;  // uniform
+  if (vec_skipped(a, sv)) return;  // uniform
   const int t = threadIdx.x & 127;
   // chunks of 512 B: shift the column window inside the shard
   EncodeArgs b = a;
@@ -222,13 +223,13 @@ __attribute__((amdgpu_waves_per_eu(EncOcc<K>::waves, 8))) void leo8_encode_kerne
   const bool active = coff + t * 4 < a.shard_bytes;
   if constexpr (H == 1) {
     if (!active) return;
-    encode_half<K, 1, 0>(b, sq, vec, t, true, nullptr);
+    encode_half<K, 1, 0, REV>(b, sq, vec, t, true, nullptr);
   } else {
     // every thread reaches the exchange barriers; inactive columns skip memory
     __shared__ uint32_t xch[2][16][128];
     const int h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 7);  // wave-uniform
-    if (h == 0) encode_half<K, H, 0>(b, sq, vec, t, active, xch);
-    else encode_half<K, H, 1>(b, sq, vec, t, active, xch);
+    if (h == 0) encode_half<K, H, 0, false>(b, sq, vec, t, active, xch);
+    else encode_half<K, H, 1, false>(b, sq, vec, t, active, xch);
   }
 }
 
@@ -236,7 +237,12 @@ template <int K>
 static hipError_t launch_k(const EncodeArgs& a, hipStream_t s) {
   const long blocks = a.nsq * a.nvec * a.nchunk;
   if (blocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(leo8_encode_kernel<K>, dim3((unsigned)blocks), dim3(128 * EncSplit<K>::H), 0, s, a);
+  if (a.reverse) {
+    if (!a.out_present) return hipErrorInvalidValue;  // reverse transform: Repair fill only
+    hipLaunchKernelGGL((leo8_encode_kernel<K, true>), dim3((unsigned)blocks), dim3(128), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((leo8_encode_kernel<K, false>), dim3((unsigned)blocks), dim3(128 * EncSplit<K>::H), 0, s, a);
+  }
   return hipGetLastError();
 }
 

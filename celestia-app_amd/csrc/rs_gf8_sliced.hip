@@ -209,11 +209,34 @@ __device__ __forceinline__ void transpose_wave2(uint32_t (&v)[16][8], u32x4* lds
   }
 }
 
+// The k = 128 two-vector transform: layer 0 in A (lane term), layers 1..2 in
+// A* (element bit 0 in the lane: no lane term), layers 3..6 in B (compile-time
+// skews), and back.  Skew offsets IO / FO: K / 0 for the encode, 0 / K for the
+// reverse fill (parity half -> data half, EncodeArgs.reverse).
+template <int IO, int FO>
+__device__ __forceinline__ void transform2(uint32_t (&v)[16][8], u32x4* lds, int w, int eb, int col, uint32_t ebmask) {
+  constexpr int K = 128;
+  ifft_A2<K, 1, IO>(v, w, ebmask);
+  transpose_wave2<true>(v, lds, w, eb, col);
+  ifft_As2<K, IO>(v, w);
+  __syncthreads();  // every wave's wave-local reads are done before the exchange writes
+  exchange2s<true>(v, lds, w, eb, col);
+  ifft_fft_B<K, IO, FO>(v);
+  __syncthreads();
+  exchange2s<false>(v, lds, w, eb, col);
+  fft_As2<K, FO>(v, w);
+  __syncthreads();  // other waves' last exchange reads of this wave's quarter are done
+  transpose_wave2<false>(v, lds, w, eb, col);
+  fft_A2<K, 1, FO>(v, w, ebmask);
+}
+
 // FILL (Repair fill mode, EncodeArgs): block = (pair of same-square vectors
 // from pair_list, chunk); each half of the lanes takes its own vector (a -1
-// entry: the lanes load the partner's data and store nothing); a parity shard
-// is stored where it is missing, a given one is compared (redo on a difference).
-template <bool FILL>
+// entry: the lanes load the partner's data and store nothing); a shard of the
+// half being rebuilt is stored where it is missing, a given one is compared
+// (redo on a difference).  REV: the reverse fill (EncodeArgs.reverse: `in` is
+// the parity half, `out` the data half).
+template <bool FILL, bool REV = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void leo8_encode_sliced2_kernel(EncodeArgs a) {
   constexpr int K = 128;
@@ -278,21 +301,8 @@ void leo8_encode_sliced2_kernel(EncodeArgs a) {
 #pragma unroll
   for (int j = 0; j < 16; j++) transpose8(v[j]);
 
-  // layer 0 in A (lane term), layers 1..2 in A* (element bit 0 in the lane:
-  // no lane term), layers 3..6 in B (compile-time skews), and back
   const int col = vv * 16 + t;
-  ifft_A2<K, 1>(v, w, ebmask);
-  transpose_wave2<true>(v, lds, w, eb, col);
-  ifft_As2<K>(v, w);
-  __syncthreads();  // every wave's wave-local reads are done before the exchange writes
-  exchange2s<true>(v, lds, w, eb, col);
-  ifft_fft_B<K>(v);
-  __syncthreads();
-  exchange2s<false>(v, lds, w, eb, col);
-  fft_As2<K>(v, w);
-  __syncthreads();  // other waves' last exchange reads of this wave's quarter are done
-  transpose_wave2<false>(v, lds, w, eb, col);
-  fft_A2<K, 1>(v, w, ebmask);
+  transform2<REV ? 0 : K, REV ? K : 0>(v, lds, w, eb, col, ebmask);
 #if defined(DAGPU_RS_PAD) && DAGPU_RS_PAD > 0
   {  // A/B instrument only: DAGPU_RS_PAD x 128 extra fast-class VALU ops per lane, results unchanged
     const uint32_t z = __builtin_amdgcn_readfirstlane((uint32_t)(a.nchunk - 1));  // 0 at run time
@@ -358,7 +368,8 @@ bool leo8_sliced_applicable(int k, const EncodeArgs& a) {
     return !(e && e[0] == '0');
   }();
   if (!enabled || k < 16 || k > 128) return false;
-  if (a.shard_bytes <= 0 || a.shard_bytes % 512 || a.nvec % 4 || a.vec_flags || a.mismatch || a.out_present)
+  if (a.shard_bytes <= 0 || a.shard_bytes % 512 || a.nvec % 4 || a.vec_flags || a.mismatch || a.out_present ||
+      a.reverse)
     return false;
   if (a.nchunk * 512 != a.shard_bytes) return false;
   const long strides[] = {a.in_sq_stride, a.in_vec_stride, a.in_shard_stride, a.out_sq_stride,
@@ -420,7 +431,8 @@ bool leo8_fill_sliced_applicable(const EncodeArgs& a) {
 hipError_t launch_leo8_fill_sliced(const EncodeArgs& a, long max_pairs, hipStream_t s) {
   const long blocks = max_pairs * a.nchunk;
   if (blocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(leo8_encode_sliced2_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s, a);
+  if (a.reverse) hipLaunchKernelGGL((leo8_encode_sliced2_kernel<true, true>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((leo8_encode_sliced2_kernel<true, false>), dim3((unsigned)blocks), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -59,7 +59,8 @@ void encode_chunk_lane(const uint8_t* data, uint8_t* parity, long shard, long co
 // Two-vector layout of leo8_encode_sliced2_kernel (k = 128): one vector's
 // column block t, the 8 (wave w, lane element bit eb) "lanes" of layout A
 // (e = j + 16 eb + 32 w, layer 0), A* (e = eb + 2 r + 32 w, layers 1..2) and
-// B (e = eb + 2 w + 8 i).
+// B (e = eb + 2 w + 8 i).  IO / FO: skew offsets (K / 0 encode, 0 / K reverse fill).
+template <int IO, int FO>
 void encode2_chunk_lane(const uint8_t* data, uint8_t* parity, long shard, long col0) {
   constexpr int K = 128;
   static uint32_t st[4][2][16][8], tmp[4][2][16][8];
@@ -75,7 +76,7 @@ void encode2_chunk_lane(const uint8_t* data, uint8_t* parity, long shard, long c
       }
   static uint32_t as[4][2][16][8];  // layout A*: e = eb + 2 r + 32 w
   for (int w = 0; w < 4; w++)
-    for (int eb = 0; eb < 2; eb++) ifft_A2<K, 1>(st[w][eb], w, eb ? 0xFFFFFFFFu : 0u);
+    for (int eb = 0; eb < 2; eb++) ifft_A2<K, 1, IO>(st[w][eb], w, eb ? 0xFFFFFFFFu : 0u);
   for (int w = 0; w < 4; w++)  // A -> A* (wave-local)
     for (int eb = 0; eb < 2; eb++)
       for (int r = 0; r < 16; r++) {
@@ -83,7 +84,7 @@ void encode2_chunk_lane(const uint8_t* data, uint8_t* parity, long shard, long c
         memcpy(as[w][eb][r], st[w][e >> 4][e & 15], 32);
       }
   for (int w = 0; w < 4; w++)
-    for (int eb = 0; eb < 2; eb++) ifft_As2<K>(as[w][eb], w);
+    for (int eb = 0; eb < 2; eb++) ifft_As2<K, IO>(as[w][eb], w);
   for (int w = 0; w < 4; w++)  // A* -> B
     for (int eb = 0; eb < 2; eb++)
       for (int i = 0; i < 16; i++) {
@@ -92,7 +93,7 @@ void encode2_chunk_lane(const uint8_t* data, uint8_t* parity, long shard, long c
       }
   for (int w = 0; w < 4; w++)
     for (int eb = 0; eb < 2; eb++) {
-      ifft_fft_B<K>(tmp[w][eb]);
+      ifft_fft_B<K, IO, FO>(tmp[w][eb]);
     }
   for (int w = 0; w < 4; w++)  // B -> A*
     for (int eb = 0; eb < 2; eb++)
@@ -101,7 +102,7 @@ void encode2_chunk_lane(const uint8_t* data, uint8_t* parity, long shard, long c
         memcpy(as[e >> 5][e & 1][(e >> 1) & 15], tmp[w][eb][i], 32);
       }
   for (int w = 0; w < 4; w++)
-    for (int eb = 0; eb < 2; eb++) fft_As2<K>(as[w][eb], w);
+    for (int eb = 0; eb < 2; eb++) fft_As2<K, FO>(as[w][eb], w);
   for (int w = 0; w < 4; w++)  // A* -> A (wave-local)
     for (int eb = 0; eb < 2; eb++)
       for (int r = 0; r < 16; r++) {
@@ -109,7 +110,7 @@ void encode2_chunk_lane(const uint8_t* data, uint8_t* parity, long shard, long c
         memcpy(st[w][e >> 4][e & 15], as[w][eb][r], 32);
       }
   for (int w = 0; w < 4; w++)
-    for (int eb = 0; eb < 2; eb++) fft_A2<K, 1>(st[w][eb], w, eb ? 0xFFFFFFFFu : 0u);
+    for (int eb = 0; eb < 2; eb++) fft_A2<K, 1, FO>(st[w][eb], w, eb ? 0xFFFFFFFFu : 0u);
   for (int w = 0; w < 4; w++)
     for (int eb = 0; eb < 2; eb++)
       for (int j = 0; j < 16; j++) {
@@ -134,7 +135,15 @@ int encode(long shard, const uint8_t* data, uint8_t* parity) {
 extern "C" int sliced2_emu_encode(long shard, const uint8_t* data, uint8_t* parity) {
   if (shard <= 0 || shard % 512) return -1;
   for (long c = 0; c < shard; c += 512)
-    for (int t = 0; t < 16; t++) encode2_chunk_lane(data, parity, shard, c + 16 * t);
+    for (int t = 0; t < 16; t++) encode2_chunk_lane<128, 0>(data, parity, shard, c + 16 * t);
+  return 0;
+}
+
+// reverse fill transform of the k = 128 Repair kernel: 128 parity shards -> data
+extern "C" int sliced2_emu_reverse(long shard, const uint8_t* parity, uint8_t* data) {
+  if (shard <= 0 || shard % 512) return -1;
+  for (long c = 0; c < shard; c += 512)
+    for (int t = 0; t < 16; t++) encode2_chunk_lane<0, 128>(parity, data, shard, c + 16 * t);
   return 0;
 }
 

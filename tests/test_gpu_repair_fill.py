@@ -1,10 +1,12 @@
 """Repair fill route and deferral (dagpu.cpp repair_device, repair.hip
 repair_plan_kernel): with DAGPU_REPAIR_FILL on (the default) a decodable axis
-whose data half is complete is re-encoded instead of decoded, and decodes of
-axes i >= k wait when every axis i < k is being rebuilt.  Both must leave
+whose data half is complete is re-encoded instead of decoded, one whose parity
+half is complete is rebuilt by the reverse transform (EncodeArgs.reverse), and
+decodes of axes i >= k wait when every axis i < k is being rebuilt.  All must leave
 exactly what the plain decoder schedule leaves -- status, every EDS byte and
 the presence map -- for consistent squares, corrupted given shares (also in
-the parity half of a filled axis, which sends it back to the decoder),
+the parity half of a filled axis or the data half of a reverse-filled one,
+which sends it back to the decoder),
 unrepairable patterns and a committed square that is not a codeword square
 (the deferred-axis check and the re-run without deferral).  Statuses are also
 checked against the oracle's rsmt2d restatement."""
@@ -35,6 +37,13 @@ def _pattern(kind, k, rng):
         p[np.ix_(np.arange(k), rng.choice(w, k, replace=False))] = True
     elif kind == "q0":  # the original data only: every axis is filled
         p[:k, :k] = True
+    elif kind == "q3":  # parity of parity only (bench --mode repair): reverse row and column fills
+        p[k:, k:] = True
+    elif kind == "subgrid_right":  # kept columns are the parity columns
+        p[np.ix_(rng.choice(w, k, replace=False), np.arange(k, w))] = True
+    elif kind == "right_half":  # every row reverse-fillable, some data shards given (compared)
+        p[:, k:] = True
+        p[:, :k] = rng.random((w, k)) < 0.3
     elif kind == "left_half":  # every row decodable by its data half, some parity given
         p[:, :k] = True
         p[:, k:] = rng.random((w, k)) < 0.3
@@ -59,6 +68,8 @@ def _corrupt(eds, p, how, rng, k):
     cells = np.argwhere(p)
     if how == "parity_half":
         cells = [(r, c) for r, c in cells if c >= k and p[r, :k].all()] or list(cells)
+    elif how == "data_half":  # a given data share of a row whose parity half is complete
+        cells = [(r, c) for r, c in cells if c < k and p[r, k:].all()] or list(cells)
     r, c = cells[rng.integers(len(cells))]
     eds[r, c, rng.integers(512)] ^= 1 << int(rng.integers(8))
 
@@ -123,18 +134,24 @@ def test_fill_equals_decoder_small(ctx, monkeypatch, k):
     specs = [("subgrid", None), ("subgrid_top", None), ("q0", None), ("left_half", None),
              ("rows_plus", None), ("0.5", None), ("0.65", None), ("0.8", None),
              ("subgrid", "any"), ("left_half", "parity_half"), ("rows_plus", "any"),
-             ("unrepairable", None), ("unrepairable", "any"), ("q0", "any")]
+             ("unrepairable", None), ("unrepairable", "any"), ("q0", "any"),
+             ("q3", None), ("subgrid_right", None), ("right_half", None), ("q3", "any"),
+             ("right_half", "data_half")]
     st = _case(ctx, monkeypatch, k, specs, 300 + k)
     assert st[0] == 0 and st[2] == 0 and st[9] == _abi.ERR_BYZANTINE
+    assert (st[14:17] == 0).all() and st[18] == _abi.ERR_BYZANTINE
 
 
 def test_fill_equals_decoder_k128(ctx, monkeypatch):
-    """The bit-sliced k = 128 fill (pair list) and decoder."""
+    """The bit-sliced k = 128 fill (forward and reverse pair lists) and decoder."""
     specs = [("subgrid", None), ("subgrid", None), ("subgrid_top", None), ("q0", None),
              ("left_half", None), ("rows_plus", None), ("0.6", None), ("subgrid", "any"),
-             ("left_half", "parity_half"), ("rows_plus", "any"), ("unrepairable", None)]
+             ("left_half", "parity_half"), ("rows_plus", "any"), ("unrepairable", None),
+             ("q3", None), ("subgrid_right", None), ("right_half", None), ("right_half", "data_half"),
+             ("q3", "any")]
     st = _case(ctx, monkeypatch, 128, specs, 1280, oracle_check=False)
     assert (st[:7] == 0).all() and st[8] == _abi.ERR_BYZANTINE
+    assert (st[11:14] == 0).all() and st[14] == _abi.ERR_BYZANTINE
 
 
 @pytest.mark.parametrize("k", [16, 128])
@@ -143,28 +160,58 @@ def test_fill_bad_encoding(ctx, monkeypatch, k):
     Q3 cells, roots over it): the same outcome with and without the shortcut,
     including the deferred-axis check and the re-run without deferral."""
     specs = [("subgrid", None), ("rows_plus", None), ("rows_plus", "any"), ("left_half", None),
-             ("subgrid_top", None), ("0.6", None)]
+             ("subgrid_top", None), ("0.6", None), ("right_half", None), ("subgrid_right", None)]
     _case(ctx, monkeypatch, k, specs, 4400 + k, oracle_check=(k <= 16), bad_encoding=range(len(specs)))
 
 
 def test_fill_equals_decoder_gf16(ctx, monkeypatch):
-    """GF(2^16) (k = 256): the register-resident fill encoder and decoder."""
-    specs = [("subgrid", None), ("left_half", "parity_half"), ("rows_plus", None)]
+    """GF(2^16) (k = 256): the register-resident fill encoder (both directions) and decoder."""
+    specs = [("subgrid", None), ("left_half", "parity_half"), ("rows_plus", None), ("q3", None),
+             ("right_half", "data_half")]
     st = _case(ctx, monkeypatch, 256, specs, 2560, oracle_check=False)
     assert st[0] == 0 and st[1] == _abi.ERR_BYZANTINE and st[2] == 0
+    assert st[3] == 0 and st[4] == _abi.ERR_BYZANTINE
+
+
+def test_fill_equals_decoder_gf16_k512(ctx, monkeypatch):
+    """k = 512 (the M = 512 register-resident encoder, reverse direction): the
+    EDS comes from the library's own extend (the oracle is too slow at this
+    size; the GF(2^16) encode is checked against it in tests/test_gpu_gf16.py),
+    then the maximal Q3-only pattern and a right half with a corrupted given
+    data share are repaired with and without the shortcut."""
+    k, n = 512, 2
+    w = 2 * k
+    rng = np.random.default_rng(5120)
+    ds = DeviceSquares(k, n, ctx=ctx, in_place=True)
+    ds.load_ods(synth.blob_squares(k, 5120, 0, n, threads=16))
+    ds.extend()
+    torch.cuda.synchronize()
+    eds = ds.eds.cpu().numpy().reshape(n, w, w, 512)
+    rr, cr = ds.row_roots.cpu().numpy(), ds.col_roots.cpu().numpy()
+    del ds
+    torch.cuda.empty_cache()
+    pres = np.stack([_pattern("q3", k, rng), _pattern("right_half", k, rng)])
+    dmg = eds * pres[..., None]
+    _corrupt(dmg[1], pres[1], "data_half", rng, k)
+    st1, e1, p1 = _run(ctx, k, dmg, pres, rr, cr, monkeypatch, True)
+    st0, e0, p0 = _run(ctx, k, dmg, pres, rr, cr, monkeypatch, False)
+    assert list(st1) == list(st0) == [0, _abi.ERR_BYZANTINE]
+    assert (e1 == e0).all() and (p1 == p0).all()
+    assert (e1[0] == eds[0]).all() and p1[0].all()
 
 
 @pytest.mark.parametrize("k", [8, 32])
 def test_fill_random_sweep(ctx, monkeypatch, k):
-    """48 squares, each a random pattern kind and density, a third of them with
+    """54 squares, each a random pattern kind and density, half of them with
     one corrupted given share: the shortcut equals the plain schedule byte for
     byte, and every status equals the oracle's."""
     rng = np.random.default_rng(9000 + k)
-    kinds = ["subgrid", "subgrid_top", "q0", "left_half", "rows_plus", "unrepairable"]
+    kinds = ["subgrid", "subgrid_top", "q0", "left_half", "rows_plus", "unrepairable",
+             "q3", "subgrid_right", "right_half"]
     specs = []
-    for i in range(48):
-        kind = kinds[i % len(kinds)] if i < 24 else f"{rng.uniform(0.35, 0.9):.2f}"
-        corrupt = ("any", "parity_half", None)[i % 3]
+    for i in range(54):
+        kind = kinds[i % len(kinds)] if i < 27 else f"{rng.uniform(0.35, 0.9):.2f}"
+        corrupt = ("any", "parity_half", None, "data_half")[i % 4]
         specs.append((kind, corrupt))
     _case(ctx, monkeypatch, k, specs, 9100 + k)
 

@@ -125,3 +125,25 @@ def test_sliced_decode_structured_patterns(emu):
         got = full * present[:, None]
         assert emu.sliced_dec_emu(shard, got.ctypes.data, present.ctypes.data) == 0
         assert np.array_equal(got, full)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_sliced2_reverse_fill_matches_oracle_decode(emu, seed):
+    """The Repair reverse fill (leo8_encode_sliced2_kernel<true, true>: IFFT
+    at skew offset 0, FFT at offset k) rebuilds the data
+    half from a complete parity half exactly as the oracle's Leopard
+    reconstruct does with the whole data half erased."""
+    emu.sliced2_emu_reverse.argtypes = [ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p]
+    k, shard = 128, 512 * (1 + seed)
+    rng = np.random.default_rng(5100 + seed)
+    cases = [rng.integers(0, 256, (k, shard), dtype=np.uint8)]
+    if seed == 0:
+        cases += [np.full((k, shard), 0xFF, np.uint8), np.zeros((k, shard), np.uint8)]
+    for data in cases:
+        parity = oracle.encode(data)
+        full = np.concatenate([data, parity])
+        present = np.r_[np.zeros(k), np.ones(k)].astype(bool)
+        assert np.array_equal(oracle.decode(full * present[:, None], present)[:k], data)
+        got = np.zeros_like(data)
+        assert emu.sliced2_emu_reverse(shard, parity.ctypes.data, got.ctypes.data) == 0
+        assert np.array_equal(got, data)
