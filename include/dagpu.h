@@ -166,7 +166,8 @@ int dagpu_repair_ex(dagpu_ctx* ctx, uint32_t k, uint8_t* eds, uint8_t* present,
  * d_workspace: dagpu_repair_workspace_size(k, n) bytes.  Enqueued on `stream`;
  * the call synchronises once per crossword round to read its counters (and
  * once more when deferred axes need their codeword check).  Axes whose data
- * half is complete are re-encoded instead of decoded (same bytes);
+ * half is complete are re-encoded instead of decoded, and axes whose parity
+ * half is complete are rebuilt by the inverse transform (same bytes);
  * DAGPU_REPAIR_FILL=0 in the environment selects the plain decoder schedule.
  * The _ex form also writes d_byz (n * 4 int32, device memory, as byz of
  * dagpu_repair_ex); a square whose crossword fails is then re-run in rsmt2d's
