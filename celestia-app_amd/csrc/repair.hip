@@ -42,10 +42,72 @@ __global__ __launch_bounds__(64) void axis_complete_kernel(const uint8_t* presen
   if (threadIdx.x == 0) complete[a] = missing ? 0 : 1;
 }
 
+// 0x80 in every byte of x that is nonzero (no carries between bytes)
+__device__ __forceinline__ uint32_t nonzero_bytes_hi(uint32_t x) {
+  return (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+}
+
+// Rows, w % 16 == 0 and 16-B aligned presence: L = w / 16 lanes per row, each
+// one 16-B load; a row is complete when no lane of its group saw a zero byte.
+__global__ __launch_bounds__(256) void axis_complete_rows_kernel(const uint8_t* present, int k, long nsq,
+                                                                 int32_t* complete) {
+  const int w = 2 * k, L = w / 16;
+  const long t = (long)blockIdx.x * 256 + threadIdx.x;
+  const long nrow = nsq * w;
+  const long row = t / L;  // square-major: sq * w + r
+  bool zero = false;
+  if (row < nrow) {
+    const uint4 v = ((const uint4*)(present + row * w))[t - row * L];
+    zero = (nonzero_bytes_hi(v.x) & nonzero_bytes_hi(v.y) & nonzero_bytes_hi(v.z) & nonzero_bytes_hi(v.w)) !=
+           0x80808080u;
+  }
+  const uint64_t b = __ballot(zero);
+  const int lane = threadIdx.x & 63;
+  const int g = lane / L;  // L <= 64 and divides 64 (w = 16 .. 1024)
+  const uint64_t m = (L == 64 ? ~0ull : ((1ull << L) - 1)) << (g * L);
+  if (row < nrow && lane == g * L) complete[row] = (b & m) ? 0 : 1;
+}
+
+// Columns, w % 4 == 0 and 4-B aligned presence: block = (square, 256 columns);
+// lane j holds columns 4j..4j+3 (dword loads, coalesced along the row), the
+// four waves take every fourth row, AND-combined in LDS.
+__global__ __launch_bounds__(256) void axis_complete_cols_kernel(const uint8_t* present, int k, long nsq,
+                                                                 int32_t* complete) {
+  __shared__ uint32_t acc_s[4][64];
+  const int w = 2 * k;
+  const int ngrp = (w + 255) / 256;
+  const long sq = blockIdx.x / ngrp;
+  const int grp = (int)(blockIdx.x - sq * ngrp);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = grp * 256 + 4 * lane;  // first of this lane's 4 columns
+  uint32_t acc = 0x80808080u;
+  if (c < w) {
+    const uint8_t* p = present + sq * (long)w * w + c;
+    for (int r = wave; r < w; r += 4) acc &= nonzero_bytes_hi(*(const uint32_t*)(p + (long)r * w));
+  }
+  acc_s[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0 && c < w) {
+    const uint32_t all = acc_s[0][lane] & acc_s[1][lane] & acc_s[2][lane] & acc_s[3][lane];
+    int32_t* out = complete + nsq * w + sq * w + c;
+#pragma unroll
+    for (int j = 0; j < 4; j++) out[j] = ((all >> (8 * j + 7)) & 1) ? 1 : 0;
+  }
+}
+
 hipError_t launch_axis_complete(const uint8_t* present, int k, long nsq, int32_t* complete,
                                 hipStream_t s) {
   const long n = nsq * 4L * k;
   if (n <= 0) return hipSuccess;
+  const int w = 2 * k;
+  if (w >= 16 && ((uintptr_t)present & 15) == 0) {
+    const long threads = nsq * w * (w / 16);
+    hipLaunchKernelGGL(axis_complete_rows_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, present,
+                       k, nsq, complete);
+    hipLaunchKernelGGL(axis_complete_cols_kernel, dim3((unsigned)(nsq * ((w + 255) / 256))), dim3(256), 0, s,
+                       present, k, nsq, complete);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(axis_complete_kernel, dim3((unsigned)n), dim3(64), 0, s, present, k, nsq, complete);
   return hipGetLastError();
 }
@@ -398,9 +460,51 @@ __global__ __launch_bounds__(256) void mark_flagged_kernel(DecodeArgs a, const i
   for (int i = threadIdx.x; i < 2 * a.k; i += 256) pres[(long)i * a.p_shard_stride] = 1;
 }
 
+// The same over the whole presence map of square-major [sq][r][c] bytes, one
+// dword (4 columns) per thread: a row axis marks whole dwords of flagged rows,
+// a column axis ORs in the bytes of flagged columns; threads gid < nsq * w
+// also do the known[] update of vector gid.
+__global__ __launch_bounds__(256) void mark_flagged_map_kernel(DecodeArgs a, const int32_t* flags, int32_t* known,
+                                                               int rows) {
+  const int w = 2 * a.k, w4 = w / 4;
+  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+  const long nv = a.nsq * w;
+  if (known && gid < nv && flags[gid] && a.flags[gid]) known[gid] = 0;
+  if (gid >= nv * w4) return;
+  const long sq = gid / ((long)w * w4);
+  const long rem = gid - sq * (long)w * w4;
+  const int r = (int)(rem / w4), c = 4 * (int)(rem - (long)r * w4);
+  uint32_t* p = (uint32_t*)(a.present + sq * a.p_sq_stride + (long)r * w + c);
+  const int32_t* f = flags + sq * w;
+  if (rows) {
+    if (f[r]) *p = 0x01010101u;
+  } else {
+    const uint32_t set = (f[c] ? 0x1u : 0u) | (f[c + 1] ? 0x100u : 0u) | (f[c + 2] ? 0x10000u : 0u) |
+                         (f[c + 3] ? 0x1000000u : 0u);
+    if (set) {
+      const uint32_t x = *p;
+      // a flagged byte becomes exactly 1 (the decoders test presence != 0)
+      uint32_t y = x;
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if ((set >> (8 * j)) & 1) y = (y & ~(0xFFu << (8 * j))) | (1u << (8 * j));
+      *p = y;
+    }
+  }
+}
+
 hipError_t launch_rs_mark_present(const DecodeArgs& a, const int32_t* flags, hipStream_t s, int32_t* known) {
   const long nv = a.nsq * a.nvec;
   if (nv <= 0) return hipSuccess;
+  const long w = 2L * a.k;
+  const bool rows = a.p_vec_stride == w && a.p_shard_stride == 1;
+  const bool cols = a.p_vec_stride == 1 && a.p_shard_stride == w;
+  if (a.nvec == w && w % 4 == 0 && a.p_sq_stride == w * w && (rows || cols) && ((uintptr_t)a.present & 3) == 0) {
+    const long threads = a.nsq * w * (w / 4);
+    hipLaunchKernelGGL(mark_flagged_map_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, a, flags,
+                       known, rows ? 1 : 0);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(mark_flagged_kernel, dim3((unsigned)nv), dim3(256), 0, s, a, flags, known);
   return hipGetLastError();
 }
