@@ -353,6 +353,24 @@ def test_repair_max_erasure(ctx, k):
     assert (fixed == eds).all()
 
 
+@pytest.mark.parametrize("k", [1, 2, 8, 32, 128])
+def test_repair_q3_only_host_api(ctx, k):
+    """C4 with the other maximal pattern, Q3 only kept (the reverse fill's
+    case: every kept row and column has a complete parity half), through the
+    single-square host entry point (dagpu_repair), against the oracle's repair."""
+    ods = synth.random_blob_square(k, 70 + k)
+    eds, rr, cr, _ = oracle.extend_and_dah(ods, k, nthreads=8)
+    w = 2 * k
+    present = np.zeros((w, w), bool)
+    present[k:, k:] = True
+    damaged = eds * present[:, :, None]
+    fixed, pres = da.repair(damaged, present, rr, cr, ctx)
+    assert pres.all() and (fixed == eds).all()
+    if k <= 32:
+        orc, ofixed = oracle.repair(damaged, present, k, rr, cr)
+        assert orc == 0 and (ofixed == fixed).all()
+
+
 @pytest.mark.parametrize("k", [4, 16])
 def test_repair_random_patterns_match_oracle(ctx, k):
     rng = np.random.default_rng(k)
