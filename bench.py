@@ -422,6 +422,9 @@ def main():
             "configs[2]_mixed_4096": run_mixed(ctx, 3, 1),
             "configs[3]_repair_k128": run_repair(ctx, 128, 256, 3, 1),
             "repair_k512_gf16": run_repair(ctx, 512, 2, 2, 1),
+            # the other maximal erasure pattern (Q3 only kept): the reverse fill's case
+            "repair_k128_q3": run_repair(ctx, 128, 256, 3, 1, pattern="q3"),
+            "repair_k512_gf16_q3": run_repair(ctx, 512, 2, 2, 1, pattern="q3"),
         }
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.cpu_threads or host_threads())
@@ -973,8 +976,8 @@ def run_repair(ctx, k, B, steps, warmup, distinct=None, pattern="subgrid"):
     ms = sum(a.elapsed_time(b) for a, b in ev) / steps
     del ds, ref, damaged, ws
     torch.cuda.empty_cache()
-    return {"k": k, "squares": B, "squares_per_s": B / (ms * 1e-3), "ms_per_step": ms, "steps": steps,
-            "bit_exact": ok, "decode_gbs": rs_bytes(k) * B / (ms * 1e-3) / 1e9}
+    return {"k": k, "squares": B, "pattern": pattern, "squares_per_s": B / (ms * 1e-3), "ms_per_step": ms,
+            "steps": steps, "bit_exact": ok, "decode_gbs": rs_bytes(k) * B / (ms * 1e-3) / 1e9}
 
 
 def bench_repair(args):
