@@ -565,8 +565,14 @@ __device__ __forceinline__ void xpose16(W16& w, uint32_t* lds, int q, int lane) 
 
 // REV: the reverse fill (EncodeArgs.reverse): skew offsets IO = 0 for the IFFT
 // and FO = M for the FFT instead of M and 0 (positions stay below kTabPos).
+// Occupancy: an M = 512 workgroup is 2 waves per SIMD, and a second one does
+// not fit below 128 VGPRs either way, so it takes the whole 256-VGPR budget
+// (at the 168 of 3 waves per SIMD it kept 948 B per lane in scratch, at 256 544 B).
+template <int M>
+struct Enc16Occ { static constexpr int waves = M == 512 ? 2 : 3; };
 template <int M, bool REV>
-__global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(3, 8))) void leo16_encode_reg_kernel(EncodeArgs a) {
+__global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(Enc16Occ<M>::waves, 8))) void
+leo16_encode_reg_kernel(EncodeArgs a) {
   constexpr int IO = REV ? 0 : M, FO = REV ? M : 0;
   constexpr int P = M / 64;
   constexpr int S = P == 8 ? 1 : 2;
