@@ -565,13 +565,13 @@ __device__ __forceinline__ void xpose16(W16& w, uint32_t* lds, int q, int lane) 
 
 // REV: the reverse fill (EncodeArgs.reverse): skew offsets IO = 0 for the IFFT
 // and FO = M for the FFT instead of M and 0 (positions stay below kTabPos).
-// Occupancy: an M = 512 workgroup is 2 waves per SIMD, and a second one does
-// not fit below 128 VGPRs either way, so it takes the whole 256-VGPR budget
-// (at the 168 of 3 waves per SIMD it kept 948 B per lane in scratch, at 256 544 B).
-template <int M>
-struct Enc16Occ { static constexpr int waves = M == 512 ? 2 : 3; };
+// Occupancy: 2 waves per SIMD, the whole 256-VGPR budget.  At the 168 VGPRs of
+// 3 waves per SIMD the kernel kept 948 (M = 512) / 1032 (M = 256) B per lane in
+// scratch, at 256 544 / 576 B; an M = 512 workgroup fits once per CU either way,
+// and for M = 256 two spilling less beat three (profiles/gf16_encoder_occupancy_r03.log:
+// Q3 repair k = 512 +6 %, k = 256 +8.5 %; split square k = 512 +4.5 %, k = 256 +6 %).
 template <int M, bool REV>
-__global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(Enc16Occ<M>::waves, 8))) void
+__global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(2, 8))) void
 leo16_encode_reg_kernel(EncodeArgs a) {
   constexpr int IO = REV ? 0 : M, FO = REV ? M : 0;
   constexpr int P = M / 64;
