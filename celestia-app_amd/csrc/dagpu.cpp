@@ -1135,27 +1135,34 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
   HIP_TRY(ctx, hipMemcpyAsync(r.p0, d_present, n * w * w, hipMemcpyDeviceToDevice, s));
   HIP_TRY(ctx, hipMemsetAsync(r.bits, 0, n * sizeof(int32_t), s));
   HIP_TRY(ctx, hipMemsetAsync(r.parity_bad, 0, n * 2 * w * sizeof(int32_t), s));
-  HIP_TRY(ctx, launch_axis_complete(d_present, (int)k, (long)n, r.complete_before, s));
-  // prerepairSanityCheck: complete axes must satisfy parity == Encode(data)
-  for (int axis = 0; axis < 2; axis++) {
-    EncodeArgs e{};
-    e.in = d_eds;
-    e.in_sq_stride = (long)eds_bytes(k);
-    e.out_sq_stride = (long)eds_bytes(k);
-    if (axis == 0) {
-      e.in_vec_stride = w * kSS; e.in_shard_stride = kSS;
-      e.out = d_eds + (long)k * kSS; e.out_vec_stride = w * kSS; e.out_shard_stride = kSS;
-    } else {
-      e.in_vec_stride = kSS; e.in_shard_stride = w * kSS;
-      e.out = d_eds + (long)k * w * kSS; e.out_vec_stride = kSS; e.out_shard_stride = w * kSS;
+  HIP_TRY(ctx, hipMemsetAsync(r.counters + 5, 0, 2 * sizeof(int32_t), s));  // [5] complete axes, [6] deferred squares
+  HIP_TRY(ctx, launch_axis_complete(d_present, (int)k, (long)n, r.complete_before, s, r.counters + 5));
+  // prerepairSanityCheck: complete axes must satisfy parity == Encode(data).
+  // Queued after the first round's counter read, and only when some axis is
+  // complete (a complete axis is never written by the crossword, so the order
+  // does not matter; the maximal erasure patterns have none).
+  auto prerepair = [&]() -> int {
+    for (int axis = 0; axis < 2; axis++) {
+      EncodeArgs e{};
+      e.in = d_eds;
+      e.in_sq_stride = (long)eds_bytes(k);
+      e.out_sq_stride = (long)eds_bytes(k);
+      if (axis == 0) {
+        e.in_vec_stride = w * kSS; e.in_shard_stride = kSS;
+        e.out = d_eds + (long)k * kSS; e.out_vec_stride = w * kSS; e.out_shard_stride = kSS;
+      } else {
+        e.in_vec_stride = kSS; e.in_shard_stride = w * kSS;
+        e.out = d_eds + (long)k * w * kSS; e.out_vec_stride = kSS; e.out_shard_stride = w * kSS;
+      }
+      e.nsq = (long)n; e.nvec = w; e.nchunk = 1; e.shard_bytes = kSS;
+      e.vec_flags = r.complete_before + (long)axis * n * w;
+      e.mismatch = r.bits;
+      e.mismatch_bit = 0;
+      e.mismatch_vec = r.parity_bad + (long)axis * n * w;
+      HIP_TRY(ctx, launch_rs_encode((int)k, e, s));
     }
-    e.nsq = (long)n; e.nvec = w; e.nchunk = 1; e.shard_bytes = kSS;
-    e.vec_flags = r.complete_before + (long)axis * n * w;
-    e.mismatch = r.bits;
-    e.mismatch_bit = 0;
-    e.mismatch_vec = r.parity_bad + (long)axis * n * w;
-    HIP_TRY(ctx, launch_rs_encode((int)k, e, s));
-  }
+    return DAGPU_OK;
+  };
   // solveCrossword: each round rebuilds every decodable row or every decodable
   // column (whichever set is larger) until no axis can make progress.
   // Fill route and deferral (repair.hip PlanArgs; DAGPU_REPAIR_FILL=0 turns
@@ -1196,8 +1203,12 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
       HIP_TRY(ctx, hipMemsetAsync(r.counters, 0, 2 * sizeof(int32_t), s));
       HIP_TRY(ctx, launch_vec_count(dr, s));
       HIP_TRY(ctx, launch_vec_count(dc, s));
-      int32_t cnt[3] = {0, 0, 0};
+      int32_t cnt[6] = {0, 0, 0, 0, 0, 0};
       HIP_TRY(ctx, read_small(cnt, r.counters, sizeof cnt, mb, s));
+      if (pass == 0 && round == 0 && cnt[5] > 0) {
+        const int prc = prerepair();
+        if (prc) return prc;
+      }
       deferred_total += cnt[2];
       if (cnt[0] == 0 && cnt[1] == 0) break;
       int ax = cnt[0] >= cnt[1] ? 0 : 1;
@@ -1276,7 +1287,11 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
     }
     if (!shortcut || deferred_total == 0) break;
     // deferred vectors whose codeword property is not implied: compare-mode encodes
-    HIP_TRY(ctx, launch_repair_defer_check(r.deferred, r.known, (int)k, (long)n, r.check, s));
+    HIP_TRY(ctx, hipMemsetAsync(r.counters + 6, 0, sizeof(int32_t), s));
+    HIP_TRY(ctx, launch_repair_defer_check(r.deferred, r.known, (int)k, (long)n, r.check, s, r.counters + 6));
+    int32_t left = 0;  // squares whose deferred axes are not proven codewords
+    HIP_TRY(ctx, read_small(&left, r.counters + 6, sizeof left, mb, s));
+    if (left == 0) break;
     for (int axis = 0; axis < 2; axis++) {
       EncodeArgs e{};
       e.in = d_eds;

@@ -154,7 +154,9 @@ constexpr int kRepByz = 4;         // rebuilt axis, root mismatch
 constexpr int kRepIncomplete = 8;  // crossword could not finish
 // Axis arrays (complete, root_bad, parity_bad) are [axis][square][idx].
 // complete[axis*nsq*w + sq*w + idx] = axis fully present
-hipError_t launch_axis_complete(const uint8_t* present, int k, long nsq, int32_t* complete, hipStream_t s);
+// (optional) *ncomplete += number of complete axes
+hipError_t launch_axis_complete(const uint8_t* present, int k, long nsq, int32_t* complete, hipStream_t s,
+                                int32_t* ncomplete = nullptr);
 // root_bad[a] = 1 for an axis complete before the repair whose root differs
 // (pre-repair "bad root input"); a rebuilt axis whose root differs ORs kRepByz
 // into bits[sq]; an incomplete axis ORs kRepIncomplete
@@ -196,9 +198,10 @@ hipError_t launch_repair_plan(const PlanArgs& p, hipStream_t s);
 // After the crossword: squares with deferred axes whose codeword property does
 // not follow from the known ones (all rows and the columns < k, or all columns
 // and the rows < k) keep their deferred[] marks for a compare-mode encode;
-// the others' marks are cleared.  check[sq] = 0.
+// the others' marks are cleared.  check[sq] = 0; (optional) *nleft += squares
+// whose marks stay.
 hipError_t launch_repair_defer_check(int32_t* deferred, const int32_t* known, int k, long nsq, int32_t* check,
-                                     hipStream_t s);
+                                     hipStream_t s, int32_t* nleft = nullptr);
 // Decodable vectors and counts without locators (Repair rounds): one lane per
 // vector; flags[v], vec_counts[v] (when set) and *ndecodable as the locator pass
 // would leave them.

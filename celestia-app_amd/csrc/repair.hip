@@ -26,7 +26,7 @@ __device__ __forceinline__ void axis_of(long a, int w, long nsq, long& sq, int& 
 
 // one wave per axis: complete[axis][sq][idx]
 __global__ __launch_bounds__(64) void axis_complete_kernel(const uint8_t* present, int k, long nsq,
-                                                            int32_t* complete) {
+                                                            int32_t* complete, int32_t* ncomplete) {
   const long a = blockIdx.x;
   const int w = 2 * k;
   long sq;
@@ -40,6 +40,7 @@ __global__ __launch_bounds__(64) void axis_complete_kernel(const uint8_t* presen
   }
   missing = __any(missing);
   if (threadIdx.x == 0) complete[a] = missing ? 0 : 1;
+  if (threadIdx.x == 0 && !missing && ncomplete) atomicAdd(ncomplete, 1);
 }
 
 // 0x80 in every byte of x that is nonzero (no carries between bytes)
@@ -50,7 +51,7 @@ __device__ __forceinline__ uint32_t nonzero_bytes_hi(uint32_t x) {
 // Rows, w % 16 == 0 and 16-B aligned presence: L = w / 16 lanes per row, each
 // one 16-B load; a row is complete when no lane of its group saw a zero byte.
 __global__ __launch_bounds__(256) void axis_complete_rows_kernel(const uint8_t* present, int k, long nsq,
-                                                                 int32_t* complete) {
+                                                                 int32_t* complete, int32_t* ncomplete) {
   const int w = 2 * k, L = w / 16;
   const long t = (long)blockIdx.x * 256 + threadIdx.x;
   const long nrow = nsq * w;
@@ -65,14 +66,17 @@ __global__ __launch_bounds__(256) void axis_complete_rows_kernel(const uint8_t* 
   const int lane = threadIdx.x & 63;
   const int g = lane / L;  // L <= 64 and divides 64 (w = 16 .. 1024)
   const uint64_t m = (L == 64 ? ~0ull : ((1ull << L) - 1)) << (g * L);
-  if (row < nrow && lane == g * L) complete[row] = (b & m) ? 0 : 1;
+  const bool done = row < nrow && lane == g * L && !(b & m);
+  if (row < nrow && lane == g * L) complete[row] = done ? 1 : 0;
+  const uint64_t dm = __ballot(done);
+  if (ncomplete && dm && lane == 0) atomicAdd(ncomplete, (int)__popcll(dm));
 }
 
 // Columns, w % 4 == 0 and 4-B aligned presence: block = (square, 256 columns);
 // lane j holds columns 4j..4j+3 (dword loads, coalesced along the row), the
 // four waves take every fourth row, AND-combined in LDS.
 __global__ __launch_bounds__(256) void axis_complete_cols_kernel(const uint8_t* present, int k, long nsq,
-                                                                 int32_t* complete) {
+                                                                 int32_t* complete, int32_t* ncomplete) {
   __shared__ uint32_t acc_s[4][64];
   const int w = 2 * k;
   const int ngrp = (w + 255) / 256;
@@ -90,25 +94,31 @@ __global__ __launch_bounds__(256) void axis_complete_cols_kernel(const uint8_t* 
   if (wave == 0 && c < w) {
     const uint32_t all = acc_s[0][lane] & acc_s[1][lane] & acc_s[2][lane] & acc_s[3][lane];
     int32_t* out = complete + nsq * w + sq * w + c;
+    int nc = 0;
 #pragma unroll
-    for (int j = 0; j < 4; j++) out[j] = ((all >> (8 * j + 7)) & 1) ? 1 : 0;
+    for (int j = 0; j < 4; j++) {
+      const int cj = (all >> (8 * j + 7)) & 1;
+      out[j] = cj;
+      nc += cj;
+    }
+    if (nc && ncomplete) atomicAdd(ncomplete, nc);
   }
 }
 
 hipError_t launch_axis_complete(const uint8_t* present, int k, long nsq, int32_t* complete,
-                                hipStream_t s) {
+                                hipStream_t s, int32_t* ncomplete) {
   const long n = nsq * 4L * k;
   if (n <= 0) return hipSuccess;
   const int w = 2 * k;
   if (w >= 16 && ((uintptr_t)present & 15) == 0) {
     const long threads = nsq * w * (w / 16);
     hipLaunchKernelGGL(axis_complete_rows_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, present,
-                       k, nsq, complete);
+                       k, nsq, complete, ncomplete);
     hipLaunchKernelGGL(axis_complete_cols_kernel, dim3((unsigned)(nsq * ((w + 255) / 256))), dim3(256), 0, s,
-                       present, k, nsq, complete);
+                       present, k, nsq, complete, ncomplete);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(axis_complete_kernel, dim3((unsigned)n), dim3(64), 0, s, present, k, nsq, complete);
+  hipLaunchKernelGGL(axis_complete_kernel, dim3((unsigned)n), dim3(64), 0, s, present, k, nsq, complete, ncomplete);
   return hipGetLastError();
 }
 
@@ -418,7 +428,7 @@ hipError_t launch_repair_plan(const PlanArgs& p, hipStream_t s) {
 // every row and every column < k is known to be a codeword (then the square is
 // G A G^T: every column is one) or every column and every row < k is.
 __global__ __launch_bounds__(256) void repair_defer_check_kernel(int32_t* deferred, const int32_t* known, int k,
-                                                                  long nsq, int32_t* check) {
+                                                                  long nsq, int32_t* check, int32_t* nleft) {
   __shared__ int any_def, rows_all, cols_low, cols_all, rows_low;
   const long sq = blockIdx.x;
   const int w = 2 * k;
@@ -435,7 +445,11 @@ __global__ __launch_bounds__(256) void repair_defer_check_kernel(int32_t* deferr
     if (!known[c]) { cols_all = 0; if (i < k) cols_low = 0; }
   }
   __syncthreads();
-  if (!any_def || !((rows_all && cols_low) || (cols_all && rows_low))) return;
+  if (!any_def) return;
+  if (!((rows_all && cols_low) || (cols_all && rows_low))) {
+    if (threadIdx.x == 0 && nleft) atomicAdd(nleft, 1);  // this square's marks stay for the compare
+    return;
+  }
   for (int i = threadIdx.x; i < w; i += 256) {
     deferred[sq * w + i] = 0;
     deferred[(nsq + sq) * w + i] = 0;
@@ -443,10 +457,10 @@ __global__ __launch_bounds__(256) void repair_defer_check_kernel(int32_t* deferr
 }
 
 hipError_t launch_repair_defer_check(int32_t* deferred, const int32_t* known, int k, long nsq, int32_t* check,
-                                     hipStream_t s) {
+                                     hipStream_t s, int32_t* nleft) {
   if (nsq <= 0) return hipSuccess;
   hipLaunchKernelGGL(repair_defer_check_kernel, dim3((unsigned)nsq), dim3(256), 0, s, deferred, known, k, nsq,
-                     check);
+                     check, nleft);
   return hipGetLastError();
 }
 
