@@ -35,6 +35,7 @@ ERR_SQUARE = -13
 # Every symbol include/dagpu.h declares (checked by tests/test_abi_cpu.py).
 EXPORTS = (
     "dagpu_version",
+    "dagpu_max_square_width",
     "dagpu_init",
     "dagpu_destroy",
     "dagpu_last_error",
@@ -63,6 +64,7 @@ EXPORTS = (
     "dagpu_profile_enable",
     "dagpu_profile_read",
     "dagpu_profile_stages",
+    "dagpu_repair_stats",
     "dagpu_dah_hash",
     "dagpu_nmt_roots",
     "dagpu_wrapper_roots",
@@ -141,6 +143,7 @@ def lib() -> ctypes.CDLL:
         if os.environ.get("DAGPU_LIB"):
             L = _Tolerant(L)
         L.dagpu_version.restype = ctypes.c_int
+        L.dagpu_max_square_width.restype = ctypes.c_uint32
         L.dagpu_init.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
         L.dagpu_destroy.argtypes = [vp]
         L.dagpu_destroy.restype = None
@@ -172,6 +175,7 @@ def lib() -> ctypes.CDLL:
         L.dagpu_repair_workspace_size.restype = sz
         L.dagpu_repair.argtypes = [vp, ctypes.c_uint32, vp, vp, vp, vp]
         L.dagpu_profile_stages.argtypes = [vp, vp]
+        L.dagpu_repair_stats.argtypes = [vp, vp]
         L.dagpu_repair_ex.argtypes = [vp, ctypes.c_uint32, vp, vp, vp, vp, vp]
         L.dagpu_square_construct.argtypes = [vp, vp, vp, sz, ctypes.c_uint32, ctypes.c_uint32, vp, sz, vp]
         L.dagpu_square_build.argtypes = [vp, vp, vp, sz, ctypes.c_uint32, ctypes.c_uint32, vp, sz, vp, vp]

@@ -98,6 +98,12 @@ class Context:
     def last_error(self) -> str:
         return self._L.dagpu_last_error(self.handle).decode()
 
+    def repair_stats(self) -> dict:
+        """Schedule of the last Repair on this context (dagpu_repair_stats)."""
+        out = np.zeros(5, np.int64)
+        self.check(self._L.dagpu_repair_stats(self.handle, out.ctypes.data))
+        return dict(zip(("rounds", "fills", "reverse_fills", "decodes", "deferred"), (int(x) for x in out)))
+
     def check(self, rc: int) -> None:
         if rc != 0:
             cls = _ERR_CLASS.get(rc, DAError)
@@ -397,13 +403,23 @@ class LeoRSCodec:
     """rsmt2d.Codec backed by the GPU Leopard encoder (LeoRSCodec equivalent)."""
 
     def __init__(self, ctx: Optional[Context] = None):
-        self.ctx = ctx or default_context()
+        self._ctx = ctx  # opened on first use, so the host-side checks need no GPU
+
+    @property
+    def ctx(self) -> Context:
+        if self._ctx is None:
+            self._ctx = default_context()
+        return self._ctx
 
     def name(self) -> str:
         return "Leopard"
 
     def max_chunks(self) -> int:
-        return 32768 * 32768
+        """rsmt2d Codec.MaxChunks: ODS chunks of the widest square this library
+        serves (dagpu_max_square_width()^2; upstream Leopard reports 32768^2,
+        beyond one GPU's HBM -- include/dagpu.h DAGPU_MAX_SQUARE_WIDTH)."""
+        w = int(_abi.lib().dagpu_max_square_width())
+        return w * w
 
     def encode(self, data: Sequence[bytes]) -> List[bytes]:
         m = _as_matrix(data)
@@ -423,7 +439,9 @@ class LeoRSCodec:
     def decode(self, shards: Sequence[Optional[bytes]]) -> List[bytes]:
         """Leopard Reconstruct: None marks a missing shard; returns all 2k shards."""
         n = len(shards)
-        size = next(len(s) for s in shards if s is not None)
+        size = next((len(s) for s in shards if s is not None), None)
+        if size is None:  # reedsolomon Reconstruct with no shard at all
+            raise ErrTooFewShards(_abi.ERR_TOO_FEW_SHARDS, "too few shards given")
         buf = np.zeros((n, size), np.uint8)
         present = np.zeros(n, np.uint8)
         for i, s in enumerate(shards):

@@ -359,6 +359,11 @@ extern "C" {
 
 int dagpu_version(void) { return 100; }
 
+uint32_t dagpu_max_square_width(void) {
+  static_assert(DAGPU_MAX_SQUARE_WIDTH == kMaxK, "header and kernels disagree on the widest square");
+  return (uint32_t)kMaxK;
+}
+
 int dagpu_init(int device, dagpu_ctx** out) {
   if (!out) return DAGPU_ERR_ARG;
   *out = nullptr;
@@ -790,9 +795,9 @@ int dagpu_decode(dagpu_ctx* ctx, uint32_t k, size_t nvec, size_t shard_size, uin
   da.p_shard_stride = 1;
   da.err = (uint8_t*)ctx->ws.p;
   da.flags = (int32_t*)((uint8_t*)ctx->ws.p + errb);
-  // locator sharing runs one workgroup over all vectors of a "square" (<= 1024)
-  da.err_key = nvec <= 1024 ? da.flags + nvec : nullptr;
-  da.err_head = nvec <= 1024 ? da.flags + 2 * nvec : nullptr;
+  // locator sharing runs one workgroup over all vectors of a "square" (<= 2 kMaxK)
+  da.err_key = nvec <= 2 * (size_t)kMaxK ? da.flags + nvec : nullptr;
+  da.err_head = nvec <= 2 * (size_t)kMaxK ? da.flags + 2 * nvec : nullptr;
   da.too_few = (int32_t*)ctx->status.p;
   da.nsq = 1;
   da.nvec = (long)nvec;
@@ -1136,6 +1141,8 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
   HIP_TRY(ctx, hipMemsetAsync(r.bits, 0, n * sizeof(int32_t), s));
   HIP_TRY(ctx, hipMemsetAsync(r.parity_bad, 0, n * 2 * w * sizeof(int32_t), s));
   HIP_TRY(ctx, hipMemsetAsync(r.counters + 5, 0, 2 * sizeof(int32_t), s));  // [5] complete axes, [6] deferred squares
+  HIP_TRY(ctx, hipMemsetAsync(r.counters + 8, 0, 3 * sizeof(int32_t), s));  // [8..10] planned fills / decodes
+  int64_t rounds_run = 0, deferred_run = 0;
   HIP_TRY(ctx, launch_axis_complete(d_present, (int)k, (long)n, r.complete_before, s, r.counters + 5));
   // prerepairSanityCheck: complete axes must satisfy parity == Encode(data).
   // Queued after the first round's counter read, and only when some axis is
@@ -1203,14 +1210,24 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
       HIP_TRY(ctx, hipMemsetAsync(r.counters, 0, 2 * sizeof(int32_t), s));
       HIP_TRY(ctx, launch_vec_count(dr, s));
       HIP_TRY(ctx, launch_vec_count(dc, s));
-      int32_t cnt[6] = {0, 0, 0, 0, 0, 0};
+      int32_t cnt[11] = {};
       HIP_TRY(ctx, read_small(cnt, r.counters, sizeof cnt, mb, s));
+      {  // schedule totals so far (diagnostics): plans of the earlier rounds are complete
+        std::lock_guard<std::mutex> g(ctx->prof_mu);
+        ctx->rep_stats[0] = rounds_run;
+        ctx->rep_stats[1] = cnt[8];
+        ctx->rep_stats[2] = cnt[9];
+        ctx->rep_stats[3] = cnt[10];
+        ctx->rep_stats[4] = deferred_run + cnt[2];
+      }
       if (pass == 0 && round == 0 && cnt[5] > 0) {
         const int prc = prerepair();
         if (prc) return prc;
       }
       deferred_total += cnt[2];
+      deferred_run += cnt[2];
       if (cnt[0] == 0 && cnt[1] == 0) break;
+      rounds_run++;
       int ax = cnt[0] >= cnt[1] ? 0 : 1;
       // after a deferral the other axis is the one with complete data halves
       if (cnt[2] > 0 && last_ax >= 0 && cnt[1 - last_ax] > 0) ax = 1 - last_ax;
@@ -1247,6 +1264,7 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
         pa.deferred = r.deferred;
         pa.nodefer = r.nodefer;
         pa.ndeferred = r.counters + 2;
+        pa.nplan = r.counters + 8;
         pa.k = (int)k;
         pa.nsq = (long)n;
         pa.axis = ax;
@@ -1332,7 +1350,11 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
   HIP_TRY(ctx, launch_verify_roots(d_rr, d_cr, r.sa.row_roots, r.sa.col_roots, r.complete_now,
                                    r.complete_before, (int)k, (long)n, r.bits, r.root_bad, s));
   HIP_TRY(ctx, launch_finalize_repair(r.bits, r.complete_before, r.root_bad, r.parity_bad, (int)k, (long)n,
-                                      d_status, d_byz, s));
+                                      d_status, d_byz, s, r.check));
+  // a square failing prerepairSanityCheck is left as its input (rsmt2d never
+  // reaches solveCrossword for it): presence back to p0; the bytes of cells
+  // not present are unspecified, as they are for any missing cell
+  HIP_TRY(ctx, launch_restore_presence(d_present, r.p0, r.check, (int)k, (long)n, s));
   if (!d_byz) return DAGPU_OK;
   // crossword failures: name the axis in rsmt2d's order (rare; synchronises)
   std::vector<int32_t> st(n), bz(4 * n);
@@ -1436,6 +1458,13 @@ int dagpu_profile_enable(dagpu_ctx* ctx, int on) {
   if (!ctx) return DAGPU_ERR_ARG;
   ctx->prof = (on & 1) != 0;
   ctx->stages_on = (on & 2) != 0;
+  return DAGPU_OK;
+}
+
+int dagpu_repair_stats(dagpu_ctx* ctx, int64_t* out) {
+  if (!ctx || !out) return DAGPU_ERR_ARG;
+  std::lock_guard<std::mutex> g(ctx->prof_mu);
+  for (int i = 0; i < DAGPU_REPAIR_STATS; i++) out[i] = ctx->rep_stats[i];
   return DAGPU_OK;
 }
 

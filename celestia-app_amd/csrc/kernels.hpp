@@ -9,7 +9,10 @@ constexpr int kShareSize = 512;
 constexpr int kNsSize = 29;
 constexpr int kNodeSize = 90;  // minNs(29) | maxNs(29) | sha256(32)
 constexpr int kDigest = 32;
-constexpr int kMaxK = 512;     // appconsts.SquareSizeUpperBound; GF(2^16) above k = 128
+// Widest square: (2k)^2 x 512 B of EDS = 128 GiB at k = 8192 fits the 288 GB of
+// HBM, k = 16384 (512 GiB) does not.  GF(2^16) above k = 128; register-resident
+// kernels at k = 256 / 512, LDS-slice kernels (rs_gf16_wide.hip) above.
+constexpr int kMaxK = 8192;
 
 // Bytes of error-locator workspace per decoded vector.
 constexpr long rs_err_bytes(int k) { return k <= 128 ? 256 : 4L * k; }
@@ -144,6 +147,10 @@ hipError_t launch_leo8_decode128_sliced(const DecodeArgs& a, hipStream_t s);
 hipError_t launch_leo16_encode(int k, const EncodeArgs& a, hipStream_t s);
 hipError_t launch_leo16_errlocs(const DecodeArgs& a, hipStream_t s);
 hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mark_present);
+// wide GF(2^16) (rs_gf16_wide.hip): k = 1024 .. kMaxK (also 256 / 512 for A/B)
+hipError_t launch_leo16w_encode(int k, const EncodeArgs& a, hipStream_t s);
+hipError_t launch_leo16w_errlocs(const DecodeArgs& a, hipStream_t s);
+hipError_t launch_leo16w_decode_only(const DecodeArgs& a, hipStream_t s, bool mark_present);
 hipError_t launch_rs_encode(int k, const EncodeArgs& a, hipStream_t s);
 hipError_t launch_rs_errlocs(const DecodeArgs& a, hipStream_t s);
 hipError_t launch_rs_decode_only(const DecodeArgs& a, hipStream_t s, bool mark_present);
@@ -190,6 +197,7 @@ struct PlanArgs {
   int32_t* deferred;
   const int32_t* nodefer;
   int32_t* ndeferred;
+  int32_t* nplan;  // optional: += [forward fills, reverse fills, decodes] of the round (diagnostics)
   int k;
   long nsq;
   int axis;
@@ -210,9 +218,13 @@ hipError_t launch_vec_count(const DecodeArgs& a, hipStream_t s);
 // `known` ([sq][idx] of that axis), known[v] = 0 where a.flags[v] is set too
 hipError_t launch_rs_mark_present(const DecodeArgs& a, const int32_t* flags, hipStream_t s,
                                   int32_t* known = nullptr);
+// (optional) pre_fail[sq] = 1 where the pre-repair check failed
 hipError_t launch_finalize_repair(const int32_t* bits, const int32_t* complete_before, const int32_t* root_bad,
                                   const int32_t* parity_bad, int k, long nsq, int32_t* status, int32_t* byz,
-                                  hipStream_t s);
+                                  hipStream_t s, int32_t* pre_fail = nullptr);
+// present of the squares with pre_fail[sq] set := p0 (their input presence)
+hipError_t launch_restore_presence(uint8_t* present, const uint8_t* p0, const int32_t* pre_fail, int k, long nsq,
+                                   hipStream_t s);
 
 struct SquareArgs {
   const uint8_t* eds;   // nsq squares, each (2k)^2 * 512 B, row-major

@@ -262,48 +262,18 @@ __global__ __launch_bounds__(256) void nmt_level_kernel(SquareArgs a, const uint
 // ---------------------------------------------------------------------------
 // Kernel 3: DAH = RFC-6962 root over rowRoots || colRoots (2w items of 90 B).
 // leaf = SHA256(0x00 | root) (91 B, 2 blocks); inner = SHA256(0x01 | l | r).
+// One workgroup per square.  The n = 4k leaves go through LDS in chunks of
+// C = min(n, 2048): each chunk's leaf digests are reduced to the root of its
+// subtree (n and C are powers of two, so every chunk is an exact subtree of
+// the RFC-6962 split), the n / C subtree digests (1 up to k = 512, 32 at
+// k = 16384) then to the DAH.
 // ---------------------------------------------------------------------------
-constexpr int kDahThreads = 1024;  // one lane per leaf up to k = 256
+constexpr int kDahThreads = 1024;
+constexpr int kDahChunk = 2048;
 
-__global__ __launch_bounds__(kDahThreads) void dah_kernel(SquareArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];  // (n + n/2) * 8 dwords
-  const long sq = blockIdx.x;
-  const int w = 2 * a.k;
-  const int n = 2 * w;
-  for (int i = threadIdx.x; i < n; i += kDahThreads) {
-    const uint8_t* root = (i < w ? a.row_roots + (sq * w + i) * kNodeSize
-                                 : a.col_roots + (sq * w + (i - w)) * kNodeSize);
-    // message bytes: [0]=0x00, [1..90]=root, [91]=0x80, len=728 bits
-    uint32_t m[32];
-#pragma unroll
-    for (int j = 0; j < 32; j++) m[j] = 0;
-    const uint16_t* r16 = (const uint16_t*)root;  // 2-B aligned (90 B stride)
-#pragma unroll
-    for (int h = 0; h < 45; h++) {
-      const uint32_t v = r16[h];
-      const int off = 1 + 2 * h;  // byte offset of this halfword in the message
-      m[off >> 2] |= v << (8 * (off & 3));
-      if ((off & 3) == 3) m[(off >> 2) + 1] |= v >> 8;
-    }
-    m[91 >> 2] |= 0x80u << (8 * (91 & 3));
-    uint32_t st[8];
-    sha256_init(st);
-#pragma unroll
-    for (int blk = 0; blk < 2; blk++) {
-      uint32_t wv[16];
-#pragma unroll
-      for (int j = 0; j < 16; j++) wv[j] = bswap32(m[16 * blk + j]);
-      if (blk == 1) { wv[14] = 0; wv[15] = 91u * 8u; }
-      sha256_compress(st, wv);
-    }
-#pragma unroll
-    for (int j = 0; j < 8; j++) lds[i * 8 + j] = bswap32(st[j]);
-  }
-  __syncthreads();
-  // inner levels ping-pong between lds[0, n) and lds[n, n + n/2) (digest slots)
-  uint32_t* src = lds;
-  uint32_t* dst = lds + n * 8;
-  int cur = n;
+// RFC-6962 inner levels over cur digests at src (8 dwords each), ping-ponging
+// with dst (cur / 2 slots); returns the buffer holding the root.
+__device__ uint32_t* rfc_reduce(uint32_t* src, uint32_t* dst, int cur) {
   while (cur > 1) {
     const int next = cur / 2;
     for (int i = threadIdx.x; i < next; i += kDahThreads) {
@@ -336,9 +306,57 @@ __global__ __launch_bounds__(kDahThreads) void dah_kernel(SquareArgs a) {
     dst = t;
     cur = next;
   }
+  return src;
+}
+
+__global__ __launch_bounds__(kDahThreads) void dah_kernel(SquareArgs a) {
+  // (C + C/2) leaf / level slots, then n / C subtree digests (8 dwords each)
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const long sq = blockIdx.x;
+  const int w = 2 * a.k;
+  const int n = 2 * w;
+  const int C = n < kDahChunk ? n : kDahChunk;
+  uint32_t* sub = lds + (C + C / 2) * 8;
+  for (int c0 = 0; c0 < n; c0 += C) {
+    for (int i = threadIdx.x; i < C; i += kDahThreads) {
+      const int li = c0 + i;
+      const uint8_t* root = (li < w ? a.row_roots + (sq * w + li) * kNodeSize
+                                    : a.col_roots + (sq * w + (li - w)) * kNodeSize);
+      // message bytes: [0]=0x00, [1..90]=root, [91]=0x80, len=728 bits
+      uint32_t m[32];
+#pragma unroll
+      for (int j = 0; j < 32; j++) m[j] = 0;
+      const uint16_t* r16 = (const uint16_t*)root;  // 2-B aligned (90 B stride)
+#pragma unroll
+      for (int h = 0; h < 45; h++) {
+        const uint32_t v = r16[h];
+        const int off = 1 + 2 * h;  // byte offset of this halfword in the message
+        m[off >> 2] |= v << (8 * (off & 3));
+        if ((off & 3) == 3) m[(off >> 2) + 1] |= v >> 8;
+      }
+      m[91 >> 2] |= 0x80u << (8 * (91 & 3));
+      uint32_t st[8];
+      sha256_init(st);
+#pragma unroll
+      for (int blk = 0; blk < 2; blk++) {
+        uint32_t wv[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) wv[j] = bswap32(m[16 * blk + j]);
+        if (blk == 1) { wv[14] = 0; wv[15] = 91u * 8u; }
+        sha256_compress(st, wv);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; j++) lds[i * 8 + j] = bswap32(st[j]);
+    }
+    __syncthreads();
+    const uint32_t* r = rfc_reduce(lds, lds + C * 8, C);
+    if (threadIdx.x < 8) sub[(c0 / C) * 8 + threadIdx.x] = r[threadIdx.x];
+    __syncthreads();
+  }
+  const uint32_t* root = rfc_reduce(sub, lds, n / C);
   if (threadIdx.x < 8) {
     uint32_t* out = (uint32_t*)(a.dah + sq * 32);
-    out[threadIdx.x] = src[threadIdx.x];
+    out[threadIdx.x] = root[threadIdx.x];
   }
 }
 
@@ -410,7 +428,8 @@ void nmt_workspace_carve(SquareArgs& a, void* ws) {
 hipError_t launch_dah(const SquareArgs& a, hipStream_t s) {
   const int n = 4 * a.k;
   if (a.k > kMaxK) return hipErrorInvalidValue;
-  const size_t lds = (size_t)(n + n / 2) * 8 * sizeof(uint32_t);  // <= 96 KiB at k = 512
+  const int C = n < kDahChunk ? n : kDahChunk;
+  const size_t lds = ((size_t)(C + C / 2) + (size_t)(n / C)) * 8 * sizeof(uint32_t);  // <= 97 KiB
   if (lds > 65536) {
     hipError_t e = hipFuncSetAttribute((const void*)dah_kernel,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

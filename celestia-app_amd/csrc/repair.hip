@@ -110,7 +110,7 @@ hipError_t launch_axis_complete(const uint8_t* present, int k, long nsq, int32_t
   const long n = nsq * 4L * k;
   if (n <= 0) return hipSuccess;
   const int w = 2 * k;
-  if (w >= 16 && ((uintptr_t)present & 15) == 0) {
+  if (w >= 16 && w <= 1024 && ((uintptr_t)present & 15) == 0) {  // L = w / 16 lanes <= 64
     const long threads = nsq * w * (w / 16);
     hipLaunchKernelGGL(axis_complete_rows_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, present,
                        k, nsq, complete, ncomplete);
@@ -172,7 +172,8 @@ hipError_t launch_verify_roots(const uint8_t* exp_rr, const uint8_t* exp_cr, con
 // exact_repair); then "no progress" (ErrUnrepairableDataSquare).
 __global__ __launch_bounds__(256) void finalize_repair_kernel(const int32_t* bits, const int32_t* complete_before,
                                                               const int32_t* root_bad, const int32_t* parity_bad,
-                                                              int k, long nsq, int32_t* status, int32_t* byz) {
+                                                              int k, long nsq, int32_t* status, int32_t* byz,
+                                                              int32_t* pre_fail) {
   __shared__ int key_s;
   const long sq = blockIdx.x;
   const int w = 2 * k;
@@ -203,6 +204,7 @@ __global__ __launch_bounds__(256) void finalize_repair_kernel(const int32_t* bit
     st = DAGPU_ERR_UNREPAIRABLE;
   }
   status[sq] = st;
+  if (pre_fail) pre_fail[sq] = key_s != 0x7fffffff;
   if (byz) {
     byz[4 * sq + 0] = ax;
     byz[4 * sq + 1] = ix;
@@ -213,10 +215,32 @@ __global__ __launch_bounds__(256) void finalize_repair_kernel(const int32_t* bit
 
 hipError_t launch_finalize_repair(const int32_t* bits, const int32_t* complete_before, const int32_t* root_bad,
                                   const int32_t* parity_bad, int k, long nsq, int32_t* status, int32_t* byz,
-                                  hipStream_t s) {
+                                  hipStream_t s, int32_t* pre_fail) {
   if (nsq <= 0) return hipSuccess;
   hipLaunchKernelGGL(finalize_repair_kernel, dim3((unsigned)nsq), dim3(256), 0, s, bits, complete_before,
-                     root_bad, parity_bad, k, nsq, status, byz);
+                     root_bad, parity_bad, k, nsq, status, byz, pre_fail);
+  return hipGetLastError();
+}
+
+// rsmt2d returns from prerepairSanityCheck before solveCrossword: a square that
+// fails it keeps its input presence (the crossword ran beside the check here).
+__global__ __launch_bounds__(256) void restore_presence_kernel(uint8_t* present, const uint8_t* p0,
+                                                               const int32_t* pre_fail, long per_sq, long nsq) {
+  const long n4 = per_sq / 4;
+  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= n4 * nsq) return;
+  const long sq = gid / n4;
+  if (!pre_fail[sq]) return;
+  ((uint32_t*)present)[gid] = ((const uint32_t*)p0)[gid];
+}
+
+hipError_t launch_restore_presence(uint8_t* present, const uint8_t* p0, const int32_t* pre_fail, int k, long nsq,
+                                   hipStream_t s) {
+  const long per = 4L * k * k;  // (2k)^2 flags, a multiple of 4
+  const long threads = nsq * (per / 4);
+  if (threads <= 0) return hipSuccess;
+  hipLaunchKernelGGL(restore_presence_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, present, p0,
+                     pre_fail, per, nsq);
   return hipGetLastError();
 }
 
@@ -263,7 +287,9 @@ __global__ __launch_bounds__(1024) void vec_count_rows_kernel(DecodeArgs a) {
     const uint8_t* pres = a.present + sq * a.p_sq_stride + (v - sq * a.nvec) * a.p_vec_stride;
     const int k = a.k, n = 2 * k;
     int sys = 0, tot = 0;
-    if (k >= 8 && ((uintptr_t)pres & 15) == 0) {
+    // 16-flag loads only where every load lies inside one half (k >= 16): a
+    // load straddling index k would count parity flags as data
+    if (k >= 16 && ((uintptr_t)pres & 15) == 0) {
       const uint4* q = (const uint4*)pres;
       for (int j = lane; j < n / 16; j += 64) {
         const uint4 x = q[j];
@@ -336,51 +362,47 @@ __global__ __launch_bounds__(kPlanThreads) void repair_plan_kernel(PlanArgs p) {
   const int k = p.k, w = 2 * k;
   if (threadIdx.x == 0) low_ok = 1;
   __syncthreads();
-  // vectors i = threadIdx.x + 256 m (w <= 1024)
-  constexpr int kPer = 4;
-  int sys[kPer], tot[kPer];
-  bool dec[kPer];
-#pragma unroll
-  for (int m = 0; m < kPer; m++) {
-    const int i = threadIdx.x + kPlanThreads * m;
-    sys[m] = tot[m] = 0;
-    dec[m] = false;
-    if (i >= w) continue;
+  // vectors i = threadIdx.x + 256 m, any w
+  for (int i = threadIdx.x; i < k; i += kPlanThreads) {
     const int32_t c = p.counts[sq * w + i];
-    sys[m] = c & 0xFFFF;
-    tot[m] = c >> 16;
-    dec[m] = p.flags[sq * w + i] != 0;
-    if (i < k && !dec[m] && tot[m] != w) low_ok = 0;
+    if (!p.flags[sq * w + i] && (c >> 16) != w) low_ok = 0;
   }
   __syncthreads();
   const bool defer = low_ok && !p.nodefer[sq];
   int nf = 0, nr = 0, nd = 0;
   const long ax0 = (long)p.axis * p.nsq * w + sq * w;  // [axis][sq][idx]
-#pragma unroll
-  for (int m = 0; m < kPer; m++) {
-    const int i = threadIdx.x + kPlanThreads * m;
-    if (i >= w) continue;
+  for (int i = threadIdx.x; i < w; i += kPlanThreads) {
     const long v = sq * w + i;
+    const int32_t c = p.counts[v];
+    const int sys = c & 0xFFFF, tot = c >> 16;
+    const bool dec = p.flags[v] != 0;
     // forward fill: data half complete; reverse fill: parity half complete
-    const bool f = dec[m] && sys[m] == k;
-    const bool r = dec[m] && !f && tot[m] - sys[m] == k;
+    const bool f = dec && sys == k;
+    const bool r = dec && !f && tot - sys == k;
     p.fill[v] = f ? 1 : (r ? 2 : 0);
     if (f || r) {
       p.flags[v] = 0;
       p.known[ax0 + i] = 1;
       if (f) nf++;
       else nr++;
-    } else if (dec[m]) {
+    } else if (dec) {
       if (defer && i >= k) {
         p.flags[v] = 0;
         p.deferred[ax0 + i] = 1;
         nd++;
       } else {
-        p.known[ax0 + i] = tot[m] == k;
+        p.known[ax0 + i] = tot == k;
       }
     }
   }
   if (nd) atomicAdd(p.ndeferred, nd);
+  if (p.nplan) {
+    int ndec = 0;
+    for (int i = threadIdx.x; i < w; i += kPlanThreads) ndec += p.flags[sq * w + i] != 0;
+    if (nf) atomicAdd(p.nplan + 0, nf);
+    if (nr) atomicAdd(p.nplan + 1, nr);
+    if (ndec) atomicAdd(p.nplan + 2, ndec);
+  }
   if (!p.pair_list) return;
   // pair lists: the square's forward fills in pairs, its reverse fills in
   // pairs in the second list; an odd one is paired with -1
@@ -405,10 +427,7 @@ __global__ __launch_bounds__(kPlanThreads) void repair_plan_kernel(PlanArgs p) {
   int32_t* out = p.pair_list + 2L * base_s;
   int32_t* rout = p.pair_list_rev + 2L * rbase_s;
   int o = nfill_s[threadIdx.x], ro = nrev_s[threadIdx.x];
-#pragma unroll
-  for (int m = 0; m < kPer; m++) {
-    const int i = threadIdx.x + kPlanThreads * m;
-    if (i >= w) continue;
+  for (int i = threadIdx.x; i < w; i += kPlanThreads) {
     const int32_t fv = p.fill[sq * w + i];
     if (fv == 1) out[o++] = (int32_t)(sq * w + i);
     else if (fv == 2) rout[ro++] = (int32_t)(sq * w + i);
@@ -419,7 +438,6 @@ __global__ __launch_bounds__(kPlanThreads) void repair_plan_kernel(PlanArgs p) {
 
 hipError_t launch_repair_plan(const PlanArgs& p, hipStream_t s) {
   if (p.nsq <= 0) return hipSuccess;
-  if (2 * p.k > 4 * kPlanThreads) return hipErrorInvalidValue;
   hipLaunchKernelGGL(repair_plan_kernel, dim3((unsigned)p.nsq), dim3(kPlanThreads), 0, s, p);
   return hipGetLastError();
 }

@@ -1218,11 +1218,20 @@ hipError_t ensure_tables() {
   return hipSuccess;
 }
 
-bool gf16_k_ok(int k) { return k >= 256 && k <= kMaxK && (k & (k - 1)) == 0; }
+bool gf16_k_ok(int k) { return k >= 256 && k <= 512 && (k & (k - 1)) == 0; }
 
 }  // namespace
 
+// Wide squares (k > 512) and DAGPU_GF16_WIDE=1 (A/B of the wide kernels at
+// k = 256 / 512): the LDS-slice kernels of rs_gf16_wide.hip.
+static bool use_wide(int k) {
+  if (k > 512) return true;
+  const char* e = getenv("DAGPU_GF16_WIDE");
+  return e && e[0] == '1';
+}
+
 hipError_t launch_leo16_encode(int k, const EncodeArgs& a, hipStream_t s) {
+  if (use_wide(k)) return launch_leo16w_encode(k, a, s);
   if (!gf16_k_ok(k) || a.shard_bytes % 64) return hipErrorInvalidValue;
   if (a.reverse && !a.out_present) return hipErrorInvalidValue;  // reverse transform: Repair fill only
   hipError_t e = ensure_tables();
@@ -1251,6 +1260,7 @@ hipError_t launch_leo16_encode(int k, const EncodeArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_leo16_errlocs(const DecodeArgs& a, hipStream_t s) {
+  if (a.k > 512) return launch_leo16w_errlocs(a, s);
   if (!gf16_k_ok(a.k)) return hipErrorInvalidValue;
   hipError_t e = ensure_tables();
   if (e != hipSuccess) return e;
@@ -1282,6 +1292,7 @@ static hipError_t dec_lds_attr() {  // above the 64 KiB default: once per proces
 }
 
 hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mark_present) {
+  if (use_wide(a.k)) return launch_leo16w_decode_only(a, s, mark_present);
   if (!gf16_k_ok(a.k) || a.shard_bytes % 64) return hipErrorInvalidValue;
   hipError_t e = ensure_tables();
   if (e != hipSuccess) return e;
@@ -1379,21 +1390,22 @@ __global__ __launch_bounds__(1024) void errloc_key_cols_kernel(DecodeArgs a) {
   if (wave == 0 && v < a.nvec) a.err_key[sq * a.nvec + v] = (int32_t)acc[lane];
 }
 
-// One workgroup per square (nvec <= 1024): keys in LDS, candidate head = the
-// first vector with an equal key.
+// One workgroup per square (nvec <= kMaxHeadVec): keys in LDS, candidate head =
+// the first vector with an equal key.
+constexpr int kMaxHeadVec = 2 * kMaxK;
 __global__ __launch_bounds__(1024) void errloc_heads_kernel(DecodeArgs a) {
-  __shared__ int32_t key[1024];
+  extern __shared__ int32_t key[];  // nvec
   const long sq = blockIdx.x;
-  const int t = threadIdx.x;
   const int nvec = (int)a.nvec;
   const long v0 = sq * a.nvec;
-  if (t < nvec) key[t] = a.err_key[v0 + t];
+  for (int t = threadIdx.x; t < nvec; t += 1024) key[t] = a.err_key[v0 + t];
   __syncthreads();
-  if (t >= nvec) return;
-  const int32_t kt = key[t];
-  int u = 0;
-  while (key[u] != kt) u++;  // ends at t at the latest
-  a.err_head[v0 + t] = (int32_t)(v0 + u);
+  for (int t = threadIdx.x; t < nvec; t += 1024) {
+    const int32_t kt = key[t];
+    int u = 0;
+    while (key[u] != kt) u++;  // ends at t at the latest
+    a.err_head[v0 + t] = (int32_t)(v0 + u);
+  }
 }
 
 // Candidate heads checked flag by flag (a key collision falls back to the
@@ -1438,7 +1450,7 @@ hipError_t launch_errloc_heads(const DecodeArgs& a, hipStream_t s) {
   if (!a.err_key || !a.err_head) return hipSuccess;
   const long nv = a.nsq * a.nvec;
   if (nv <= 0) return hipSuccess;
-  if (a.nvec > 1024) return hipErrorInvalidValue;
+  if (a.nvec > kMaxHeadVec) return hipErrorInvalidValue;
   if (a.p_shard_stride == 1)
     hipLaunchKernelGGL(errloc_key_rows_kernel, dim3((unsigned)((nv + 15) / 16)), dim3(1024), 0, s, a);
   else
@@ -1446,7 +1458,7 @@ hipError_t launch_errloc_heads(const DecodeArgs& a, hipStream_t s) {
                        s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(errloc_heads_kernel, dim3((unsigned)a.nsq), dim3(1024), 0, s, a);
+  hipLaunchKernelGGL(errloc_heads_kernel, dim3((unsigned)a.nsq), dim3(1024), (size_t)a.nvec * 4, s, a);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (a.p_shard_stride == 1)

@@ -1,0 +1,649 @@
+// rs_gf16_wide.hip -- Leopard GF(2^16) encode / reconstruct for wide squares,
+// k = 1024 .. kMaxK (2k = 2048 .. 16384 shards per vector).
+//
+// Replaces klauspost/reedsolomon v1.11.8 leopardFF16 encode / reconstruct
+// (leopard.go), which rsmt2d v0.11.0 LeoRSCodec uses for every width above
+// 128; pkg/da/data_availability_header.go:65-75
+// ExtendShares itself puts no upper bound on k.  Same arithmetic as the
+// register-resident k = 256 / 512 kernels (rs_gf16.hip): a symbol is the byte
+// pair (b[i], b[i+32]) of a 64-byte block, IFFT/FFT butterflies with the
+// fftSkew multipliers, formal derivative and errLocs multiplies for decode.
+// Parity unpinned (no reference vector beyond k = 128): checked against the
+// oracle's GF(2^16) restatement and by erase/decode round trips.
+//
+// Layout.  At these widths one transform (m = k or n = 2k elements) does not
+// fit in registers: a workgroup keeps the elements of ONE column slice of ONE
+// vector in LDS -- S symbols of every element (S = 32 / 16 / 8 / 4, chosen so
+// the slice stays <= 128 KiB) as a low-byte plane and a high-byte plane of
+// dwords (4 symbols per dword, element-major, one pad dword per element
+// against bank conflicts).  Each butterfly stage is one pass of radix-4 units
+// (4 elements x G dword groups per lane, both layers of the radix-4 step in
+// registers, one barrier per stage).  A multiply by a skew constant is the
+// 16-dword product table of that skew position (the products of every 2-bit
+// group of a symbol, low and high bytes, for v_perm; 1 MiB for all positions
+// < 2 kMaxK), loaded once per unit and applied to its G groups.  The decoder's
+// per-element errLocs multiplies use log/exp gathers (L2-resident tables).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <mutex>
+#include <vector>
+
+#include "gf16_host.hpp"
+#include "kernels.hpp"
+#include "sha256.hpp"
+
+namespace dagpu {
+
+namespace {
+
+constexpr uint32_t kMod = 65535u;
+constexpr int kWideThreads = 512;
+constexpr int kPtabPos = 2 * kMaxK;  // skew positions used by any transform <= 2 kMaxK
+
+struct WideTabs {
+  const uint16_t* log;
+  const uint16_t* exp;
+  const uint32_t* ptab;   // kPtabPos x 16 dwords
+  const uint16_t* wfold;  // folded Walsh weights, n = 2048 .. 2 kMaxK, back to back
+};
+
+__device__ __forceinline__ uint32_t xor3w(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// x ^= y * skew[pos] for 4 symbols (lo / hi byte dwords) with the position's
+// product table t[16] (rs_gf16.hip mul16_add, table from registers)
+__device__ __forceinline__ void pmul_add(uint32_t& xlo, uint32_t& xhi, uint32_t ylo, uint32_t yhi,
+                                         const uint32_t (&t)[16]) {
+  uint32_t pl[8], ph[8];
+#pragma unroll
+  for (int g = 0; g < 4; g++) {
+    const uint32_t sl = (ylo >> (2 * g)) & 0x03030303u;
+    const uint32_t sh = (yhi >> (2 * g)) & 0x03030303u;
+    pl[g] = __builtin_amdgcn_perm(t[g], t[g], sl);
+    ph[g] = __builtin_amdgcn_perm(t[8 + g], t[8 + g], sl);
+    pl[4 + g] = __builtin_amdgcn_perm(t[4 + g], t[4 + g], sh);
+    ph[4 + g] = __builtin_amdgcn_perm(t[12 + g], t[12 + g], sh);
+  }
+  xlo = xor3w(xor3w(xor3w(xlo, pl[0], pl[1]), xor3w(pl[2], pl[3], pl[4]), pl[5]), pl[6], pl[7]);
+  xhi = xor3w(xor3w(xor3w(xhi, ph[0], ph[1]), xor3w(ph[2], ph[3], ph[4]), ph[5]), ph[6], ph[7]);
+}
+
+__device__ __forceinline__ void load_tab(const WideTabs& T, int pos, uint32_t (&t)[16]) {
+  const uint4* p = (const uint4*)(T.ptab + (long)pos * 16);
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint4 v = p[i];
+    t[4 * i] = v.x;
+    t[4 * i + 1] = v.y;
+    t[4 * i + 2] = v.z;
+    t[4 * i + 3] = v.w;
+  }
+}
+
+// mulLog on one 16-bit symbol (leopard.go mulLog): a * exp(lm), 0 stays 0
+__device__ __forceinline__ uint32_t mul_log(const WideTabs& T, uint32_t a, uint32_t lm) {
+  if (a == 0) return 0;
+  uint32_t s = (uint32_t)T.log[a] + lm;
+  s = (s + (s >> 16)) & 0xFFFFu;
+  return T.exp[s];
+}
+
+// 4 symbols of a (lo, hi) dword pair times exp(lm)
+__device__ __forceinline__ void mul4(const WideTabs& T, uint32_t& lo, uint32_t& hi, uint32_t lm) {
+  uint32_t rl = 0, rh = 0;
+#pragma unroll
+  for (int b = 0; b < 4; b++) {
+    const uint32_t s = ((lo >> (8 * b)) & 0xFFu) | (((hi >> (8 * b)) & 0xFFu) << 8);
+    const uint32_t p = mul_log(T, s, lm);
+    rl |= (p & 0xFFu) << (8 * b);
+    rh |= (p >> 8) << (8 * b);
+  }
+  lo = rl;
+  hi = rh;
+}
+
+// LDS planes: lo[e * NGP + g], hi[...] (NG = S / 4 dword groups, NGP = NG + 1
+// for odd element strides, so lanes on different elements spread over banks)
+template <int NG>
+struct Planes {
+  static constexpr int NGP = NG == 1 ? 1 : NG + 1;
+  uint32_t* lo;
+  uint32_t* hi;
+  __device__ __forceinline__ int at(int e, int g) const { return e * NGP + g; }
+};
+
+// One radix-4 (or radix-2) unit: elements e[0..R), dword groups g0 .. g0+G-1.
+template <int NG, int G, int R>
+struct Unit {
+  uint32_t lo[R][G], hi[R][G];
+  __device__ __forceinline__ void load(const Planes<NG>& P, const int (&e)[R], int g0) {
+#pragma unroll
+    for (int r = 0; r < R; r++)
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        lo[r][g] = P.lo[P.at(e[r], g0 + g)];
+        hi[r][g] = P.hi[P.at(e[r], g0 + g)];
+      }
+  }
+  __device__ __forceinline__ void store(const Planes<NG>& P, const int (&e)[R], int g0) const {
+#pragma unroll
+    for (int r = 0; r < R; r++)
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        P.lo[P.at(e[r], g0 + g)] = lo[r][g];
+        P.hi[P.at(e[r], g0 + g)] = hi[r][g];
+      }
+  }
+  // ifftDIT2: y ^= x; x ^= y * skew
+  __device__ __forceinline__ void ifft2(int i, int j, const uint32_t (&t)[16]) {
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      lo[j][g] ^= lo[i][g];
+      hi[j][g] ^= hi[i][g];
+      pmul_add(lo[i][g], hi[i][g], lo[j][g], hi[j][g], t);
+    }
+  }
+  // fftDIT2: x ^= y * skew; y ^= x
+  __device__ __forceinline__ void fft2(int i, int j, const uint32_t (&t)[16]) {
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      pmul_add(lo[i][g], hi[i][g], lo[j][g], hi[j][g], t);
+      lo[j][g] ^= lo[i][g];
+      hi[j][g] ^= hi[i][g];
+    }
+  }
+};
+
+// ifftDITEncoder / ifftDITDecoder over n elements (mtrunc = n), skew index
+// base + iend (encoder: base = IO - 1; decoder: -1)
+template <int NG, int G>
+__device__ void wide_ifft(const Planes<NG>& P, const WideTabs& T, int n, int base) {
+  constexpr int CH = NG / G;
+  int dist = 1, dist4 = 4;
+  uint32_t t[16];
+  while (dist4 <= n) {
+    const int units = (n / 4) * CH;
+    for (int u = threadIdx.x; u < units; u += kWideThreads) {
+      const int quad = u / CH, g0 = (u - quad * CH) * G;
+      const int r = (quad / dist) * dist4, i = r + (quad % dist), iend = r + dist;
+      const int e[4] = {i, i + dist, i + 2 * dist, i + 3 * dist};
+      Unit<NG, G, 4> x;
+      x.load(P, e, g0);
+      load_tab(T, base + iend, t);
+      x.ifft2(0, 1, t);
+      load_tab(T, base + iend + 2 * dist, t);
+      x.ifft2(2, 3, t);
+      load_tab(T, base + iend + dist, t);
+      x.ifft2(0, 2, t);
+      x.ifft2(1, 3, t);
+      x.store(P, e, g0);
+    }
+    __syncthreads();
+    dist = dist4;
+    dist4 <<= 2;
+  }
+  if (dist < n) {  // one radix-2 layer left (log2 n odd)
+    const int units = (n / 2) * CH;
+    load_tab(T, base + dist, t);
+    for (int u = threadIdx.x; u < units; u += kWideThreads) {
+      const int p = u / CH, g0 = (u - p * CH) * G;
+      const int e[2] = {p, p + dist};
+      Unit<NG, G, 2> x;
+      x.load(P, e, g0);
+      x.ifft2(0, 1, t);
+      x.store(P, e, g0);
+    }
+    __syncthreads();
+  }
+}
+
+// fftDIT over n elements (mtrunc = n), skew index fo + iend - 1
+template <int NG, int G>
+__device__ void wide_fft(const Planes<NG>& P, const WideTabs& T, int n, int fo) {
+  constexpr int CH = NG / G;
+  int dist4 = n, dist = n >> 2;
+  uint32_t t[16];
+  while (dist != 0) {
+    const int units = (n / 4) * CH;
+    for (int u = threadIdx.x; u < units; u += kWideThreads) {
+      const int quad = u / CH, g0 = (u - quad * CH) * G;
+      const int r = (quad / dist) * dist4, i = r + (quad % dist), iend = r + dist;
+      const int e[4] = {i, i + dist, i + 2 * dist, i + 3 * dist};
+      Unit<NG, G, 4> x;
+      x.load(P, e, g0);
+      load_tab(T, fo + iend + dist - 1, t);
+      x.fft2(0, 2, t);
+      x.fft2(1, 3, t);
+      load_tab(T, fo + iend - 1, t);
+      x.fft2(0, 1, t);
+      load_tab(T, fo + iend + 2 * dist - 1, t);
+      x.fft2(2, 3, t);
+      x.store(P, e, g0);
+    }
+    __syncthreads();
+    dist4 = dist;
+    dist >>= 2;
+  }
+  if (dist4 == 2) {
+    const int units = (n / 2) * CH;
+    for (int u = threadIdx.x; u < units; u += kWideThreads) {
+      const int p = u / CH, g0 = (u - p * CH) * G;
+      const int e[2] = {2 * p, 2 * p + 1};
+      load_tab(T, fo + 2 * p, t);
+      Unit<NG, G, 2> x;
+      x.load(P, e, g0);
+      x.fft2(0, 1, t);
+      x.store(P, e, g0);
+    }
+    __syncthreads();
+  }
+}
+
+// Column slice of a workgroup: blockIdx -> (vector v, 64-B block, slice of
+// S = 4 NG symbols).  Consecutive logical blocks (the slices and blocks of one
+// vector, which share cache lines) are kept on one XCD: hardware dispatch
+// deals workgroups round-robin over the 8 XCDs.
+struct SliceCoord {
+  long v, blk;
+  int sl;
+};
+template <int NG>
+__device__ __forceinline__ SliceCoord slice_of(long nblk) {
+  constexpr int nsl = 8 / NG;
+  long b = blockIdx.x;
+  const long G = gridDim.x;
+  if ((G & 7) == 0) b = (b & 7) * (G >> 3) + (b >> 3);
+  SliceCoord c;
+  c.sl = (int)(b % nsl);
+  b /= nsl;
+  c.blk = b % nblk;
+  c.v = b / nblk;
+  return c;
+}
+
+// ---------------------------------------------------------------------------
+// Encode: parity = FFT_m(IFFT_m(data)), m = k.  EncodeArgs semantics as the
+// other encoders: Q0 placement copy, compare mode (mismatch), Repair fill
+// (out_present / redo), reverse fill (IFFT at skew offset 0, FFT at m).
+// ---------------------------------------------------------------------------
+template <int NG, int G>
+__global__ __launch_bounds__(kWideThreads) void leo16w_encode_kernel(EncodeArgs a, WideTabs T, int k) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  Planes<NG> P{lds, lds + k * Planes<NG>::NGP};
+  const SliceCoord c = slice_of<NG>(a.shard_bytes / 64);
+  const long sq = c.v / a.nvec, vec = c.v % a.nvec;
+  if (vec_skipped(a, c.v)) return;  // uniform
+  const long col = c.blk * 64 + (long)c.sl * 4 * NG;  // byte of lo dword 0 of this slice
+  const uint8_t* in = a.in + sq * a.in_sq_stride + vec * a.in_vec_stride + col;
+  uint8_t* cp = a.copy ? a.copy + sq * a.copy_sq_stride + vec * a.copy_vec_stride + col : nullptr;
+  for (int t = threadIdx.x; t < k * NG; t += kWideThreads) {
+    const int e = t / NG, g = t - e * NG;
+    const uint32_t* src = (const uint32_t*)(in + (long)e * a.in_shard_stride) + g;
+    const uint32_t lo = src[0], hi = src[8];
+    P.lo[P.at(e, g)] = lo;
+    P.hi[P.at(e, g)] = hi;
+    if (cp) {
+      uint32_t* dst = (uint32_t*)(cp + (long)e * a.copy_shard_stride) + g;
+      dst[0] = lo;
+      dst[8] = hi;
+    }
+  }
+  __syncthreads();
+  wide_ifft<NG, G>(P, T, k, a.reverse ? -1 : k - 1);
+  wide_fft<NG, G>(P, T, k, a.reverse ? k : 0);
+  uint8_t* out = a.out + sq * a.out_sq_stride + vec * a.out_vec_stride + col;
+  bool diff = false;
+  for (int t = threadIdx.x; t < k * NG; t += kWideThreads) {
+    const int e = t / NG, g = t - e * NG;
+    const uint32_t lo = P.lo[P.at(e, g)], hi = P.hi[P.at(e, g)];
+    uint32_t* dst = (uint32_t*)(out + (long)e * a.out_shard_stride) + g;
+    if (a.mismatch || (a.out_present && fill_given(a, sq, vec, e))) {
+      diff |= (dst[0] != lo) || (dst[8] != hi);
+    } else {
+      dst[0] = lo;
+      dst[8] = hi;
+    }
+  }
+  if (a.mismatch && diff) {
+    atomicOr(a.mismatch + sq, a.mismatch_bit);
+    if (a.mismatch_vec) a.mismatch_vec[sq * a.nvec + vec] = 1;
+  }
+  if (a.out_present && !a.mismatch && diff) a.redo[c.v] = 1;  // Repair fill: a given shard differs
+}
+
+// ---------------------------------------------------------------------------
+// Error locators (leopard.go reconstruct, first part) from n-point transforms:
+// FWHT_n(FWHT_n(e) * wfold), wfold[r] = sum_q logWalsh[q n + r] mod 65535
+// (see rs_gf16.hip leo16_errlocs_fold_kernel; n = 2k up to 2 kMaxK here).
+// ---------------------------------------------------------------------------
+constexpr int kFoldThreads = 512;
+
+__device__ __forceinline__ uint32_t add_mod(uint32_t a, uint32_t b) {
+  const uint32_t s = a + b;
+  return (s + (s >> 16)) & 0xFFFFu;
+}
+__device__ __forceinline__ uint32_t sub_mod(uint32_t a, uint32_t b) {
+  const uint32_t d = a - b;
+  return (d + (d >> 16)) & 0xFFFFu;
+}
+
+__device__ void fwht_rt(uint32_t* e, int n) {
+  int dist = 1;
+  if ((__builtin_ctz(n) & 1) != 0) {  // odd log2: one radix-2 stage first
+    for (int g = threadIdx.x; g < n / 2; g += kFoldThreads) {
+      const int i = 2 * g;
+      const uint32_t t0 = e[i], t1 = e[i + 1];
+      e[i] = add_mod(t0, t1);
+      e[i + 1] = sub_mod(t0, t1);
+    }
+    __syncthreads();
+    dist = 2;
+  }
+  for (; dist < n; dist <<= 2) {
+    const int dist4 = dist << 2;
+    for (int g = threadIdx.x; g < n / 4; g += kFoldThreads) {
+      const int r = (g / dist) * dist4;
+      const int i = r + (g % dist);
+      const uint32_t t0 = e[i], t1 = e[i + dist], t2 = e[i + 2 * dist], t3 = e[i + 3 * dist];
+      const uint32_t a0 = add_mod(t0, t1), a1 = sub_mod(t0, t1);
+      const uint32_t a2 = add_mod(t2, t3), a3 = sub_mod(t2, t3);
+      e[i] = add_mod(a0, a2);
+      e[i + 2 * dist] = sub_mod(a0, a2);
+      e[i + dist] = add_mod(a1, a3);
+      e[i + 3 * dist] = sub_mod(a1, a3);
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kFoldThreads) void leo16w_errlocs_kernel(DecodeArgs a, WideTabs T, long wf_off) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t e[];
+  __shared__ int cnt_s;
+  const long v = blockIdx.x;
+  const long sq = v / a.nvec, vec = v % a.nvec;
+  const int k = a.k, n = 2 * k;
+  const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
+  if (a.locators_only && (!a.flags[v] || !err_computes(a, v, err_vec(a, v)))) return;  // uniform
+  if (threadIdx.x == 0) cnt_s = 0;
+  __syncthreads();
+  int cnt = 0;
+  for (int i = threadIdx.x; i < n; i += kFoldThreads) {
+    const uint32_t x = i < k ? (pres[(long)(k + i) * a.p_shard_stride] ? 0u : 1u)   // parity k+i -> work i
+                             : (pres[(long)(i - k) * a.p_shard_stride] ? 0u : 1u);  // data i-k -> work i
+    e[i] = x;
+    cnt += (x == 0);
+  }
+  atomicAdd(&cnt_s, cnt);
+  __syncthreads();
+  const int present = cnt_s;
+  bool decode = true;
+  if (!a.locators_only) {
+    decode = present >= k && present < n && vec_selected(a, v);
+    if (threadIdx.x == 0) {
+      a.flags[v] = decode ? 1 : 0;
+      if (present < k && a.too_few) atomicOr(a.too_few, 1);
+      if (decode && a.ndecodable) atomicAdd(a.ndecodable, 1);
+    }
+  }
+  if (!decode) return;  // uniform
+  const long hv = err_vec(a, v);
+  if (!err_computes(a, v, hv)) return;  // shares an earlier vector's locators
+  fwht_rt(e, n);
+  const uint16_t* wf = T.wfold + wf_off;
+  for (int i = threadIdx.x; i < n; i += kFoldThreads) e[i] = (e[i] * (uint32_t)wf[i]) % kMod;
+  __syncthreads();
+  fwht_rt(e, n);
+  uint16_t* out = (uint16_t*)(a.err + hv * (long)rs_err_bytes(k));
+  for (int i = threadIdx.x; i < n; i += kFoldThreads) out[i] = (uint16_t)e[i];
+}
+
+// ---------------------------------------------------------------------------
+// Decode: work[i] = shard(pos(i)) * errLocs[i] (0 where missing; layout
+// [parity k][data k]) -> ifftDITDecoder -> formal derivative -> fftDIT ->
+// erased shard = work[pos] * (65535 - errLocs[pos]).
+// The formal derivative D(x)_e = x_e ^ XOR_{b: bit b of e == 0} x_{e + 2^b}
+// (the closed form of leopard.go's in-place loop) runs in place: it only reads
+// elements above e, so element chunks are processed in ascending order, each
+// reading before a barrier and writing after it.
+// ---------------------------------------------------------------------------
+template <int NG, int G>
+__global__ __launch_bounds__(kWideThreads) void leo16w_decode_kernel(DecodeArgs a, WideTabs T) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  constexpr int CH = NG / G;
+  const int k = a.k, n = 2 * k;
+  Planes<NG> P{lds, lds + n * Planes<NG>::NGP};
+  const SliceCoord c = slice_of<NG>(a.shard_bytes / 64);
+  const long v = c.v;
+  if (a.flags[v] == 0) return;  // uniform
+  const long sq = v / a.nvec, vec = v % a.nvec;
+  const long col = c.blk * 64 + (long)c.sl * 4 * NG;
+  uint8_t* base = a.data + sq * a.sq_stride + vec * a.vec_stride + col;
+  const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
+  const uint16_t* err = (const uint16_t*)(a.err + err_vec(a, v) * (long)rs_err_bytes(k));
+  for (int t = threadIdx.x; t < n * NG; t += kWideThreads) {
+    const int i = t / NG, g = t - i * NG;
+    const long shard = i < k ? k + i : i - k;
+    uint32_t lo = 0, hi = 0;
+    if (pres[shard * a.p_shard_stride]) {
+      const uint32_t* src = (const uint32_t*)(base + shard * a.shard_stride) + g;
+      lo = src[0];
+      hi = src[8];
+      mul4(T, lo, hi, err[i]);
+    }
+    P.lo[P.at(i, g)] = lo;
+    P.hi[P.at(i, g)] = hi;
+  }
+  __syncthreads();
+  wide_ifft<NG, G>(P, T, n, -1);
+  {  // formal derivative, ascending chunks of X elements
+    constexpr int X = kWideThreads / CH;
+    for (int x0 = 0; x0 < n; x0 += X) {
+      const int u = threadIdx.x;
+      const int x = x0 + u / CH, g0 = (u % CH) * G;
+      uint32_t dl[G], dh[G];
+      const bool act = x < n;
+      if (act) {
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+          dl[g] = P.lo[P.at(x, g0 + g)];
+          dh[g] = P.hi[P.at(x, g0 + g)];
+        }
+        for (int b = 1; b < n; b <<= 1) {
+          if (x & b) continue;
+#pragma unroll
+          for (int g = 0; g < G; g++) {
+            dl[g] ^= P.lo[P.at(x + b, g0 + g)];
+            dh[g] ^= P.hi[P.at(x + b, g0 + g)];
+          }
+        }
+      }
+      __syncthreads();
+      if (act) {
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+          P.lo[P.at(x, g0 + g)] = dl[g];
+          P.hi[P.at(x, g0 + g)] = dh[g];
+        }
+      }
+      __syncthreads();
+    }
+  }
+  wide_fft<NG, G>(P, T, n, 0);
+  for (int t = threadIdx.x; t < n * NG; t += kWideThreads) {
+    const int i = t / NG, g = t - i * NG;
+    const long shard = i < k ? k + i : i - k;
+    if (pres[shard * a.p_shard_stride]) continue;
+    uint32_t lo = P.lo[P.at(i, g)], hi = P.hi[P.at(i, g)];
+    mul4(T, lo, hi, kMod - err[i]);
+    uint32_t* dst = (uint32_t*)(base + shard * a.shard_stride) + g;
+    dst[0] = lo;
+    dst[8] = hi;
+  }
+}
+
+__global__ __launch_bounds__(256) void leo16w_mark_present_kernel(DecodeArgs a) {
+  const long v = blockIdx.x;
+  if (a.flags[v] == 0) return;
+  const long sq = v / a.nvec, vec = v % a.nvec;
+  uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
+  for (int i = threadIdx.x; i < 2 * a.k; i += 256) pres[(long)i * a.p_shard_stride] = 1;
+  if (threadIdx.x == 0 && a.progress) atomicAdd(a.progress, 1);
+}
+
+// ---------------------------------------------------------------------------
+// Tables: one device copy per device, built on the host from gf16::make_tables.
+// ---------------------------------------------------------------------------
+std::mutex g_mu;
+WideTabs g_tabs[64];
+bool g_done[64];
+
+long wfold_offset(int n) {  // n = 2048, 4096, ...: offsets of the folded tables
+  long off = 0;
+  for (int m = 2048; m < n; m <<= 1) off += m;
+  return off;
+}
+
+hipError_t tables(WideTabs& out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+  std::lock_guard<std::mutex> g(g_mu);
+  if (g_done[dev]) {
+    out = g_tabs[dev];
+    return hipSuccess;
+  }
+  static const gf16::Tables t = gf16::make_tables();
+  std::vector<uint32_t> pt((size_t)kPtabPos * 16, 0u);
+  for (int pos = 0; pos < kPtabPos; pos++) {
+    const unsigned lm = t.skew[pos];
+    if (lm == kMod) continue;  // leopard skips the multiply: zero table
+    for (int g = 0; g < 8; g++)
+      for (int e2 = 0; e2 < 4; e2++) {
+        const unsigned x = (unsigned)e2 << (2 * g);
+        unsigned prod = 0;
+        if (x) {
+          unsigned s = (unsigned)t.log[x] + lm;
+          s = (s + (s >> 16)) & 0xFFFFu;
+          prod = t.exp[s];
+        }
+        const int lo_idx = g, hi_idx = 8 + g;  // (g < 4: low-byte groups, g >= 4: high-byte groups)
+        pt[(size_t)pos * 16 + lo_idx] |= (prod & 0xFFu) << (8 * e2);
+        pt[(size_t)pos * 16 + hi_idx] |= ((prod >> 8) & 0xFFu) << (8 * e2);
+      }
+  }
+  std::vector<uint16_t> wf((size_t)wfold_offset(2 * 2 * kMaxK), 0);
+  for (int n = 2048; n <= 2 * kMaxK; n <<= 1) {
+    const long off = wfold_offset(n);
+    for (int r = 0; r < n; r++) {
+      uint64_t acc = 0;
+      for (int q = 0; q < 65536 / n; q++) acc += t.walsh[(size_t)q * n + r];
+      wf[(size_t)(off + r)] = (uint16_t)(acc % kMod);
+    }
+  }
+  void *d_log = nullptr, *d_exp = nullptr, *d_pt = nullptr, *d_wf = nullptr;
+  if ((e = hipMalloc(&d_log, 65536 * 2)) != hipSuccess) return e;
+  if ((e = hipMalloc(&d_exp, 65536 * 2)) != hipSuccess) return e;
+  if ((e = hipMalloc(&d_pt, pt.size() * 4)) != hipSuccess) return e;
+  if ((e = hipMalloc(&d_wf, wf.size() * 2)) != hipSuccess) return e;
+  if ((e = hipMemcpy(d_log, t.log.data(), 65536 * 2, hipMemcpyHostToDevice)) != hipSuccess) return e;
+  if ((e = hipMemcpy(d_exp, t.exp.data(), 65536 * 2, hipMemcpyHostToDevice)) != hipSuccess) return e;
+  if ((e = hipMemcpy(d_pt, pt.data(), pt.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return e;
+  if ((e = hipMemcpy(d_wf, wf.data(), wf.size() * 2, hipMemcpyHostToDevice)) != hipSuccess) return e;
+  g_tabs[dev] = WideTabs{(const uint16_t*)d_log, (const uint16_t*)d_exp, (const uint32_t*)d_pt,
+                         (const uint16_t*)d_wf};
+  g_done[dev] = true;
+  out = g_tabs[dev];
+  return hipSuccess;
+}
+
+// Slice width per element count: S = 4 NG symbols, LDS = 2 planes x n x (NG + 1)
+// dwords <= 144 KiB (n <= 2048: 32 symbols; 4096: 8; 8192: 4 (64 KiB); 16384: 4 (128 KiB)).
+int slice_ng(int n) { return n <= 2048 ? 8 : n <= 4096 ? 2 : 1; }
+
+size_t lds_bytes(int n, int ng) { return (size_t)2 * n * (ng == 1 ? 1 : ng + 1) * sizeof(uint32_t); }
+
+template <class K>
+hipError_t lds_attr(K kernel, size_t bytes) {
+  return bytes > 65536 ? hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)bytes)
+                       : hipSuccess;
+}
+
+template <int NG, int G>
+hipError_t launch_enc(const EncodeArgs& a, const WideTabs& T, int k, hipStream_t s) {
+  const size_t lds = lds_bytes(k, NG);
+  hipError_t e = lds_attr(leo16w_encode_kernel<NG, G>, lds);
+  if (e != hipSuccess) return e;
+  const long blocks = a.nsq * a.nvec * (a.shard_bytes / 64) * (8 / NG);
+  if (blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL((leo16w_encode_kernel<NG, G>), dim3((unsigned)blocks), dim3(kWideThreads), lds, s, a, T, k);
+  return hipGetLastError();
+}
+
+template <int NG, int G>
+hipError_t launch_dec(const DecodeArgs& a, const WideTabs& T, hipStream_t s) {
+  const int n = 2 * a.k;
+  const size_t lds = lds_bytes(n, NG);
+  hipError_t e = lds_attr(leo16w_decode_kernel<NG, G>, lds);
+  if (e != hipSuccess) return e;
+  const long blocks = a.nsq * a.nvec * (a.shard_bytes / 64) * (8 / NG);
+  if (blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL((leo16w_decode_kernel<NG, G>), dim3((unsigned)blocks), dim3(kWideThreads), lds, s, a, T);
+  return hipGetLastError();
+}
+
+bool wide_k_ok(int k) { return k >= 256 && k <= kMaxK && (k & (k - 1)) == 0; }
+
+}  // namespace
+
+hipError_t launch_leo16w_encode(int k, const EncodeArgs& a, hipStream_t s) {
+  if (!wide_k_ok(k) || a.shard_bytes % 64) return hipErrorInvalidValue;
+  if (a.reverse && !a.out_present) return hipErrorInvalidValue;
+  WideTabs T;
+  hipError_t e = tables(T);
+  if (e != hipSuccess) return e;
+  switch (slice_ng(k)) {
+    case 8: return launch_enc<8, 4>(a, T, k, s);
+    case 2: return launch_enc<2, 2>(a, T, k, s);
+    default: return launch_enc<1, 1>(a, T, k, s);
+  }
+}
+
+hipError_t launch_leo16w_errlocs(const DecodeArgs& a, hipStream_t s) {
+  if (!wide_k_ok(a.k) || a.k < 1024) return hipErrorInvalidValue;
+  WideTabs T;
+  hipError_t e = tables(T);
+  if (e != hipSuccess) return e;
+  const long nv = a.nsq * a.nvec;
+  if (nv <= 0) return hipSuccess;
+  const int n = 2 * a.k;
+  const size_t lds = (size_t)n * 4;
+  if ((e = lds_attr(leo16w_errlocs_kernel, lds)) != hipSuccess) return e;
+  hipLaunchKernelGGL(leo16w_errlocs_kernel, dim3((unsigned)nv), dim3(kFoldThreads), lds, s, a, T, wfold_offset(n));
+  return hipGetLastError();
+}
+
+hipError_t launch_leo16w_decode_only(const DecodeArgs& a, hipStream_t s, bool mark_present) {
+  if (!wide_k_ok(a.k) || a.shard_bytes % 64) return hipErrorInvalidValue;
+  WideTabs T;
+  hipError_t e = tables(T);
+  if (e != hipSuccess) return e;
+  const long nv = a.nsq * a.nvec;
+  if (nv <= 0) return hipSuccess;
+  switch (slice_ng(2 * a.k)) {
+    case 8: e = launch_dec<8, 4>(a, T, s); break;
+    case 2: e = launch_dec<2, 2>(a, T, s); break;
+    default: e = launch_dec<1, 1>(a, T, s); break;
+  }
+  if (e != hipSuccess) return e;
+  if (mark_present) {
+    hipLaunchKernelGGL(leo16w_mark_present_kernel, dim3((unsigned)nv), dim3(256), 0, s, a);
+    e = hipGetLastError();
+  }
+  return e;
+}
+
+}  // namespace dagpu

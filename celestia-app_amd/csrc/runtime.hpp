@@ -115,6 +115,8 @@ struct dagpu_ctx {
   std::vector<ProfRec> pending;
   std::vector<hipEvent_t> pool;
   double prof_ms[DAGPU_PROFILE_KERNELS] = {};
+  // the last Repair call's schedule (dagpu_repair_stats), under prof_mu
+  int64_t rep_stats[DAGPU_REPAIR_STATS] = {};
   uint64_t prof_n[DAGPU_PROFILE_KERNELS] = {};
 };
 

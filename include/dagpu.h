@@ -62,6 +62,16 @@ typedef struct dagpu_ctx dagpu_ctx;
 /* Library version (major*10000 + minor*100 + patch). */
 int dagpu_version(void);
 
+/* Widest square (and codec width k = data shards per vector) this build
+ * serves: DAGPU_MAX_SQUARE_WIDTH.  pkg/da ExtendShares (data_availability_header.go:65-75)
+ * checks only that the share count is a power of two, and rsmt2d's LeoRSCodec
+ * reports MaxChunks() = 32768 * 32768 (Leopard GF(2^16): 65536 shards); the EDS
+ * of k = 8192 is 128 GiB, which fits one MI355X's 288 GB of HBM, and k = 16384
+ * (512 GiB) does not, so every entry point returns DAGPU_ERR_UNSUPPORTED above
+ * it.  A cgo LeoRSCodec.MaxChunks() over this library returns the square of it. */
+#define DAGPU_MAX_SQUARE_WIDTH 8192
+uint32_t dagpu_max_square_width(void);
+
 /* Open a context on HIP device `device` (one context per GPU per process). */
 int dagpu_init(int device, dagpu_ctx** out);
 void dagpu_destroy(dagpu_ctx* ctx);
@@ -156,7 +166,11 @@ int dagpu_repair(dagpu_ctx* ctx, uint32_t k, uint8_t* eds, uint8_t* present,
  * On DAGPU_ERR_BYZANTINE, present[] is left as rsmt2d leaves the square: the
  * cells filled by the attempts before the failing one (their bytes in eds are
  * the committed ones); ErrByzantineData.Shares = the cells of the rebuilt axis
- * with present[] set.  Replaces ExtendedDataSquare.Repair (rsmt2d v0.11.0). */
+ * with present[] set.  A prerepairSanityCheck failure (DAGPU_ERR_BAD_ROOTS, or
+ * DAGPU_ERR_BYZANTINE from the check) returns before rsmt2d's crossword:
+ * present[] is the input's.  The bytes of cells whose present[] flag is 0 are
+ * unspecified (rsmt2d holds nil there).  Replaces ExtendedDataSquare.Repair
+ * (rsmt2d v0.11.0). */
 int dagpu_repair_ex(dagpu_ctx* ctx, uint32_t k, uint8_t* eds, uint8_t* present,
                     const uint8_t* row_roots, const uint8_t* col_roots, int32_t* byz);
 
@@ -211,6 +225,14 @@ int dagpu_profile_read(dagpu_ctx* ctx, double* total_ms, uint64_t* launches, int
 #define DAGPU_STAGE_EDS_TOP 8    /* [Q0|Q1] halves downloaded (copy stream) */
 #define DAGPU_STAGE_EDS_BOTTOM 9 /* [Q2|Q3] halves downloaded (copy stream) */
 int dagpu_profile_stages(dagpu_ctx* ctx, float* ms);
+
+/* Schedule of the last Repair on this context (diagnostics): out[0] crossword
+ * rounds that rebuilt something, out[1] vectors re-encoded from a complete data
+ * half (fill), out[2] vectors rebuilt from a complete parity half (reverse
+ * fill), out[3] vectors planned for the decoder, out[4] decodes deferred to the
+ * other axis.  All zero with DAGPU_REPAIR_FILL=0 except out[0]. */
+#define DAGPU_REPAIR_STATS 5
+int dagpu_repair_stats(dagpu_ctx* ctx, int64_t* out);
 
 /* RFC-6962 root of rowRoots || colRoots (DataAvailabilityHeader.Hash,
  * pkg/da/data_availability_header.go:92-108), computed on the host side of the

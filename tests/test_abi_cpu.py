@@ -93,3 +93,22 @@ def test_min_shares_is_tail_padding():
     assert len(s) == 1 and len(s[0]) == 512
     assert s[0][:29] == b"\xff" * 28 + b"\xfe" and s[0][29] == 1
     assert bytes(synth.tail_padding_square(1)[0]) == s[0]
+
+
+def test_max_square_width_and_codec_limits():
+    # the widest square the library serves: (2k)^2 x 512 B of EDS must fit one
+    # GPU's 288 GB (k = 8192: 128 GiB; k = 16384: 512 GiB)
+    L = _abi.lib()
+    text = open(HEADER).read()
+    m = re.search(r"#define DAGPU_MAX_SQUARE_WIDTH (\d+)", text)
+    assert m and int(m.group(1)) == L.dagpu_max_square_width() == 8192
+    codec = da.LeoRSCodec()
+    assert codec.max_chunks() == 8192 * 8192
+    assert codec.name() == "Leopard"
+
+
+def test_codec_decode_without_any_shard_is_too_few():
+    # reedsolomon Reconstruct with every shard nil -> ErrTooFewShards (no GPU
+    # call is reached: the shard size cannot even be known)
+    with pytest.raises(da.ErrTooFewShards):
+        da.LeoRSCodec().decode([None] * 8)

@@ -60,6 +60,8 @@ def _check_one(ctx, k, eds, bad, pres, rr, cr, what):
     axis = ("row", "col")[byz[0]]
     if rc == _abi.ERR_BAD_ROOTS:
         assert msg.startswith(f"bad root input: {axis} {byz[1]} expected ["), (what, msg)
+        # rsmt2d returns before the crossword: presence is the input's
+        assert (p == pres).all() and (opres.astype(bool) == pres).all(), what
         return "bad-roots"
     assert msg == f"byzantine {axis}: {byz[1]}", (what, msg)
     # the square as rsmt2d leaves it: cells of the attempts before the failing one
@@ -137,9 +139,20 @@ def test_precheck_order(ctx):
     irr2, icr2 = oracle.compute_roots(inc2, k)
     wrong_r = irr2.copy()
     wrong_r[5, 80] ^= 1
-    rc, _, _, byz, _ = _gpu_repair(ctx, inc2, pres, wrong_r, icr2)
-    orc, _, _, obyz = oracle.repair_ex(inc2, pres, k, wrong_r, icr2)
+    rc, _, p, byz, _ = _gpu_repair(ctx, inc2, pres, wrong_r, icr2)
+    orc, _, opres, obyz = oracle.repair_ex(inc2, pres, k, wrong_r, icr2)
     assert rc == orc == _abi.ERR_BYZANTINE and byz == obyz == [1, 2, 1, 2]
+    # a pre-repair failure leaves the square as given (rsmt2d never reaches
+    # solveCrossword): the missing cell stays missing
+    assert (p == pres).all() and (opres.astype(bool) == pres).all()
+    # (c) the same with a decodable gap pattern: many missing cells, presence untouched
+    pres3 = np.ones((w, w), bool)
+    pres3[6, [0, 1, 3]] = False       # gaps off row 5 and column 2 (both still complete)
+    pres3[:2, 7] = False
+    rc, _, p, byz, _ = _gpu_repair(ctx, inc2 * pres3[:, :, None], pres3, irr2, icr2)
+    orc, _, opres, obyz = oracle.repair_ex(inc2 * pres3[:, :, None], pres3, k, irr2, icr2)
+    assert rc == orc == _abi.ERR_BYZANTINE and byz == obyz == [1, 2, 1, 2]
+    assert (p == pres3).all() and (opres.astype(bool) == pres3).all()
 
 
 def test_k128_byzantine_matches_oracle(ctx):

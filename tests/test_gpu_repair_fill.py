@@ -259,3 +259,28 @@ def test_two_threads_repair_one_context(ctx):
         assert torch.equal(ds.eds, ref) and bool((present == 1).all()), name
     del sets
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("k", [8, 16])
+def test_fill_classification_mixed_halves(ctx, k):
+    """The plan's classification itself (dagpu_repair_stats), not just the
+    bytes: even rows keep k/2 data + k/2 parity shards (decoder), odd rows
+    their parity half (reverse fill).  At k = 8 the row counter's 16-flag loads
+    would straddle index k and count parity flags as data, sending the mixed
+    rows to the forward fill; the counts must be the same at both
+    k.  Round 1 (rows): k reverse fills, k/2 decodes of rows < k, k/2 deferred
+    decodes of rows >= k; round 2 (columns): the k columns that are not already
+    complete are re-encoded from their complete data half."""
+    w = 2 * k
+    eds, rr, cr, _ = oracle.extend_and_dah(synth.random_blob_square(k, 808 + k), k)
+    p = np.zeros((w, w), bool)
+    h = k // 2
+    for r in range(w):
+        if r % 2 == 0:
+            p[r, :h] = True
+            p[r, k:k + h] = True
+        else:
+            p[r, k:] = True
+    fixed, pres = da.repair(eds * p[:, :, None], p, rr, cr, ctx)
+    assert pres.all() and (fixed == eds).all()
+    assert ctx.repair_stats() == {"rounds": 2, "fills": k, "reverse_fills": k, "decodes": h, "deferred": h}

@@ -1,0 +1,188 @@
+"""Squares and codec vectors wider than k = 512 (k = 1024 ... 8192): the
+LDS-slice GF(2^16) kernels of csrc/rs_gf16_wide.hip, the chunked DAH kernel
+and the width-generic Repair helpers.
+
+pkg/da/data_availability_header.go:65-75 (ExtendShares) checks only that the
+share count is a power of two, and rsmt2d's LeoRSCodec serves any width up to
+Leopard's 65536 shards, so these widths give a result in the reference, not
+an error.  Parity unpinned (no reference vector above k = 128): bit-for-bit
+against the oracle's GF(2^16) restatement where the oracle finishes in
+seconds (codec vectors at 64-B shards up to k = 8192, the whole k = 1024
+square), and through size-independent properties at k = 2048 (sampled
+vectors and roots against the oracle, the Q3 identity, erase/decode round
+trips, the DAH recomputed from the roots).  The wide kernels are also run at
+k = 256 / 512 (DAGPU_GF16_WIDE=1) against the register-resident ones."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from celestia_da import _abi, da, synth
+from celestia_da.device import DeviceSquares
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = da.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("k", [1024, 2048, 4096, 8192])
+def test_wide_encode_matches_oracle(ctx, k):
+    # one slice width per element count: n = k elements -> 32 / 32 / 8 / 4 symbols
+    rng = np.random.default_rng(k)
+    shard = 64 if k > 2048 else 128
+    data = rng.integers(0, 256, (2, k, shard), dtype=np.uint8)
+    par = da.LeoRSCodec(ctx).encode_batch(data)
+    for v in range(2):
+        assert (par[v] == oracle.encode(data[v])).all()
+
+
+@pytest.mark.parametrize("k", [1024, 2048, 4096, 8192])
+def test_wide_decode_matches_oracle(ctx, k):
+    # decode transforms n = 2k = 2048 .. 16384 elements (the last at 128 KiB of LDS)
+    rng = np.random.default_rng(k + 1)
+    shard = 64
+    data = rng.integers(0, 256, (k, shard), dtype=np.uint8)
+    full = np.concatenate([data, oracle.encode(data)])
+    codec = da.LeoRSCodec(ctx)
+    pats = [np.isin(np.arange(2 * k), rng.choice(2 * k, k + extra, replace=False)) for extra in (0, 3)]
+    pats += [np.arange(2 * k) >= k, np.arange(2 * k) < k]
+    for j, present in enumerate(pats):
+        present = present.astype(np.uint8)
+        damaged = full * present[:, None]
+        if j == 0:
+            assert (oracle.decode(damaged, present) == full).all()
+        got = codec.decode([damaged[i].tobytes() if present[i] else None for i in range(2 * k)])
+        assert b"".join(got) == full.tobytes()
+
+
+def test_wide_decode_too_few_and_limits(ctx):
+    k = 1024
+    with pytest.raises(da.ErrTooFewShards):
+        da.LeoRSCodec(ctx).decode([bytes(64)] * (k - 1) + [None] * (k + 1))
+    # beyond the widest square this library serves: an explicit error, not a fault
+    big = 2 * _abi.lib().dagpu_max_square_width()
+    d = np.zeros(big * 64, np.uint8)
+    p = np.zeros_like(d)
+    rc = ctx._L.dagpu_encode(ctx.handle, big, 1, 64, _abi.addr(d), _abi.addr(p))
+    assert rc == _abi.ERR_UNSUPPORTED
+
+
+@pytest.mark.parametrize("k", [256, 512])
+def test_wide_kernels_equal_register_kernels(ctx, k, monkeypatch):
+    """The LDS-slice kernels at the widths the register-resident ones serve:
+    encode (plain, 1536-B shards) and decode, byte-equal to the default path
+    and the oracle."""
+    rng = np.random.default_rng(5 * k)
+    data = rng.integers(0, 256, (3, k, 1536), dtype=np.uint8)
+    codec = da.LeoRSCodec(ctx)
+    ref = codec.encode_batch(data)
+    monkeypatch.setenv("DAGPU_GF16_WIDE", "1")
+    got = codec.encode_batch(data)
+    assert (got == ref).all()
+    assert (got[0] == oracle.encode(data[0])).all()
+    full = np.concatenate([data[1], ref[1]])
+    present = np.isin(np.arange(2 * k), rng.choice(2 * k, k + 5, replace=False)).astype(np.uint8)
+    damaged = full * present[:, None]
+    out = codec.decode([damaged[i].tobytes() if present[i] else None for i in range(2 * k)])
+    assert b"".join(out) == full.tobytes()
+
+
+def test_wide_extend_k1024_matches_oracle(ctx):
+    """The whole k = 1024 square: EDS bytes, every row and column root, DAH."""
+    k = 1024
+    ods = synth.blob_squares(k, 1024, 0, 1)[0].reshape(k * k, 512)
+    eds = da.extend_shares(ods, ctx)
+    dah = da.new_data_availability_header(eds)
+    oeds, orr, ocr, odah = oracle.extend_and_dah(ods, k, nthreads=16)
+    assert (eds.data == oeds).all()
+    assert b"".join(dah.row_roots) == orr.tobytes()
+    assert b"".join(dah.column_roots) == ocr.tobytes()
+    assert dah.hash() == odah
+    # the reference ValidateBasic caps a DAH at 256 roots per axis
+    with pytest.raises(da.DAError, match="maximum"):
+        dah.validate_basic()
+
+
+def test_wide_repair_k1024_max_erasure(ctx):
+    """k = 1024 Repair, maximal erasure (a random k x k sub-grid kept): rows
+    and columns decoded by the wide decoder, every root re-verified; then one
+    corrupted surviving share -> ErrByzantineData."""
+    k = 1024
+    w = 2 * k
+    ods = synth.blob_squares(k, 99, 0, 1)[0].reshape(k * k, 512)
+    eds_obj = da.extend_shares(ods, ctx)
+    dah = da.new_data_availability_header(eds_obj)
+    eds = eds_obj.data
+    rng = np.random.default_rng(12)
+    present = np.zeros((w, w), bool)
+    present[np.ix_(rng.choice(w, k, replace=False), rng.choice(w, k, replace=False))] = True
+    fixed, pres = da.repair(eds * present[:, :, None], present, dah.row_roots, dah.column_roots, ctx)
+    assert pres.all()
+    assert (fixed == eds).all()
+    st = ctx.repair_stats()
+    assert st["decodes"] >= k and st["rounds"] >= 2, st
+    bad = eds * present[:, :, None]
+    r, c = np.argwhere(present)[5]
+    bad[r, c, 300] ^= 0x11
+    with pytest.raises(da.ErrByzantineData):
+        da.repair(bad, present, dah.row_roots, dah.column_roots, ctx)
+
+
+def test_wide_k2048_properties(ctx):
+    """k = 2048 (8 GiB EDS, device-resident): sampled rows / columns of every
+    quadrant against the oracle's encoder, the Q3 identity through the codec,
+    sampled roots against the oracle's wrapper tree, the DAH recomputed from
+    the GPU's roots, and erase/decode round trips of sampled vectors."""
+    k = 2048
+    w = 2 * k
+    ds = DeviceSquares(k, 1, ctx=ctx, in_place=True)
+    ods = synth.blob_squares(k, 2048, 0, 1)
+    ds.load_ods(ods)
+    ds.extend()
+    torch.cuda.synchronize()
+    assert int(ds.status[0]) == 0
+    e = ds.eds.view(w, w, 512)
+    rng = np.random.default_rng(2048)
+    q0 = ods.reshape(k, k, 512)
+    for r in rng.choice(k, 2, replace=False):  # Q1 rows = Encode(Q0 rows)
+        assert (e[r, :k].cpu().numpy() == q0[r]).all()
+        assert (e[r, k:].cpu().numpy() == oracle.encode(q0[r])).all()
+    for c in rng.choice(w, 2, replace=False):  # Q2 / Q3 columns = Encode([Q0|Q1] columns)
+        col = e[:, c].cpu().numpy()
+        assert (col[k:] == oracle.encode(np.ascontiguousarray(col[:k]))).all()
+    # Q3 identity: rows of Q2 encode to the rows of Q3 (the column pass built Q3)
+    rows = rng.choice(np.arange(k, w), 8, replace=False)
+    q2 = np.ascontiguousarray(e[rows, :k].cpu().numpy())
+    assert (da.LeoRSCodec(ctx).encode_batch(q2) == e[rows, k:].cpu().numpy()).all()
+    # roots: sampled axes against the oracle, DAH from all roots
+    rr = ds.row_roots[0].cpu().numpy()
+    cr = ds.col_roots[0].cpu().numpy()
+    assert bytes(ds.dah[0].cpu().numpy()) == oracle.dah_hash(rr, cr)
+    for ax, idx in ((0, 0), (0, w - 1), (1, 1), (1, k + 3)):
+        vec = (e[idx] if ax == 0 else e[:, idx]).cpu().numpy()
+        got = (rr if ax == 0 else cr)[idx].tobytes()
+        assert got == _axis_root(vec, idx, k), (ax, idx)
+    # erase / decode round trips of a row and a column
+    codec = da.LeoRSCodec(ctx)
+    for vec in (e[5].cpu().numpy(), e[:, w - 7].cpu().numpy()):
+        keep = set(rng.choice(w, k, replace=False).tolist())
+        out = codec.decode([vec[i].tobytes() if i in keep else None for i in range(w)])
+        assert b"".join(out) == vec.tobytes()
+    del ds
+    torch.cuda.empty_cache()
+
+
+def _axis_root(vec: np.ndarray, idx: int, k: int) -> bytes:
+    """Wrapper tree root of one EDS axis (pkg/wrapper/nmt_wrapper.go:93-124):
+    leaf j keeps its namespace iff j < k and idx < k, else the parity namespace."""
+    leaves = []
+    for j in range(vec.shape[0]):
+        share = vec[j].tobytes()
+        ns = share[:29] if (j < k and idx < k) else b"\xff" * 29
+        leaves.append(oracle.nmt_leaf(ns, share))
+    return oracle.nmt_root(leaves)
