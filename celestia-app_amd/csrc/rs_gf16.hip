@@ -1211,8 +1211,8 @@ hipError_t ensure_tables() {
   if ((e = hipFuncSetAttribute((const void*)leo16_errlocs_kernel,
                                hipFuncAttributeMaxDynamicSharedMemorySize, kErrLds)) != hipSuccess)
     return e;
-  if ((e = hipFuncSetAttribute((const void*)leo16_decode_kernel,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, kMaxK * 256)) != hipSuccess)
+  if ((e = hipFuncSetAttribute((const void*)leo16_decode_kernel,  // k <= 512 here (wider: rs_gf16_wide.hip)
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 512 * 256)) != hipSuccess)
     return e;
   g_tab_done[dev] = true;
   return hipSuccess;
