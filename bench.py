@@ -106,6 +106,46 @@ def all_gather_rows(dist, world, t):
     return allg
 
 
+def per_rank_ms(dist, world, ms: float):
+    """Every rank's own ms per step (its stream drained, before the barrier)."""
+    if dist is None:
+        return [ms]
+    got = [None] * world
+    dist.all_gather_object(got, float(ms))
+    return got
+
+
+def ranks_report(dist, rank_ms, numa_report):
+    """N > 1 context for the bench line: per-rank step times (min / max / all),
+    each rank's GPU, NUMA node and affinity, the collective library and its
+    version, and the GPU-to-GPU links the KFD topology offers (xGMI point to
+    point or PCIe) -- what a first scaling line needs to explain itself."""
+    from celestia_da import numa
+    world = len(rank_ms)
+    placement = [None] * world
+    dist.all_gather_object(placement, numa_report)
+    backend = dist.get_backend()
+    rep = {"backend": backend, "world": world,
+           "step_ms": {"min": min(rank_ms), "max": max(rank_ms), "per_rank": [round(x, 4) for x in rank_ms]},
+           "placement": placement}
+    try:
+        v = torch.cuda.nccl.version()
+        rep["rccl_version"] = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception as e:  # noqa: BLE001 -- report, never fail the bench on it
+        rep["rccl_version"] = f"unavailable ({type(e).__name__})"
+    links = numa.gpu_links()
+    mine = [p.get("pci") for p in placement if p]
+    rep["links"] = {pci: links.get(pci) for pci in dict.fromkeys(mine)}
+    if backend == "gloo":
+        rep["transport"] = "gloo over host memory (DAGPU_BENCH_SHARED_GPU rehearsal, one GPU)"
+    else:
+        peers = [links.get(a, {}).get("xgmi", []) for a in mine]
+        all_xgmi = all(b in peers[i] for i, a in enumerate(mine) for b in mine if b != a) if mine else False
+        rep["transport"] = ("RCCL P2P over xGMI (every rank pair directly linked)" if all_xgmi and len(set(mine)) > 1
+                            else "RCCL (not every rank pair has a direct xGMI link: PCIe / host path)")
+    return rep
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -310,9 +350,11 @@ def main():
     for _ in range(args.steps):
         ds.extend(stream)
     torch.cuda.synchronize()
+    el_own = time.perf_counter() - t0  # this rank's own work (before waiting for the others)
     barrier(dist)
     el = time.perf_counter() - t0
     el_max = max_over_ranks(dist, el, local)
+    rank_ms = per_rank_ms(dist, world, el_own / args.steps * 1e3)
     # the timed batch proves its own output before anything else runs on it
     headline_check = (check_headline(dist, local, ctx, ds, batch_ods) if args.check
                       else {"bit_exact": None, "skipped": "--no-check (profiling run)"})
@@ -430,6 +472,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.cpu_threads or host_threads())
         out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
         out["gpu_over_cpu_core"] = value / out["cpu_baseline"]["per_core_squares_per_s"]
+    if dist is not None:
+        out["ranks"] = ranks_report(dist, rank_ms, numa_report)
     if dist is not None and not args.no_split:
         # configs[4] stress: one oversized square split over all ranks (RCCL all-to-all)
         if "ds" in locals():

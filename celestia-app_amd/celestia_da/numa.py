@@ -66,7 +66,11 @@ def gpu_pci_addresses(sysfs: str = "/sys") -> List[str]:
 
 
 def _visible(addrs: List[str], env) -> Optional[List[str]]:
-    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+    # ROCr filters first; HIP then honours ONE of HIP_VISIBLE_DEVICES /
+    # CUDA_VISIBLE_DEVICES (HIP_ wins when both are set, as launchers often
+    # set both to the same list), indexing the devices ROCr left.
+    hip_var = "HIP_VISIBLE_DEVICES" if env.get("HIP_VISIBLE_DEVICES") else "CUDA_VISIBLE_DEVICES"
+    for var in ("ROCR_VISIBLE_DEVICES", hip_var):
         v = env.get(var)
         if v is None or v == "":
             continue
@@ -78,6 +82,53 @@ def _visible(addrs: List[str], env) -> Optional[List[str]]:
             return None
         addrs = [addrs[i] for i in idx]
     return addrs
+
+
+_LINK_TYPES = {2: "pcie", 11: "xgmi"}  # KFD CRAT io-link types
+
+
+def _props(path: str) -> Dict[str, int]:
+    kv: Dict[str, int] = {}
+    for line in (_read(path) or "").splitlines():
+        f = line.split()
+        if len(f) == 2 and f[1].lstrip("-").isdigit():
+            kv[f[0]] = int(f[1])
+    return kv
+
+
+def gpu_links(sysfs: str = "/sys") -> Dict[str, Dict]:
+    """Direct links between GPU agents from the KFD topology (io_links of each
+    GPU node): {pci: {"xgmi": [peer pci...], "pcie_to_cpu": n, ...}}.  The
+    transport RCCL can use between two ranks' GPUs (xGMI point to point, or
+    PCIe through the host)."""
+    base = os.path.join(sysfs, "class/kfd/kfd/topology/nodes")
+    try:
+        nodes = sorted(int(n) for n in os.listdir(base) if n.isdigit())
+    except OSError:
+        return {}
+    gpu_pci: Dict[int, str] = {}
+    for n in nodes:
+        kv = _props(os.path.join(base, str(n), "properties"))
+        if kv.get("simd_count", 0) > 0:
+            loc, dom = kv.get("location_id", 0), kv.get("domain", 0)
+            gpu_pci[n] = f"{dom:04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 0x7:x}"
+    out: Dict[str, Dict] = {}
+    for n, pci in gpu_pci.items():
+        d: Dict = {"xgmi": [], "pcie_peers": [], "pcie_to_cpu": 0}
+        ldir = os.path.join(base, str(n), "io_links")
+        try:
+            links = sorted(os.listdir(ldir))
+        except OSError:
+            links = []
+        for li in links:
+            kv = _props(os.path.join(ldir, li, "properties"))
+            to, kind = kv.get("node_to", -1), _LINK_TYPES.get(kv.get("type", -1), "other")
+            if to in gpu_pci:
+                (d["xgmi"] if kind == "xgmi" else d["pcie_peers"]).append(gpu_pci[to])
+            elif kind == "pcie":
+                d["pcie_to_cpu"] += 1
+        out[pci] = d
+    return out
 
 
 def gpu_numa(gpu_index: int, sysfs: str = "/sys", env=None) -> Dict:

@@ -34,53 +34,42 @@ namespace {
 size_t eds_bytes(uint64_t k) { return 4ull * k * k * kSS; }
 size_t ods_bytes(uint64_t k) { return 1ull * k * k * kSS; }
 
-// RS row pass over Q0 rows [r0, r1) of n squares: row r -> Q1 (and Q0 copied
-// into place when the ODS is a separate buffer).
-int enqueue_row_pass(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_ods, uint8_t* d_eds, hipStream_t s,
-                     uint32_t r0, uint32_t r1) {
+// RS extension of n squares (uniform k), device pointers.
+// ev_rows (optional) is recorded between the row and the column pass: rows
+// 0..k-1 of every EDS ([Q0|Q1]) are final from that point on.
+int enqueue_rs(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_ods, uint8_t* d_eds,
+               hipStream_t s, hipEvent_t ev_rows = nullptr) {
   const long w = 2L * k;
   const long esq = (long)eds_bytes(k);
   EncodeArgs ra{};
+  // Row pass: vector r = row r of Q0 -> Q1 (and copy Q0 into place).
   if (d_ods) {
-    ra.in = d_ods + (long)r0 * k * kSS;
+    ra.in = d_ods;
     ra.in_sq_stride = (long)ods_bytes(k);
     ra.in_vec_stride = (long)k * kSS;
     ra.in_shard_stride = kSS;
-    ra.copy = d_eds + (long)r0 * w * kSS;
+    ra.copy = d_eds;
     ra.copy_sq_stride = esq;
     ra.copy_vec_stride = w * kSS;
     ra.copy_shard_stride = kSS;
   } else {
-    ra.in = d_eds + (long)r0 * w * kSS;
+    ra.in = d_eds;
     ra.in_sq_stride = esq;
     ra.in_vec_stride = w * kSS;
     ra.in_shard_stride = kSS;
     ra.copy = nullptr;
   }
-  ra.out = d_eds + (long)r0 * w * kSS + (long)k * kSS;
+  ra.out = d_eds + (long)k * kSS;
   ra.out_sq_stride = esq;
   ra.out_vec_stride = w * kSS;
   ra.out_shard_stride = kSS;
   ra.nsq = (long)n;
-  ra.nvec = (long)(r1 - r0);
+  ra.nvec = k;
   ra.nchunk = 1;
   ra.shard_bytes = kSS;
-  ProfScope p(ctx, 0, s);
-  HIP_TRY(ctx, launch_rs_encode((int)k, ra, s));
-  return DAGPU_OK;
-}
-
-// RS extension of n squares (uniform k), device pointers.
-// ev_rows (optional) is recorded between the row and the column pass: rows
-// 0..k-1 of every EDS ([Q0|Q1]) are final from that point on.
-// rows_done: the row pass already ran (the single-square slab pipeline).
-int enqueue_rs(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_ods, uint8_t* d_eds,
-               hipStream_t s, hipEvent_t ev_rows = nullptr, bool rows_done = false) {
-  const long w = 2L * k;
-  const long esq = (long)eds_bytes(k);
-  if (!rows_done) {
-    int rc = enqueue_row_pass(ctx, k, n, d_ods, d_eds, s, 0, k);
-    if (rc) return rc;
+  {
+    ProfScope p(ctx, 0, s);
+    HIP_TRY(ctx, launch_rs_encode((int)k, ra, s));
   }
   stage_mark(ctx, DAGPU_STAGE_ROWS, s);
   if (ev_rows) HIP_TRY(ctx, hipEventRecord(ev_rows, s));
@@ -107,28 +96,9 @@ int enqueue_rs(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_ods, uint8
   return DAGPU_OK;
 }
 
-// Leaf digests of EDS rows [r0, r1) of n squares (the slab pipeline hashes the
-// rows of [Q0|Q1] while the rest of the ODS is still uploading).
-int enqueue_leaves_rows(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_eds, void* d_ws, hipStream_t s,
-                        uint32_t r0, uint32_t r1) {
-  SquareArgs sa{};
-  sa.eds = d_eds;
-  sa.eds_sq_stride = (long)eds_bytes(k);
-  sa.k = (int)k;
-  sa.nsq = (long)n;
-  nmt_workspace_carve(sa, d_ws);
-  sa.leaf_cell0 = (long)r0 * 2 * k;
-  sa.leaf_ncell = (long)(r1 - r0) * 2 * k;
-  ProfScope p(ctx, 2, s);
-  HIP_TRY(ctx, launch_nmt_leaves(sa, s));
-  return DAGPU_OK;
-}
-
-// d_dah = NULL: roots only (Repair's verification needs no DAH).
-// leaf_row0: leaf digests of rows < leaf_row0 are already in the workspace.
+// d_dah = NULL: roots only (Repair's verification needs no DAH)
 int enqueue_roots(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_eds, uint8_t* d_rr,
-                  uint8_t* d_cr, uint8_t* d_dah, int32_t* d_status, void* d_ws, hipStream_t s,
-                  uint32_t leaf_row0 = 0) {
+                  uint8_t* d_cr, uint8_t* d_dah, int32_t* d_status, void* d_ws, hipStream_t s) {
   SquareArgs sa{};
   sa.eds = d_eds;
   sa.eds_sq_stride = (long)eds_bytes(k);
@@ -142,13 +112,9 @@ int enqueue_roots(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_eds, ui
   sa.k = (int)k;
   sa.nsq = (long)n;
   HIP_TRY(ctx, hipMemsetAsync(d_status, 0, n * sizeof(int32_t), s));
-  HIP_TRY(ctx, launch_nmt_prepare(sa, s));
   {
     ProfScope p(ctx, 2, s);
-    SquareArgs la = sa;
-    la.leaf_cell0 = (long)leaf_row0 * 2 * k;
-    la.leaf_ncell = (long)(2 * k - leaf_row0) * 2 * k;
-    HIP_TRY(ctx, launch_nmt_leaves(la, s));
+    HIP_TRY(ctx, launch_nmt_leaves(sa, s));
   }
   stage_mark(ctx, DAGPU_STAGE_LEAVES, s);
   {
@@ -156,7 +122,7 @@ int enqueue_roots(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_eds, ui
     HIP_TRY(ctx, launch_nmt_trees(sa, s));
   }
   stage_mark(ctx, DAGPU_STAGE_TREES, s);
-  if (d_dah && !nmt_trees_do_dah(sa)) {  // (the latency path hashed it with the tree tops)
+  if (d_dah) {
     ProfScope p(ctx, 4, s);
     HIP_TRY(ctx, launch_dah(sa, s));
   }
@@ -317,34 +283,6 @@ hipError_t wait_stream(hipStream_t s, bool spin) {
   return e;
 }
 
-hipEvent_t ev_take(dagpu_ctx* c) {
-  std::lock_guard<std::mutex> g(c->ev_mu);
-  if (!c->ev_pool.empty()) {
-    hipEvent_t e = c->ev_pool.back();
-    c->ev_pool.pop_back();
-    return e;
-  }
-  hipEvent_t e = nullptr;
-  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
-  return e;
-}
-
-void ev_give(dagpu_ctx* c, hipEvent_t e) {
-  if (!e) return;
-  std::lock_guard<std::mutex> g(c->ev_mu);
-  c->ev_pool.push_back(e);
-}
-
-// Row slabs of a single-square host call (see run_group_host).
-uint32_t slab_count(uint32_t k, size_t n) {
-  if (n != 1 || k < 64) return 1;
-  const char* e = getenv("DAGPU_SLAB_UPLOAD");
-  if (e && e[0] == '0') return 1;
-  const long v = e ? atol(e) : 0;
-  const uint32_t s = v > 1 ? (uint32_t)v : 4;
-  return s > k ? k : s;
-}
-
 // Runs one uniform-k group from host memory.  Caller holds ctx->mu.
 int run_group_host(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* ods, uint8_t* eds_out,
                    uint8_t* rr, uint8_t* cr, uint8_t* dah, int32_t* status) {
@@ -361,43 +299,8 @@ int run_group_host(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* ods, uin
   HIP_TRY(ctx, ctx->ws.ensure(dagpu_workspace_size(k, n)));
   ctx->stage_mask = 0;
   stage_mark(ctx, DAGPU_STAGE_START, s);
-  // Single square: the ODS goes up in row slabs on the copy stream, and each
-  // slab's row pass and the leaf digests of its [Q0|Q1] rows run while the
-  // next slab is in flight; what is left after the last byte lands is the
-  // column pass and the rows k..2k-1.  DAGPU_SLAB_UPLOAD=0: one upload.
-  const uint32_t slabs = slab_count(k, n);
-  if (slabs > 1) {
-    // (no wait needed: every host call has drained both streams before returning)
-    std::vector<hipEvent_t> ev(slabs, nullptr);
-    for (auto& e : ev)
-      if (!(e = ev_take(ctx))) {
-        for (auto x : ev) ev_give(ctx, x);
-        return set_err(ctx, DAGPU_ERR_DEVICE, "hipEventCreate failed");
-      }
-    auto give = [&](int r) {
-      for (auto x : ev) ev_give(ctx, x);
-      return r;
-    };
-    const size_t rb = (size_t)k * kSS;  // one ODS row
-    for (uint32_t i = 0; i < slabs; i++) {
-      const uint32_t r0 = k * i / slabs, r1 = k * (i + 1) / slabs;
-      if (hipMemcpyAsync((uint8_t*)ctx->ods.p + r0 * rb, ods + r0 * rb, (r1 - r0) * rb, hipMemcpyHostToDevice,
-                         cs) != hipSuccess || hipEventRecord(ev[i], cs) != hipSuccess)
-        return give(set_err(ctx, DAGPU_ERR_DEVICE, "slab upload failed"));
-    }
-    stage_mark(ctx, DAGPU_STAGE_UPLOADED, cs);
-    for (uint32_t i = 0; i < slabs; i++) {
-      const uint32_t r0 = k * i / slabs, r1 = k * (i + 1) / slabs;
-      if (hipStreamWaitEvent(s, ev[i], 0) != hipSuccess) return give(set_err(ctx, DAGPU_ERR_DEVICE, "slab wait failed"));
-      rc = enqueue_row_pass(ctx, k, 1, (const uint8_t*)ctx->ods.p, (uint8_t*)ctx->eds.p, s, r0, r1);
-      if (!rc) rc = enqueue_leaves_rows(ctx, k, 1, (const uint8_t*)ctx->eds.p, ctx->ws.p, s, r0, r1);
-      if (rc) return give(rc);
-    }
-    give(0);
-  } else {
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->ods.p, ods, ods_bytes(k) * n, hipMemcpyHostToDevice, s));
-    stage_mark(ctx, DAGPU_STAGE_UPLOADED, s);
-  }
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->ods.p, ods, ods_bytes(k) * n, hipMemcpyHostToDevice, s));
+  stage_mark(ctx, DAGPU_STAGE_UPLOADED, s);
   // An EDS requested back goes down on the copy stream while the kernels run:
   // the top halves ([Q0|Q1], final after the row pass) during the column pass
   // and the NMT kernels, the bottom halves ([Q2|Q3]) during the NMT kernels.
@@ -406,7 +309,7 @@ int run_group_host(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* ods, uin
   // device->host copy runs synchronously on this thread, so there the whole
   // kernel chain and the results download are queued first.
   rc = enqueue_rs(ctx, k, n, (const uint8_t*)ctx->ods.p, (uint8_t*)ctx->eds.p, s,
-                  eds_out ? ctx->ev_loaded[0] : nullptr, slabs > 1);
+                  eds_out ? ctx->ev_loaded[0] : nullptr);
   if (rc) return rc;
   if (eds_out) HIP_TRY(ctx, hipEventRecord(ctx->ev_loaded[1], s));
   // from the first EDS copy on, DMA may be writing into eds_out: every return
@@ -435,8 +338,7 @@ int run_group_host(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* ods, uin
   };
   const bool early = eds_out && host_pinned(eds_out);
   if (early && (rc = eds_copies())) return rc;
-  rc = enqueue_roots(ctx, k, n, (const uint8_t*)ctx->eds.p, res.rr, res.cr, res.dah, res.st, ctx->ws.p, s,
-                     slabs > 1 ? k : 0);
+  rc = enqueue_roots(ctx, k, n, (const uint8_t*)ctx->eds.p, res.rr, res.cr, res.dah, res.st, ctx->ws.p, s);
   if (rc) return rc;
   HIP_TRY(ctx, res.download(ctx, s));
   stage_mark(ctx, DAGPU_STAGE_RESULTS, s);
@@ -640,6 +542,24 @@ int dagpu_roots_device(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_ed
 }
 
 namespace {
+
+hipEvent_t ev_take(dagpu_ctx* c) {
+  std::lock_guard<std::mutex> g(c->ev_mu);
+  if (!c->ev_pool.empty()) {
+    hipEvent_t e = c->ev_pool.back();
+    c->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+  return e;
+}
+
+void ev_give(dagpu_ctx* c, hipEvent_t e) {
+  if (!e) return;
+  std::lock_guard<std::mutex> g(c->ev_mu);
+  c->ev_pool.push_back(e);
+}
 
 long env_long(const char* name) {
   const char* e = getenv(name);

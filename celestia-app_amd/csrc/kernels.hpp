@@ -239,20 +239,12 @@ struct SquareArgs {
   int32_t* status;      // nsq status words (kernels OR bits into them)
   int k;
   long nsq;
-  // leaf kernel only: cells [leaf_cell0, leaf_cell0 + leaf_ncell) of each
-  // square (row-major cell index); leaf_ncell = 0 means all (2k)^2 cells
-  long leaf_cell0, leaf_ncell;
 };
 
 hipError_t launch_nmt_leaves(const SquareArgs& a, hipStream_t s);
 // workspace layout for SquareArgs (digests | ns_table | rec_a | rec_b)
 size_t nmt_workspace_bytes(int k, long nsq);
 void nmt_workspace_carve(SquareArgs& a, void* ws);
-// Small batches (2 <= k <= 128) take a latency path: levels >= 2 and the DAH in
-// one launch.  launch_nmt_prepare (before the leaves) zeroes its counters;
-// nmt_trees_do_dah tells whether launch_nmt_trees already wrote the DAH.
-hipError_t launch_nmt_prepare(const SquareArgs& a, hipStream_t s);
-bool nmt_trees_do_dah(const SquareArgs& a);
 hipError_t launch_nmt_trees(const SquareArgs& a, hipStream_t s);
 hipError_t launch_dah(const SquareArgs& a, hipStream_t s);
 

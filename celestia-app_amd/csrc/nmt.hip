@@ -52,13 +52,12 @@ constexpr int kLeafWave = 256;
 __global__ __launch_bounds__(kLeafWave) void nmt_leaf_kernel(SquareArgs a) {
   const int k = a.k;
   const long w = 2L * k;
-  const long cells = a.leaf_ncell ? a.leaf_ncell : w * w;
+  const long cells = w * w;
   const long total = cells * a.nsq;
-  const long gid_ = (long)blockIdx.x * kLeafWave + threadIdx.x;
-  if (gid_ >= total) return;
-  const long sq = gid_ / cells;
-  const long cell = a.leaf_cell0 + (gid_ - sq * cells);
-  const long gid = sq * w * w + cell;  // digest slot
+  const long gid = (long)blockIdx.x * kLeafWave + threadIdx.x;
+  if (gid >= total) return;
+  const long sq = gid / cells;
+  const long cell = gid - sq * cells;
   const long r = cell / w, c = cell - (cell / w) * w;
   const bool q0 = (r < k) && (c < k);
   const uint4* src = (const uint4*)(a.eds + sq * a.eds_sq_stride + cell * kShareSize);
@@ -274,11 +273,10 @@ constexpr int kDahChunk = 2048;
 
 // RFC-6962 inner levels over cur digests at src (8 dwords each), ping-ponging
 // with dst (cur / 2 slots); returns the buffer holding the root.
-template <int NT>
-__device__ uint32_t* rfc_reduce_t(uint32_t* src, uint32_t* dst, int cur) {
+__device__ uint32_t* rfc_reduce(uint32_t* src, uint32_t* dst, int cur) {
   while (cur > 1) {
     const int next = cur / 2;
-    for (int i = threadIdx.x; i < next; i += NT) {
+    for (int i = threadIdx.x; i < next; i += kDahThreads) {
       uint32_t m[32];
 #pragma unroll
       for (int j = 0; j < 32; j++) m[j] = 0;
@@ -351,172 +349,15 @@ __global__ __launch_bounds__(kDahThreads) void dah_kernel(SquareArgs a) {
       for (int j = 0; j < 8; j++) lds[i * 8 + j] = bswap32(st[j]);
     }
     __syncthreads();
-    const uint32_t* r = rfc_reduce_t<kDahThreads>(lds, lds + C * 8, C);
+    const uint32_t* r = rfc_reduce(lds, lds + C * 8, C);
     if (threadIdx.x < 8) sub[(c0 / C) * 8 + threadIdx.x] = r[threadIdx.x];
     __syncthreads();
   }
-  const uint32_t* root = rfc_reduce_t<kDahThreads>(sub, lds, n / C);
+  const uint32_t* root = rfc_reduce(sub, lds, n / C);
   if (threadIdx.x < 8) {
     uint32_t* out = (uint32_t*)(a.dah + sq * 32);
     out[threadIdx.x] = root[threadIdx.x];
   }
-}
-
-// ---------------------------------------------------------------------------
-// Latency path (a few squares, e.g. the single-square ProcessProposal call,
-// app/process_proposal.go:147-161): tree levels 2..top AND the DAH in ONE
-// launch.  A workgroup takes TPW consecutive trees of one square (row trees
-// 0..w-1, then column trees), reads their level-1 records from global memory,
-// keeps every higher level in LDS, writes the roots and the DAH leaf digest
-// SHA256(0x00 | root) of each of its trees; the workgroup whose trees complete
-// the square (agent-scope counter) hashes the DAH from those digests.  Hand-off:
-// sc1 stores, every storing wave's vmcnt(0), a barrier, ONE agent atomic per
-// workgroup, sc1 loads by the last one (MI355X_MICROARCH.md, the counter row of
-// the hand-off table).  Per-level launches cost ~5 us of launch gap each on a
-// dependent chain of 8 tree levels + the DAH (single square: trees 95 us + DAH
-// 67 us, r03).  k <= 512 (level 2 of a workgroup's trees fits 256 threads).
-// ---------------------------------------------------------------------------
-constexpr int kTopThreads = 256;
-constexpr int kTopRec = 10;  // dwords per LDS record: digest(8) | minRef | maxRef
-constexpr int kTopMaxK = 128;
-constexpr int kTopMaxLeaves = 4 * kTopMaxK;  // DAH leaves of one square
-
-__device__ __forceinline__ void st_sc1(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// SHA256(0x00 | root) of a 90-B root at a 2-byte aligned address (DAH leaf)
-__device__ __forceinline__ void dah_leaf_digest(const uint8_t* root, uint32_t (&out)[8]) {
-  uint32_t m[32];
-#pragma unroll
-  for (int j = 0; j < 32; j++) m[j] = 0;
-  const uint16_t* r16 = (const uint16_t*)root;
-#pragma unroll
-  for (int h = 0; h < 45; h++) {
-    const uint32_t v = r16[h];
-    const int off = 1 + 2 * h;
-    m[off >> 2] |= v << (8 * (off & 3));
-    if ((off & 3) == 3) m[(off >> 2) + 1] |= v >> 8;
-  }
-  m[91 >> 2] |= 0x80u << (8 * (91 & 3));
-  uint32_t st[8];
-  sha256_init(st);
-#pragma unroll
-  for (int blk = 0; blk < 2; blk++) {
-    uint32_t wv[16];
-#pragma unroll
-    for (int j = 0; j < 16; j++) wv[j] = bswap32(m[16 * blk + j]);
-    if (blk == 1) { wv[14] = 0; wv[15] = 91u * 8u; }
-    sha256_compress(st, wv);
-  }
-#pragma unroll
-  for (int j = 0; j < 8; j++) out[j] = bswap32(st[j]);
-}
-
-__global__ __launch_bounds__(kTopThreads) void nmt_top_kernel(SquareArgs a, const uint8_t* rec1, int tpw,
-                                                              uint32_t* dah_leaf, int32_t* counter) {
-  __shared__ uint32_t buf[2][kTopThreads * kTopRec];
-  __shared__ uint32_t dl[kTopMaxLeaves * 8 + kTopMaxLeaves / 2 * 8];  // DAH levels (last workgroup)
-  __shared__ int last_s;
-  const int k = a.k, w = 2 * k;
-  const int groups = 2 * w / tpw;
-  const long sq = blockIdx.x / groups;
-  const int t0 = (int)(blockIdx.x - sq * groups) * tpw;  // first tree (axis * w + idx)
-  int levels = 0;
-  while ((1 << levels) < w) levels++;
-  const uint8_t* ns_sq = a.ns_table + sq * (long)k * k * 32;
-  int cur = 0;
-  for (int L = 2; L <= levels; L++) {
-    const int per = w >> L;
-    const int nodes = tpw * per;
-    const bool fin = L == levels;
-    for (int j = threadIdx.x; j < nodes; j += kTopThreads) {
-      const int tl = j / per, p = j - tl * per;
-      const int tree = t0 + tl, axis = tree >= w, idx = tree - (axis ? w : 0);
-      uint32_t dl_[8], dr_[8], lref[2], rref[2];
-      if (L == 2) {
-        const uint4* li = (const uint4*)(rec1 + level_rec(sq, w, 2 * per, axis, idx, 2 * p) * 48);
-        const uint4* ri = (const uint4*)(rec1 + level_rec(sq, w, 2 * per, axis, idx, 2 * p + 1) * 48);
-        const uint4 l0 = li[0], l1 = li[1], l2 = li[2], r0 = ri[0], r1 = ri[1], r2 = ri[2];
-        dl_[0] = l0.x; dl_[1] = l0.y; dl_[2] = l0.z; dl_[3] = l0.w;
-        dl_[4] = l1.x; dl_[5] = l1.y; dl_[6] = l1.z; dl_[7] = l1.w;
-        dr_[0] = r0.x; dr_[1] = r0.y; dr_[2] = r0.z; dr_[3] = r0.w;
-        dr_[4] = r1.x; dr_[5] = r1.y; dr_[6] = r1.z; dr_[7] = r1.w;
-        lref[0] = l2.x; lref[1] = l2.y; rref[0] = r2.x; rref[1] = r2.y;
-      } else {
-        const uint32_t* li = &buf[cur][(tl * 2 * per + 2 * p) * kTopRec];
-        const uint32_t* ri = li + kTopRec;
-#pragma unroll
-        for (int i = 0; i < 8; i++) { dl_[i] = li[i]; dr_[i] = ri[i]; }
-        lref[0] = li[8]; lref[1] = li[9]; rref[0] = ri[8]; rref[1] = ri[9];
-      }
-      uint32_t lmn[8], lmx[8], rmn[8], rmx[8];
-      ns_by_ref(ns_sq, lref[0], lmn);
-      ns_by_ref(ns_sq, lref[1], lmx);
-      ns_by_ref(ns_sq, rref[0], rmn);
-      ns_by_ref(ns_sq, rref[1], rmx);
-      uint32_t st[8];
-      if (__all(lref[0] == kParityRef && rref[0] == kParityRef)) {
-        auto get = [&](int P, int i) -> uint32_t {
-          return P == 2 ? dl_[i] : P == 5 ? dr_[i] : 0xFFFFFFFFu;
-        };
-        sha_node_msg<true, true, true>(get, st);
-      } else if (__all(lref[0] == kParityRef)) {
-        auto get = [&](int P, int i) -> uint32_t {
-          return P <= 1 ? 0xFFFFFFFFu : P == 2 ? dl_[i] : P == 3 ? rmn[i] : P == 4 ? rmx[i] : dr_[i];
-        };
-        sha_node_msg<true>(get, st);
-      } else {
-        auto get = [&](int P, int i) -> uint32_t {
-          return P == 0 ? lmn[i] : P == 1 ? lmx[i] : P == 2 ? dl_[i] : P == 3 ? rmn[i] : P == 4 ? rmx[i] : dr_[i];
-        };
-        sha_node_msg(get, st);
-      }
-      uint32_t dg[8];
-#pragma unroll
-      for (int i = 0; i < 8; i++) dg[i] = bswap32(st[i]);
-      const bool rpar = rref[0] == kParityRef;
-      if (fin) {
-        uint8_t* dst = (axis == 0 ? a.row_roots : a.col_roots) + (sq * w + idx) * kNodeSize;
-        if (rpar) write_root(dst, lmn, lmx, dg);
-        else write_root(dst, lmn, rmx, dg);
-        if (dah_leaf) {  // this lane reads back its own stores
-          uint32_t h[8];
-          dah_leaf_digest(dst, h);
-          uint32_t* o = dah_leaf + (sq * 2 * w + tree) * 8;
-#pragma unroll
-          for (int i = 0; i < 8; i++) st_sc1(o + i, h[i]);
-        }
-      } else {
-        uint32_t* o = &buf[cur ^ 1][(tl * per + p) * kTopRec];
-#pragma unroll
-        for (int i = 0; i < 8; i++) o[i] = dg[i];
-        o[8] = lref[0];
-        o[9] = rpar ? lref[1] : rref[1];
-      }
-    }
-    __syncthreads();
-    cur ^= 1;
-  }
-  if (!dah_leaf) return;
-  // hand-off: every storing wave's stores done, then one agent atomic per workgroup
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int old = __hip_atomic_fetch_add(counter + sq, tpw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last_s = old + tpw == 2 * w;
-  }
-  __syncthreads();
-  if (!last_s) return;
-  // the square's DAH: RFC-6962 over its 2w leaf digests (n <= kTopMaxLeaves)
-  const int n = 2 * w;
-  for (int i = threadIdx.x; i < n * 8; i += kTopThreads) dl[i] = ld_sc1(dah_leaf + sq * n * 8 + i);
-  __syncthreads();
-  const uint32_t* root = rfc_reduce_t<kTopThreads>(dl, dl + n * 8, n);
-  if (threadIdx.x < 8) ((uint32_t*)(a.dah + sq * 32))[threadIdx.x] = root[threadIdx.x];
 }
 
 // DAGPU_LEAF_LDS_KB (experiments): dynamic LDS requested per leaf workgroup,
@@ -532,53 +373,13 @@ static size_t leaf_lds_bytes() {
 
 hipError_t launch_nmt_leaves(const SquareArgs& a, hipStream_t s) {
   const long w = 2L * a.k;
-  const long total = (a.leaf_ncell ? a.leaf_ncell : w * w) * a.nsq;
-  if (total <= 0) return hipSuccess;
+  const long total = w * w * a.nsq;
   const long blocks = (total + kLeafWave - 1) / kLeafWave;
   hipLaunchKernelGGL(nmt_leaf_kernel, dim3((unsigned)blocks), dim3(kLeafWave), leaf_lds_bytes(), s, a);
   return hipGetLastError();
 }
 
-// Latency path switch: small batches of 2 <= k <= kTopMaxK; DAGPU_TREE_FUSED=0
-// turns it off, =1 forces it for any batch size (A/B; read per call).
-static bool top_fused(const SquareArgs& a) {
-  if (a.k < 2 || a.k > kTopMaxK) return false;
-  const char* e = getenv("DAGPU_TREE_FUSED");
-  if (e && e[0] == '0') return false;
-  if (e && e[0] == '1') return true;
-  return a.nsq <= 4;
-}
-
-// dah_leaf digests and per-square counters of the fused path live in rec_b,
-// which the fused path does not use for tree levels
-static uint32_t* top_dah_leaf(const SquareArgs& a) { return (uint32_t*)a.rec_b; }
-static int32_t* top_counter(const SquareArgs& a) {
-  const size_t leaf = ((size_t)a.nsq * 4 * a.k * 32 + 255) & ~(size_t)255;
-  return (int32_t*)(a.rec_b + leaf);
-}
-
-hipError_t launch_nmt_prepare(const SquareArgs& a, hipStream_t s) {
-  if (!top_fused(a) || !a.dah) return hipSuccess;
-  return hipMemsetAsync(top_counter(a), 0, (size_t)a.nsq * sizeof(int32_t), s);
-}
-
-bool nmt_trees_do_dah(const SquareArgs& a) { return top_fused(a) && a.dah; }
-
 hipError_t launch_nmt_trees(const SquareArgs& a, hipStream_t s) {
-  if (top_fused(a)) {
-    const int w = 2 * a.k;
-    const long total = a.nsq * 2L * w * (w / 2);
-    hipLaunchKernelGGL(nmt_level1_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a, a.rec_a, 0);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    const int per2 = w / 4;
-    int tpw = kTopThreads / per2;
-    if (tpw > 2 * w) tpw = 2 * w;
-    const long blocks = a.nsq * (2L * w / tpw);
-    hipLaunchKernelGGL(nmt_top_kernel, dim3((unsigned)blocks), dim3(kTopThreads), 0, s, a,
-                       (const uint8_t*)a.rec_a, tpw, a.dah ? top_dah_leaf(a) : nullptr, top_counter(a));
-    return hipGetLastError();
-  }
   const int w = 2 * a.k;
   int levels = 0;
   while ((1 << levels) < w) levels++;

@@ -574,7 +574,8 @@ extern "C" {
 int dagpu_square_construct(dagpu_ctx* ctx, const uint8_t* txs, const uint64_t* tx_lens, size_t ntx,
                            uint32_t max_square_size, uint32_t subtree_root_threshold, uint8_t* ods_out,
                            size_t ods_cap, uint32_t* square_size) {
-  if ((ntx && (!txs || !tx_lens)) || subtree_root_threshold == 0) return DAGPU_ERR_ARG;
+  if (ntx && (!txs || !tx_lens)) return set_err(ctx, DAGPU_ERR_ARG, "txs and tx_lens are required when ntx > 0");
+  if (subtree_root_threshold == 0) return set_err(ctx, DAGPU_ERR_ARG, "subtree_root_threshold must be > 0");
   try {
     SquareBuilder b(max_square_size, subtree_root_threshold);
     const std::vector<Span> v = split_txs(txs, tx_lens, ntx);
@@ -603,7 +604,8 @@ int dagpu_square_construct(dagpu_ctx* ctx, const uint8_t* txs, const uint64_t* t
 int dagpu_square_build(dagpu_ctx* ctx, const uint8_t* txs, const uint64_t* tx_lens, size_t ntx,
                        uint32_t max_square_size, uint32_t subtree_root_threshold, uint8_t* ods_out,
                        size_t ods_cap, uint32_t* square_size, uint8_t* kept) {
-  if ((ntx && (!txs || !tx_lens)) || subtree_root_threshold == 0) return DAGPU_ERR_ARG;
+  if (ntx && (!txs || !tx_lens)) return set_err(ctx, DAGPU_ERR_ARG, "txs and tx_lens are required when ntx > 0");
+  if (subtree_root_threshold == 0) return set_err(ctx, DAGPU_ERR_ARG, "subtree_root_threshold must be > 0");
   try {
     SquareBuilder b(max_square_size, subtree_root_threshold);
     const std::vector<Span> v = split_txs(txs, tx_lens, ntx);

@@ -37,7 +37,7 @@ def _want(k, seed):
 
 
 @pytest.mark.parametrize("k,parts", [(2, 1), (2, 2), (8, 1), (8, 2), (8, 8), (32, 4), (128, 8),
-                                     (256, 1), (256, 2), (256, 8), (512, 8)])
+                                     (256, 1), (256, 2), (256, 8), (512, 8), (1024, 8)])
 def test_split_local_matches_oracle(ctx, k, parts):
     ods, rr, cr, dah = _want(k, 7100 + k)
     d = torch.from_numpy(np.ascontiguousarray(ods).reshape(-1)).cuda()
@@ -86,17 +86,21 @@ def _dist_worker(rank, world, port, k, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("k", [16, 256])
-def test_split_two_processes(k):
+@pytest.mark.parametrize("k,world", [(16, 2), (256, 2), (256, 4), (512, 8)])
+def test_split_processes(k, world):
+    """One square over `world` processes through torch.distributed (gloo,
+    host-staged, all ranks on this one GPU): the RCCL code path of the 8-GPU
+    stress square (bench.py --gpus 8 split_stress) with every rank's roots and
+    DAH equal to the oracle's single-square result (configs[4]: k = 512, P = 8)."""
     import torch.multiprocessing as mp
     _, rr, cr, dah = _want(k, 7100 + k)
     ctxm = mp.get_context("spawn")
     q = ctxm.Queue()
     port = _free_port()
-    procs = [ctxm.Process(target=_dist_worker, args=(r, 2, port, k, q)) for r in range(2)]
+    procs = [ctxm.Process(target=_dist_worker, args=(r, world, port, k, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=120) for _ in range(2)]
+    res = [q.get(timeout=180) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

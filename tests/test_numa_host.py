@@ -59,3 +59,33 @@ def test_bind_restricts_or_keeps_mask(tmp_path):
         assert r["numa_node"] == -1 and not r["bound"] and os.sched_getaffinity(0) == before
     finally:
         os.sched_setaffinity(0, before)
+
+
+def test_hip_and_cuda_visible_both_set(tmp_path):
+    # HIP honours HIP_VISIBLE_DEVICES over CUDA_VISIBLE_DEVICES (one of them,
+    # not both in sequence): launchers often set both to the same list
+    root = _fake(tmp_path)
+    env = {"HIP_VISIBLE_DEVICES": "1", "CUDA_VISIBLE_DEVICES": "1"}
+    assert numa.gpu_numa(0, root, env=env)["pci"] == "0001:85:00.0"
+    # CUDA_VISIBLE_DEVICES alone still applies; ROCR filters first
+    assert numa.gpu_numa(0, root, env={"CUDA_VISIBLE_DEVICES": "1"})["pci"] == "0001:85:00.0"
+    env = {"ROCR_VISIBLE_DEVICES": "1,0", "HIP_VISIBLE_DEVICES": "1", "CUDA_VISIBLE_DEVICES": "0"}
+    assert numa.gpu_numa(0, root, env=env)["pci"] == "0000:05:00.0"
+
+
+def test_gpu_links_xgmi_and_pcie(tmp_path):
+    root = _fake(tmp_path)
+    base = tmp_path / "class/kfd/kfd/topology/nodes"
+
+    def link(n, i, props):
+        d = base / str(n) / "io_links" / str(i)
+        d.mkdir(parents=True)
+        (d / "properties").write_text("".join(f"{k} {v}\n" for k, v in props.items()))
+
+    link(1, 0, {"type": 2, "node_from": 1, "node_to": 0, "weight": 20})   # GPU 0 -> CPU over PCIe
+    link(1, 1, {"type": 11, "node_from": 1, "node_to": 2, "weight": 15})  # GPU 0 <-> GPU 1 over xGMI
+    link(2, 0, {"type": 11, "node_from": 2, "node_to": 1, "weight": 15})
+    got = numa.gpu_links(root)
+    assert got["0000:05:00.0"] == {"xgmi": ["0001:85:00.0"], "pcie_peers": [], "pcie_to_cpu": 1}
+    assert got["0001:85:00.0"]["xgmi"] == ["0000:05:00.0"]
+    assert numa.gpu_links(str(tmp_path / "nowhere")) == {}

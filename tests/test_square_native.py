@@ -144,3 +144,25 @@ def _timed(txs):
     t0 = time.perf_counter()
     sq.construct_native(txs)
     return time.perf_counter() - t0
+
+
+def test_argument_errors_carry_this_calls_message():
+    # a stale message from an earlier failure must not leak into the next
+    # argument error of a context-free call
+    import ctypes
+
+    import numpy as np
+    from celestia_da import _abi
+    L = _abi.lib()
+    with pytest.raises(sh.ShareError if hasattr(sh, "ShareError") else Exception):
+        sq.construct_native([b"x" * 400] * 20, max_square_size=1)  # an earlier failure with a message
+    assert L.dagpu_last_error(None).decode().startswith("not enough space")
+    out = np.empty(512, np.uint8)
+    k = ctypes.c_uint32(0)
+    rc = L.dagpu_square_construct(None, None, None, 0, 64, 0, _abi.addr(out), 512, ctypes.addressof(k))
+    assert rc == _abi.ERR_ARG
+    assert L.dagpu_last_error(None).decode() == "subtree_root_threshold must be > 0"
+    lens = np.array([4], np.uint64)
+    rc = L.dagpu_square_build(None, None, _abi.addr(lens), 1, 64, 64, _abi.addr(out), 512, ctypes.addressof(k), None)
+    assert rc == _abi.ERR_ARG
+    assert L.dagpu_last_error(None).decode() == "txs and tx_lens are required when ntx > 0"

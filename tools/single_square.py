@@ -1,9 +1,10 @@
 """A/B of the single-square drop-in latency (bench.py bench_single, the
-ProcessProposal shape) over the latency-path switches, in one process with
-the variants interleaved: DAGPU_SLAB_UPLOAD (row-slab upload pipeline) and
-DAGPU_TREE_FUSED (tree levels >= 2 + DAH in one launch).
+ProcessProposal shape) over environment switches of the library, in one
+process with the variants interleaved (the library reads them per call).
+Round 4 used it for the row-slab upload and fused tree-top experiments
+(profiles/single_square_ab_r04.log; both removed).
 
-    python tools/single_square.py [rounds]
+    python tools/single_square.py [rounds] [VAR=a,b ...]
 """
 import json
 import os
@@ -16,12 +17,14 @@ for p in (ROOT, os.path.join(ROOT, "celestia-app_amd"), os.path.join(ROOT, "orac
 import bench  # noqa: E402
 from celestia_da import da  # noqa: E402
 
-VARIANTS = {
-    "r03 (one upload, level launches)": {"DAGPU_SLAB_UPLOAD": "0", "DAGPU_TREE_FUSED": "0"},
-    "fused tops only": {"DAGPU_SLAB_UPLOAD": "0", "DAGPU_TREE_FUSED": "auto"},
-    "slabs only": {"DAGPU_SLAB_UPLOAD": "auto", "DAGPU_TREE_FUSED": "0"},
-    "default (slabs + fused tops)": {"DAGPU_SLAB_UPLOAD": "auto", "DAGPU_TREE_FUSED": "auto"},
-}
+
+def variants(args):
+    """VAR=a,b -> one variant per value ('auto' = unset); no args: the default build."""
+    out = {"default": {}}
+    for a in args:
+        key, vals = a.split("=", 1)
+        out = {f"{n} {key}={v}".strip(): dict(env, **{key: v}) for n, env in out.items() for v in vals.split(",")}
+    return out
 
 
 def main():
@@ -29,7 +32,7 @@ def main():
     ctx = da.Context(0)
     out = {}
     for r in range(rounds):
-        for name, env in VARIANTS.items():
+        for name, env in variants(sys.argv[2:]).items():
             for key, v in env.items():
                 if v == "auto":
                     os.environ.pop(key, None)
