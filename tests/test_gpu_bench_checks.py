@@ -161,9 +161,11 @@ def test_rccl_replay_corruption_is_fatal():
 
 def test_two_threads_one_context(ctx):
     """Device-resident calls from two host threads on one context, each on its
-    own stream; thread B fails on purpose (k = 3, then k = 4096) on every
+    own stream; thread B fails on purpose (k = 3, then twice the widest
+    supported k) on every
     iteration while thread A extends squares."""
     L = ctx._L
+    too_wide = 2 * L.dagpu_max_square_width()  # rejected before anything is enqueued
     k, n = 32, 6
     ods = synth.blob_squares(k, 31337, 0, n)
     _, _, _, want, _ = da.extend_batch(ods.reshape(-1), [k] * n, ctx)
@@ -186,7 +188,7 @@ def test_two_threads_one_context(ctx):
     def worker_b():
         try:
             for i in range(iters):
-                bad_k = 3 if i % 2 == 0 else 4096
+                bad_k = 3 if i % 2 == 0 else too_wide
                 rc = L.dagpu_extend_batch_device(ctx.handle, bad_k, 1, _abi.addr(ds.ods), _abi.addr(ds.eds),
                                                  _abi.addr(ds.row_roots), _abi.addr(ds.col_roots),
                                                  _abi.addr(ds.dah), _abi.addr(ds.status),
