@@ -280,6 +280,8 @@ def main():
     ap.add_argument("--batch", type=int, default=256,
                     help="squares per GPU per step (SURVEY.md §8d: C2 batches of >= 256 squares)")
     ap.add_argument("--distinct", type=int, default=256, help="distinct generated squares per GPU")
+    ap.add_argument("--repair-slices", type=int, default=1,
+                    help="--mode repair: the batch as this many asynchronous calls on their own streams")
     ap.add_argument("--pattern", choices=["subgrid", "q3"], default="subgrid",
                     help="--mode repair: kept cells = a random k x k sub-grid (configs[3]) or Q3 only")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time per k (64 and 128)")
@@ -974,13 +976,16 @@ def bench_mixed(args):
 REPAIR_SEED = 777
 
 
-def run_repair(ctx, k, B, steps, warmup, distinct=None, pattern="subgrid"):
+def run_repair(ctx, k, B, steps, warmup, distinct=None, pattern="subgrid", slices=1):
     """configs[3]: rsmt2d Repair of B distinct k x k squares with the maximal
     recoverable erasure pattern (a random k x k sub-grid kept, 3k^2 cells
     erased; pattern "q3": the k x k sub-grid of parity rows and parity columns,
     which the reverse fill rebuilds), every row/column root re-verified.  Timed with HIP events around
     the repair only (each step first restores the damaged input).  bit_exact
-    (fatal if false): the repaired EDS equals the extended one, status 0."""
+    (fatal if false): the repaired EDS equals the extended one, status 0.
+    slices > 1: the batch as that many started repairs (dagpu_repair_start,
+    each crossword on its own worker thread and stream), joined back to the
+    timed stream, so that one slice's round trips overlap another's kernels."""
     from celestia_da import synth
     from celestia_da.device import DeviceSquares
 
@@ -1002,14 +1007,29 @@ def run_repair(ctx, k, B, steps, warmup, distinct=None, pattern="subgrid"):
     damaged = (ds.eds.view(B, w * w, 512) * pres_t.view(B, w * w, 1)).view(B, -1).clone()
     present = pres_t.clone()
     status = torch.zeros(B, dtype=torch.int32, device="cuda")
-    ws = ds.repair_workspace()
+    cut = [B * j // slices for j in range(slices + 1)]
+    if slices == 1:
+        ws = ds.repair_workspace()
+    else:
+        wss = [ds.repair_workspace(cut[j + 1] - cut[j]) for j in range(slices)]
+        ws = None
+
+    def repair_step():
+        if slices == 1:
+            ds.repair(present, status, ws)
+            return
+        hs = [ds.repair_start(present, status, wss[j], first=cut[j], count=cut[j + 1] - cut[j])
+              for j in range(slices)]
+        for h in hs:
+            ds.repair_join(h)
+
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     for i in range(warmup + steps):
         ds.eds.copy_(damaged)
         present.copy_(pres_t)
         if i >= warmup:
             ev[i - warmup][0].record()
-        ds.repair(present, status, ws)
+        repair_step()
         if i >= warmup:
             ev[i - warmup][1].record()
     torch.cuda.synchronize()
@@ -1020,7 +1040,8 @@ def run_repair(ctx, k, B, steps, warmup, distinct=None, pattern="subgrid"):
     ms = sum(a.elapsed_time(b) for a, b in ev) / steps
     del ds, ref, damaged, ws
     torch.cuda.empty_cache()
-    return {"k": k, "squares": B, "pattern": pattern, "squares_per_s": B / (ms * 1e-3), "ms_per_step": ms,
+    return {"k": k, "squares": B, "pattern": pattern, "slices": slices, "squares_per_s": B / (ms * 1e-3),
+            "ms_per_step": ms,
             "steps": steps, "bit_exact": ok, "decode_gbs": rs_bytes(k) * B / (ms * 1e-3) / 1e9}
 
 
@@ -1028,7 +1049,8 @@ def bench_repair(args):
     from celestia_da import da
 
     torch.cuda.set_device(0)
-    r = run_repair(da.Context(0), args.k, args.batch, args.steps, args.warmup, args.distinct, args.pattern)
+    r = run_repair(da.Context(0), args.k, args.batch, args.steps, args.warmup, args.distinct, args.pattern,
+                   args.repair_slices)
     kept = "Q3 kept" if args.pattern == "q3" else "random k x k sub-grid kept"
     out = {"metric": f"Repair squares/sec (k={args.k}, maximal erasure, roots re-verified)",
            "value": r["squares_per_s"], "unit": "squares/s", "n_gpus": 1, "steps": args.steps,

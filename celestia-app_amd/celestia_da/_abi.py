@@ -57,6 +57,8 @@ EXPORTS = (
     "dagpu_repair_workspace_size",
     "dagpu_repair_batch_device",
     "dagpu_repair_batch_device_ex",
+    "dagpu_repair_start",
+    "dagpu_repair_join",
     "dagpu_repair",
     "dagpu_repair_ex",
     "dagpu_square_construct",
@@ -181,6 +183,9 @@ def lib() -> ctypes.CDLL:
         L.dagpu_square_build.argtypes = [vp, vp, vp, sz, ctypes.c_uint32, ctypes.c_uint32, vp, sz, vp, vp]
         L.dagpu_repair_batch_device_ex.argtypes = [vp, ctypes.c_uint32, sz, vp, vp, vp, vp, vp, vp,
                                                    vp, vp]
+        L.dagpu_repair_start.argtypes = [vp, ctypes.c_uint32, sz, vp, vp, vp, vp, vp, vp, vp,
+                                         ctypes.POINTER(ctypes.c_uint64)]
+        L.dagpu_repair_join.argtypes = [vp, ctypes.c_uint64, vp]
         L.dagpu_dah_hash.argtypes = [vp, vp, sz, vp]
         L.dagpu_nmt_roots.argtypes = [vp, sz, vp, vp, sz, ctypes.c_int, vp, ctypes.c_int, vp, vp]
         L.dagpu_wrapper_roots.argtypes = [vp, ctypes.c_uint64, sz, vp, vp, vp, sz, vp, vp]

@@ -114,8 +114,30 @@ class DeviceSquares:
             _abi.addr(self.row_roots), _abi.addr(self.col_roots), _abi.addr(status), _abi.addr(byz),
             _abi.addr(workspace), _stream_handle(stream)))
 
-    def repair_workspace(self) -> torch.Tensor:
-        ws = self.ctx._L.dagpu_repair_workspace_size(self.k, self.n)
+    def repair_start(self, present: torch.Tensor, status: torch.Tensor, workspace: torch.Tensor,
+                     stream: Optional[torch.cuda.Stream] = None, first: int = 0, count: Optional[int] = None) -> int:
+        """dagpu_repair_start on squares [first, first + count) (default all):
+        returns at once with a handle for repair_join; the crossword runs on a
+        library worker thread and stream forked from `stream`.  present /
+        status / workspace as repair() (status and present indexed from
+        `first`; workspace sized for `count` squares)."""
+        import ctypes
+        count = self.n - first if count is None else count
+        w = 2 * self.k
+        h = ctypes.c_uint64(0)
+        self._ck(self.ctx._L.dagpu_repair_start(
+            self.ctx.handle, self.k, count, self.eds.data_ptr() + first * w * w * 512,
+            present.data_ptr() + first * w * w, self.row_roots.data_ptr() + first * w * ROOT,
+            self.col_roots.data_ptr() + first * w * ROOT, status.data_ptr() + 4 * first, workspace.data_ptr(),
+            _stream_handle(stream), ctypes.byref(h)))
+        return h.value
+
+    def repair_join(self, handle: int, stream: Optional[torch.cuda.Stream] = None) -> None:
+        """dagpu_repair_join: `stream` waits for the started repair."""
+        self._ck(self.ctx._L.dagpu_repair_join(self.ctx.handle, handle, _stream_handle(stream)))
+
+    def repair_workspace(self, count: Optional[int] = None) -> torch.Tensor:
+        ws = self.ctx._L.dagpu_repair_workspace_size(self.k, self.n if count is None else count)
         return torch.empty((ws,), dtype=torch.uint8, device=self.eds.device)
 
     def roots(self, stream: Optional[torch.cuda.Stream] = None) -> None:

@@ -392,6 +392,10 @@ void dagpu_destroy(dagpu_ctx* c) {
   if (!c) return;
   if (thread_err().ctx == c && thread_err().gen == c->gen) thread_err() = ThreadErr{};
   (void)hipSetDevice(c->device);
+  for (auto& sl : c->async_slot) {  // started Repairs finish first
+    if (sl.worker.joinable()) sl.worker.join();
+    if (sl.stream) (void)hipStreamSynchronize(sl.stream);
+  }
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
   c->h_out.release();
@@ -416,6 +420,11 @@ void dagpu_destroy(dagpu_ctx* c) {
   for (auto& cs : c->side)
     for (hipStream_t x : {cs.rs, cs.rs_hi, cs.nmt})
       if (x) (void)hipStreamDestroy(x);
+  for (auto& sl : c->async_slot) {
+    if (sl.fork) (void)hipEventDestroy(sl.fork);
+    if (sl.finished) (void)hipEventDestroy(sl.finished);
+    if (sl.stream) (void)hipStreamDestroy(sl.stream);
+  }
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1099,7 +1108,10 @@ int exact_repair(dagpu_ctx* ctx, uint32_t k, size_t n, size_t sq, uint8_t* d_eds
 struct Mailbox {
   dagpu_ctx* c;
   void* p = nullptr;
+  Mailbox(const Mailbox&) = delete;
+  Mailbox(Mailbox&& o) noexcept : c(o.c), p(o.p) { o.p = nullptr; }
   explicit Mailbox(dagpu_ctx* c_) : c(c_) {
+    if (!c) return;  // (an empty mailbox: read_small then copies straight to the destination)
     {
       std::lock_guard<std::mutex> g(c->mb_mu);
       if (!c->mailboxes.empty()) {
@@ -1132,9 +1144,12 @@ hipError_t read_small(void* dst, const void* src, size_t bytes, Mailbox& mb, hip
 // rsmt2d Repair for n same-k squares resident on the device (see repair.hip).
 // d_byz (optional, n * 4 int32): failing axis per square; asking for it makes
 // the call resolve crossword failures in rsmt2d's order (exact_repair).
+// mb_in (optional): a mailbox the caller took already (the asynchronous path
+// allocates nothing on its worker thread: an allocation there could wait for
+// a stream that is itself waiting for the worker).
 int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t* d_present,
                   const uint8_t* d_rr, const uint8_t* d_cr, int32_t* d_status, int32_t* d_byz, void* d_ws,
-                  hipStream_t s) {
+                  hipStream_t s, Mailbox* mb_in = nullptr) {
   const long w = 2L * k;
   RepairWs r = carve_repair(k, n, d_ws);
   HIP_TRY(ctx, hipMemcpyAsync(r.p0, d_present, n * w * w, hipMemcpyDeviceToDevice, s));
@@ -1196,7 +1211,8 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
     HIP_TRY(ctx, hipMemsetAsync(r.nodefer, 0, n * sizeof(int32_t), s));
   }
   const int max_rounds = 4 * (int)w + 4;
-  Mailbox mb(ctx);
+  Mailbox mb_own(mb_in ? nullptr : ctx);
+  Mailbox& mb = mb_in ? *mb_in : mb_own;
   for (int pass = 0; pass < 2; pass++) {
     long deferred_total = 0;
     int last_ax = -1;
@@ -1333,11 +1349,9 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
     for (size_t i = 0; i < n; i++) {
       if (!chk[i]) continue;
       rerun = true;
-      const int32_t one = 1;
       HIP_TRY(ctx, hipMemcpyAsync(d_present + i * w * w, r.p0 + i * w * w, w * w, hipMemcpyDeviceToDevice, s));
-      HIP_TRY(ctx, hipMemcpyAsync(r.nodefer + i, &one, sizeof one, hipMemcpyHostToDevice, s));
+      HIP_TRY(ctx, hipMemsetD32Async((hipDeviceptr_t)(r.nodefer + i), 1, 1, s));
     }
-    HIP_TRY(ctx, hipStreamSynchronize(s));  // (the host-side `one` above)
     if (!rerun) break;
   }
   // verify every complete axis against the given roots
@@ -1389,12 +1403,102 @@ int dagpu_repair_batch_device_ex(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* 
                        (hipStream_t)stream);
 }
 
+}  // extern "C"
+
+namespace {
+
+hipError_t async_init_slot(dagpu_ctx::AsyncSlot& sl) {
+  hipError_t e = hipSuccess;
+  if (!sl.stream && (e = hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking)) != hipSuccess) return e;
+  if (!sl.fork && (e = hipEventCreateWithFlags(&sl.fork, hipEventDisableTiming)) != hipSuccess) return e;
+  if (!sl.finished && (e = hipEventCreateWithFlags(&sl.finished, hipEventDisableTiming)) != hipSuccess) return e;
+  return e;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Asynchronous Repair: the crossword's host decisions (one counter read per
+// round) run on a library worker thread that queues the kernels on a stream
+// of its own, forked from `stream` at the call; dagpu_repair_join then makes a
+// stream wait for the finished repair.  Nothing on the device ever waits for
+// work queued later: a first design whose caller stream waited on a signal
+// word the worker would write later (hipStreamWaitValue32) hung inside the
+// test suite although the primitives pass alone (tools/waitvalue_probe.hip) --
+// with GPU_MAX_HW_QUEUES = 4 two streams can share one hardware queue, and a
+// wait ahead of its own release in that queue never passes.  So a join blocks
+// the calling thread until the worker has queued its last command, and calls
+// started back to back (e.g. slices of a batch) run side by side
+// (profiles/repair_async_r04.log).
+int dagpu_repair_start(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t* d_present,
+                       const uint8_t* d_row_roots, const uint8_t* d_col_roots, int32_t* d_status,
+                       void* d_workspace, void* stream, uint64_t* handle) {
+  if (!ctx || !handle || !d_eds || !d_present || !d_row_roots || !d_col_roots || !d_status || !d_workspace)
+    return DAGPU_ERR_ARG;
+  *handle = 0;
+  int rc = check_k(ctx, k);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  std::lock_guard<std::mutex> g(ctx->async_mu);
+  int si = -1;
+  for (int i = 0; i < dagpu_ctx::kAsyncSlots && si < 0; i++)
+    if (!ctx->async_slot[i].busy) si = i;
+  if (si < 0) return set_err(ctx, DAGPU_ERR_ARG, "too many repairs started and not joined");
+  dagpu_ctx::AsyncSlot& sl = ctx->async_slot[si];
+  HIP_TRY(ctx, async_init_slot(sl));
+  HIP_TRY(ctx, launch_rs_prepare((int)k));  // first-use table uploads here, not on the worker
+  HIP_TRY(ctx, hipEventRecord(sl.fork, s));
+  if (++ctx->async_gen == 0) ++ctx->async_gen;
+  sl.busy = true;
+  sl.gen = ctx->async_gen;
+  sl.rc = DAGPU_OK;
+  auto mb = std::make_shared<Mailbox>(ctx);
+  hipStream_t ws = sl.stream;
+  hipEvent_t fork = sl.fork, fin = sl.finished;
+  int* rc_out = &sl.rc;
+  const int dev = ctx->device;
+  sl.worker = std::thread([=]() {
+    (void)hipSetDevice(dev);
+    int r = hipStreamWaitEvent(ws, fork, 0) == hipSuccess ? DAGPU_OK : DAGPU_ERR_DEVICE;
+    if (r == DAGPU_OK && n)
+      r = repair_device(ctx, k, n, d_eds, d_present, d_row_roots, d_col_roots, d_status, nullptr, d_workspace, ws,
+                        mb.get());
+    if (r != DAGPU_OK) (void)hipMemsetD32Async((hipDeviceptr_t)d_status, (int)DAGPU_ERR_DEVICE, n, ws);
+    (void)hipEventRecord(fin, ws);
+    *rc_out = r;
+  });
+  *handle = ((uint64_t)sl.gen << 8) | (uint64_t)si;
+  return DAGPU_OK;
+}
+
+int dagpu_repair_join(dagpu_ctx* ctx, uint64_t handle, void* stream) {
+  if (!ctx) return DAGPU_ERR_ARG;
+  const int si = (int)(handle & 0xFF);
+  std::lock_guard<std::mutex> g(ctx->async_mu);
+  if (si >= dagpu_ctx::kAsyncSlots || !ctx->async_slot[si].busy ||
+      ctx->async_slot[si].gen != (uint32_t)(handle >> 8))
+    return set_err(ctx, DAGPU_ERR_ARG, "unknown or already joined repair handle");
+  dagpu_ctx::AsyncSlot& sl = ctx->async_slot[si];
+  if (sl.worker.joinable()) sl.worker.join();  // its last command is queued
+  sl.busy = false;
+  HIP_TRY(ctx, hipStreamWaitEvent((hipStream_t)stream, sl.finished, 0));
+  return sl.rc;
+}
+
+// Start + join on the same stream: returns once every kernel of the repair is
+// queued (the caller's stream then runs them in order with its later work).
 int dagpu_repair_batch_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds,
                               uint8_t* d_present, const uint8_t* d_row_roots,
                               const uint8_t* d_col_roots, int32_t* d_status, void* d_workspace,
                               void* stream) {
-  return dagpu_repair_batch_device_ex(ctx, k, n, d_eds, d_present, d_row_roots, d_col_roots, d_status,
-                                      nullptr, d_workspace, stream);
+  if (!ctx || !d_eds || !d_present || !d_row_roots || !d_col_roots || !d_status || !d_workspace)
+    return DAGPU_ERR_ARG;
+  int rc = check_k(ctx, k);
+  if (rc) return rc;
+  if (n == 0) return DAGPU_OK;
+  return repair_device(ctx, k, n, d_eds, d_present, d_row_roots, d_col_roots, d_status, nullptr, d_workspace,
+                       (hipStream_t)stream);
 }
 
 int dagpu_repair_ex(dagpu_ctx* ctx, uint32_t k, uint8_t* eds, uint8_t* present,

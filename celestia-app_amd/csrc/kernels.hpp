@@ -151,6 +151,10 @@ hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mar
 hipError_t launch_leo16w_encode(int k, const EncodeArgs& a, hipStream_t s);
 hipError_t launch_leo16w_errlocs(const DecodeArgs& a, hipStream_t s);
 hipError_t launch_leo16w_decode_only(const DecodeArgs& a, hipStream_t s, bool mark_present);
+// one-time per-device setup (tables, LDS attributes) of the codec of width k,
+// so that later launches allocate and upload nothing
+hipError_t launch_rs_prepare(int k);
+hipError_t leo16w_prepare();
 hipError_t launch_rs_encode(int k, const EncodeArgs& a, hipStream_t s);
 hipError_t launch_rs_errlocs(const DecodeArgs& a, hipStream_t s);
 hipError_t launch_rs_decode_only(const DecodeArgs& a, hipStream_t s, bool mark_present);

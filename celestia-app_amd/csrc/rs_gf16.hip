@@ -1469,6 +1469,14 @@ hipError_t launch_errloc_heads(const DecodeArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+hipError_t launch_rs_prepare(int k) {
+  if (k <= 128) return hipSuccess;  // GF(2^8): constexpr tables
+  hipError_t e = ensure_tables();
+  if (e == hipSuccess) e = dec_lds_attr();
+  if (e == hipSuccess) e = leo16w_prepare();
+  return e;
+}
+
 // Field dispatch used by the host runtime: GF(2^8) for 2k <= 256, else GF(2^16).
 hipError_t launch_rs_encode(int k, const EncodeArgs& a, hipStream_t s) {
   return k <= 128 ? launch_leo8_encode(k, a, s) : launch_leo16_encode(k, a, s);

@@ -599,6 +599,21 @@ bool wide_k_ok(int k) { return k >= 256 && k <= kMaxK && (k & (k - 1)) == 0; }
 
 }  // namespace
 
+hipError_t leo16w_prepare() {
+  WideTabs T;
+  hipError_t e = tables(T);
+  // LDS attributes of every instantiation (hipFuncSetAttribute at launch time otherwise)
+  const size_t big = 2 * 16384 * 4;  // <= the largest slice any width asks for
+  if (e == hipSuccess) e = lds_attr(leo16w_encode_kernel<8, 4>, lds_bytes(2048, 8));
+  if (e == hipSuccess) e = lds_attr(leo16w_encode_kernel<2, 2>, lds_bytes(4096, 2));
+  if (e == hipSuccess) e = lds_attr(leo16w_encode_kernel<1, 1>, big);
+  if (e == hipSuccess) e = lds_attr(leo16w_decode_kernel<8, 4>, lds_bytes(2048, 8));
+  if (e == hipSuccess) e = lds_attr(leo16w_decode_kernel<2, 2>, lds_bytes(4096, 2));
+  if (e == hipSuccess) e = lds_attr(leo16w_decode_kernel<1, 1>, big);
+  if (e == hipSuccess) e = lds_attr(leo16w_errlocs_kernel, (size_t)4 * 2 * kMaxK);
+  return e;
+}
+
 hipError_t launch_leo16w_encode(int k, const EncodeArgs& a, hipStream_t s) {
   if (!wide_k_ok(k) || a.shard_bytes % 64) return hipErrorInvalidValue;
   if (a.reverse && !a.out_present) return hipErrorInvalidValue;

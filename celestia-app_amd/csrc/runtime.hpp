@@ -7,8 +7,10 @@
 #include <stdio.h>
 
 #include <atomic>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -118,6 +120,22 @@ struct dagpu_ctx {
   // the last Repair call's schedule (dagpu_repair_stats), under prof_mu
   int64_t rep_stats[DAGPU_REPAIR_STATS] = {};
   uint64_t prof_n[DAGPU_PROFILE_KERNELS] = {};
+  // Started Repairs (dagpu_repair_start / dagpu_repair_join): each runs its
+  // host-driven crossword on a worker thread and a stream of its slot, forked
+  // from the caller's stream; the join waits for the worker (all commands
+  // queued) and makes a stream wait for the slot's `finished` event.
+  static constexpr int kAsyncSlots = 64;
+  struct AsyncSlot {
+    bool busy = false;
+    uint32_t gen = 0;
+    int rc = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t fork = nullptr, finished = nullptr;
+    std::thread worker;
+  };
+  std::mutex async_mu;
+  uint32_t async_gen = 0;
+  AsyncSlot async_slot[kAsyncSlots];
 };
 
 constexpr size_t kSS = dagpu::kShareSize;

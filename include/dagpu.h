@@ -178,8 +178,9 @@ int dagpu_repair_ex(dagpu_ctx* ctx, uint32_t k, uint8_t* eds, uint8_t* present,
  * d_present = n * (2k)^2 flags (updated in place), expected roots as produced by
  * dagpu_extend_batch_device.  d_status gets one dagpu_status per square.
  * d_workspace: dagpu_repair_workspace_size(k, n) bytes.  Enqueued on `stream`;
- * the call synchronises once per crossword round to read its counters (and
- * once more when deferred axes need their codeword check).  Axes whose data
+ * the call reads the round counters on the host once per crossword round (and
+ * once more when deferred axes need their codeword check), so it returns when
+ * its last command is queued.  Axes whose data
  * half is complete are re-encoded instead of decoded, and axes whose parity
  * half is complete are rebuilt by the inverse transform (same bytes);
  * DAGPU_REPAIR_FILL=0 in the environment selects the plain decoder schedule.
@@ -197,6 +198,21 @@ int dagpu_repair_batch_device_ex(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* 
                                  uint8_t* d_present, const uint8_t* d_row_roots,
                                  const uint8_t* d_col_roots, int32_t* d_status, int32_t* d_byz,
                                  void* d_workspace, void* stream);
+
+/* dagpu_repair_batch_device split in two: dagpu_repair_start returns at once
+ * (*handle names the repair); a library worker thread makes the crossword's
+ * host decisions and queues its kernels on a stream of its own, forked from
+ * `stream` at the call (work already queued there runs first).
+ * dagpu_repair_join(ctx, handle, stream2) waits until the worker has queued
+ * its last command and makes stream2 wait for the repair; it returns the
+ * repair's call status (per-square results in d_status).  Repairs started back
+ * to back (slices of a batch, squares of several blocks) run side by side; a
+ * context serves 64 started, not yet joined repairs.  The buffers must stay
+ * valid until the joined stream has passed the repair. */
+int dagpu_repair_start(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t* d_present,
+                       const uint8_t* d_row_roots, const uint8_t* d_col_roots, int32_t* d_status,
+                       void* d_workspace, void* stream, uint64_t* handle);
+int dagpu_repair_join(dagpu_ctx* ctx, uint64_t handle, void* stream);
 
 /* Per-kernel timing with HIP events recorded on the launch stream around each
  * kernel the pipeline enqueues (for bench.py's roofline; off by default).
