@@ -748,7 +748,9 @@ __device__ __forceinline__ void mul16_by(uint32_t& xlo, uint32_t& xhi, const uin
 // wave -- one exp() gather per lane, 4 DPP ORs and 16 v_readlane per element --
 // and the k = 512 decoder waited on memory half of its cycles).
 // out[G] byte e2 = low byte of (e2 << 2G) * exp(lm), out[8 + G] its high byte.
-__device__ __forceinline__ void mul16_table_to(uint32_t* out, uint32_t lm) {
+// zero: the all-zero table (multiply by 0: the decoders' premultiply of a
+// missing shard, whose bytes are then never selected out of the loaded word)
+__device__ __forceinline__ void mul16_table_to(uint32_t* out, uint32_t lm, bool zero = false) {
   uint32_t lo[8], hi[8];
 #pragma unroll
   for (int G = 0; G < 8; G++) {
@@ -756,7 +758,7 @@ __device__ __forceinline__ void mul16_table_to(uint32_t* out, uint32_t lm) {
 #pragma unroll
     for (int e2 = 1; e2 < 4; e2++) {
       const uint32_t x = (uint32_t)e2 << (2 * G);
-      const uint32_t p = mul16_prod(x, (uint32_t)g_log16[x], lm);
+      const uint32_t p = zero ? 0u : mul16_prod(x, (uint32_t)g_log16[x], lm);
       lo[G] |= (p & 0xFFu) << (8 * e2);
       hi[G] |= (p >> 8) << (8 * e2);
     }
@@ -849,14 +851,13 @@ __global__ __launch_bounds__(kDecN) __attribute__((amdgpu_waves_per_eu(2, 2))) v
     const uint32_t so = (uint32_t)shard * (uint32_t)a.shard_stride;
     const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(rsrc, cl, so, 0);
     const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rsrc, cl + 32u, so, 0);
-    const bool p = (pm >> j) & 1;
-    w.lo[j] = p ? lo : 0u;
-    w.hi[j] = p ? hi : 0u;
+    w.lo[j] = lo;  // a missing shard's bytes: zeroed by its premultiply table
+    w.hi[j] = hi;
   }
   // work *= errLocs: thread i builds element i's tables in LDS (the premultiply
   // one in the transpose buffer, free until the first transpose; the erasure
   // one kept to the end), each wave then reads its 64 elements' tables
-  mul16_table_to(lds + threadIdx.x * 16, my_err);
+  mul16_table_to(lds + threadIdx.x * 16, my_err, !((pm >> lane) & 1));
   mul16_table_to(post_tab + threadIdx.x * 16, kMod16 - my_err);
   __syncthreads();
 #pragma unroll
@@ -904,11 +905,16 @@ __global__ __launch_bounds__(kDecN) __attribute__((amdgpu_waves_per_eu(2, 2))) v
 #pragma unroll
   for (int j = 0; j < 32; j++) fft2_16(w, j, j + 32, 64 * q + 31);  // second sub-layer (bit 5)
   fft16_block<8>(w, 64 * q);                                         // bits 4 .. 0
-  // erased shards = work * (65535 - errLocs); only active lanes store
+  // erased shards = work * (65535 - errLocs); only active lanes store.  pm and
+  // q made opaque here: otherwise the 64 per-element conditions and offsets
+  // of the load loop are kept live through the whole kernel (SGPR spills)
+  uint64_t pm_e = pm;
+  int q_e = q;
+  asm volatile("" : "+s"(pm_e), "+s"(q_e));
 #pragma unroll
   for (int j = 0; j < 64; j++) {
-    if ((pm >> j) & 1) continue;  // uniform
-    const int i = 64 * q + j;
+    if ((pm_e >> j) & 1) continue;  // uniform
+    const int i = 64 * q_e + j;
     const int shard = i < K ? K + i : i - K;
     uint32_t t[16];
     mul16_table_from(post_tab, i, t);
@@ -941,17 +947,59 @@ __global__ __launch_bounds__(kDecN) __attribute__((amdgpu_waves_per_eu(2, 2))) v
 constexpr int kDec1k = 1024;
 
 // y * c for a packed dword, t = c's 16-dword product table (t[G] low bytes,
-// t[8 + G] high bytes of (e2 << 2G) * c, e2 = 0..3)
-__device__ __forceinline__ uint32_t mulp_g(uint32_t y, const uint32_t* t, int G) {
-  const uint32_t sg = (y >> (G < 4 ? 2 * G : 16 + 2 * (G - 4))) & 0x0303u;
-  const uint32_t sel = (sg | (sg << 16)) + 0x04040000u;  // bytes 2,3 select from t[8 + G]
-  return __builtin_amdgcn_perm(t[8 + G], t[G], sel);
+// t[8 + G] high bytes of (e2 << 2G) * c, e2 = 0..3).  One selector serves two
+// bit groups: (y >> 2G) & 0x03030303 holds group G of both symbols' low bytes
+// (bytes 0, 1) and group G + 4 of their high bytes (bytes 2, 3); with 4 added
+// to bytes 2, 3 they index src0, so perm(t[G + 4], t[G], sel) looks up group G
+// of the two symbols in t[G] and group G + 4 in t[G + 4] at once.  Summed over
+// G = 0..3, bytes 0, 1 hold the low-byte products of the low groups and bytes
+// 2, 3 those of the high groups (the same for the high-byte tables); two byte
+// permutes fold the halves: 22 ops per 2 symbols (36 with one group per perm).
+__device__ __forceinline__ uint32_t mulp_sel(uint32_t y, int G) {
+  return __builtin_amdgcn_bitop3_b32(y >> (2 * G), 0x03030303u, 0x04040000u, 0xEA);  // (a & b) | c
 }
-__device__ __forceinline__ uint32_t mulp(uint32_t y, const uint32_t* t) {
-  uint32_t acc = xor3(mulp_g(y, t, 0), mulp_g(y, t, 1), mulp_g(y, t, 2));
-  acc = xor3(acc, mulp_g(y, t, 3), mulp_g(y, t, 4));
-  acc = xor3(acc, mulp_g(y, t, 5), mulp_g(y, t, 6));
-  return acc ^ mulp_g(y, t, 7);
+// acc ^ y * c; T: anything indexable by 0..15 (the table of c)
+template <class T>
+__device__ __forceinline__ uint32_t mulp_add_t(uint32_t acc, uint32_t y, const T& t) {
+  const uint32_t s0 = mulp_sel(y, 0), s1 = mulp_sel(y, 1), s2 = mulp_sel(y, 2), s3 = mulp_sel(y, 3);
+  const uint32_t a = xor3(xor3(__builtin_amdgcn_perm(t[4], t[0], s0), __builtin_amdgcn_perm(t[5], t[1], s1),
+                               __builtin_amdgcn_perm(t[6], t[2], s2)),
+                          __builtin_amdgcn_perm(t[7], t[3], s3), 0u);
+  const uint32_t b = xor3(xor3(__builtin_amdgcn_perm(t[12], t[8], s0), __builtin_amdgcn_perm(t[13], t[9], s1),
+                               __builtin_amdgcn_perm(t[14], t[10], s2)),
+                          __builtin_amdgcn_perm(t[15], t[11], s3), 0u);
+  // acc ^ [a0 ^ a2, a1 ^ a3, b0 ^ b2, b1 ^ b3]
+  return xor3(acc, __builtin_amdgcn_perm(b, a, 0x05040100u), __builtin_amdgcn_perm(b, a, 0x07060302u));
+}
+__device__ __forceinline__ uint32_t mulp(uint32_t y, const uint32_t (&t)[16]) { return mulp_add_t(0u, y, t); }
+
+// A skew position's table for the packed multiplies, loaded per radix-4 unit:
+// the position is made opaque so that each unit loads its tables afresh
+// (scalar-cache hits) instead of the compiler keeping every table of the
+// kernel live (1,100 SGPR spills through v_writelane / v_readlane).
+// a wave-uniform value the compiler cannot see through: values derived from it
+// in one phase are not kept live (in SGPRs, then spilled) for the next
+__device__ __forceinline__ int opaque_s(int x) {
+  asm volatile("" : "+s"(x));
+  return x;
+}
+
+struct PTab {
+  uint32_t s[16];
+  __device__ __forceinline__ uint32_t operator[](int i) const { return s[i]; }
+};
+__device__ __forceinline__ PTab ptab(int pos) {
+  const uint4* t = (const uint4*)(g_ptab16 + pos * 16);
+  PTab p;
+#pragma unroll
+  for (int h = 0; h < 4; h++) {
+    const uint4 x = t[h];
+    p.s[4 * h] = x.x;
+    p.s[4 * h + 1] = x.y;
+    p.s[4 * h + 2] = x.z;
+    p.s[4 * h + 3] = x.w;
+  }
+  return p;
 }
 
 struct W1k {
@@ -959,13 +1007,68 @@ struct W1k {
 };
 
 // ifftDIT2: y ^= x; x ^= y * skew[pos]     fftDIT2: x ^= y * skew[pos]; y ^= x
-__device__ __forceinline__ void ifft2_p(W1k& w, int i, int j, int pos) {
+__device__ __forceinline__ void ifft2_p(W1k& w, int i, int j, const PTab& t) {
   w.v[j] ^= w.v[i];
-  w.v[i] ^= mulp(w.v[j], g_ptab16 + pos * 16);
+  w.v[i] = mulp_add_t(w.v[i], w.v[j], t);
 }
-__device__ __forceinline__ void fft2_p(W1k& w, int i, int j, int pos) {
-  w.v[i] ^= mulp(w.v[j], g_ptab16 + pos * 16);
+__device__ __forceinline__ void fft2_p(W1k& w, int i, int j, const PTab& t) {
+  w.v[i] = mulp_add_t(w.v[i], w.v[j], t);
   w.v[j] ^= w.v[i];
+}
+
+// Radix-4 steps layer by layer: every butterfly of one skew position, then
+// the next position, so that one 16-SGPR table is live at a time (radix-4
+// units with their three tables live across the unit spilled ~850 SGPRs).
+// IFFT: (i, i+D) at p01, (i+2D, i+3D) at p23, then (i, i+2D), (i+D, i+3D) at
+// p02; i over N butterflies starting at s0 with stride ST.
+template <int N, int ST, int D>
+__device__ __forceinline__ void ifftp_r4(W1k& w, int s0, int p01, int p02, int p23) {
+  {
+    const PTab t = ptab(p01);
+#pragma unroll
+    for (int u = 0; u < N; u++) ifft2_p(w, s0 + ST * u, s0 + ST * u + D, t);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  {
+    const PTab t = ptab(p23);
+#pragma unroll
+    for (int u = 0; u < N; u++) ifft2_p(w, s0 + ST * u + 2 * D, s0 + ST * u + 3 * D, t);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  {
+    const PTab t = ptab(p02);
+#pragma unroll
+    for (int u = 0; u < N; u++) {
+      ifft2_p(w, s0 + ST * u, s0 + ST * u + 2 * D, t);
+      ifft2_p(w, s0 + ST * u + D, s0 + ST * u + 3 * D, t);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+// FFT: (i, i+2D), (i+D, i+3D) at p02, then (i, i+D) at p01, (i+2D, i+3D) at p23
+template <int N, int ST, int D>
+__device__ __forceinline__ void fftp_r4(W1k& w, int s0, int p01, int p02, int p23) {
+  {
+    const PTab t = ptab(p02);
+#pragma unroll
+    for (int u = 0; u < N; u++) {
+      fft2_p(w, s0 + ST * u, s0 + ST * u + 2 * D, t);
+      fft2_p(w, s0 + ST * u + D, s0 + ST * u + 3 * D, t);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  {
+    const PTab t = ptab(p01);
+#pragma unroll
+    for (int u = 0; u < N; u++) fft2_p(w, s0 + ST * u, s0 + ST * u + D, t);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  {
+    const PTab t = ptab(p23);
+#pragma unroll
+    for (int u = 0; u < N; u++) fft2_p(w, s0 + ST * u + 2 * D, s0 + ST * u + 3 * D, t);
+  }
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 // block layout, decoder IFFT radix-4 steps dist D..16 (skew index iend - 1)
@@ -973,15 +1076,8 @@ template <int D>
 __device__ __forceinline__ void ifftp_block(W1k& w, int base) {
 #pragma unroll
   for (int r = 0; r < 64; r += 4 * D) {
-    const int p01 = base + r + D, p02 = p01 + D, p23 = p01 + 2 * D;
-#pragma unroll
-    for (int i = r; i < r + D; i++) {
-      ifft2_p(w, i, i + D, p01);
-      ifft2_p(w, i + 2 * D, i + 3 * D, p23);
-      ifft2_p(w, i, i + 2 * D, p02);
-      ifft2_p(w, i + D, i + 3 * D, p02);
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    const int b = opaque_s(base);
+    ifftp_r4<D, 1, D>(w, r, b + r + D, b + r + 2 * D, b + r + 3 * D);
   }
   if constexpr (D * 16 <= 64) ifftp_block<D * 4>(w, base);
 }
@@ -991,15 +1087,8 @@ __device__ __forceinline__ void fftp_block(W1k& w, int base) {
 #pragma unroll
   for (int r = 0; r < 64; r += 4 * DIST) {
     const int iend = r + DIST;
-    const int p01 = base + iend - 1, p02 = base + iend + DIST - 1, p23 = base + iend + 2 * DIST - 1;
-#pragma unroll
-    for (int i = r; i < r + DIST; i++) {
-      fft2_p(w, i, i + 2 * DIST, p02);
-      fft2_p(w, i + DIST, i + 3 * DIST, p02);
-      fft2_p(w, i, i + DIST, p01);
-      fft2_p(w, i + 2 * DIST, i + 3 * DIST, p23);
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    const int b = opaque_s(base);
+    fftp_r4<DIST, 1, DIST>(w, r, b + iend - 1, b + iend + DIST - 1, b + iend + 2 * DIST - 1);
   }
   if constexpr (DIST >= 4) fftp_block<DIST / 4>(w, base);
 }
@@ -1059,7 +1148,10 @@ __global__ __launch_bounds__(kDec1k) __attribute__((amdgpu_waves_per_eu(4, 4))) 
   const int lane = threadIdx.x & 63;
   const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // lane: 64-B block (lane >> 4) of this 256-B piece, symbols 2 (lane & 15) and +1
-  const uint32_t col = (uint32_t)half * 256u + (uint32_t)(lane >> 4) * 64u + (uint32_t)(lane & 15) * 2u;
+  // (memory: lane pair 2m, 2m+1 moves the dword of low bytes and the dword of
+  // high bytes of symbols 4m .. 4m+3, even lane the low one)
+  const bool odd = lane & 1;
+  const uint32_t wcol = (uint32_t)half * 256u + (uint32_t)(lane >> 4) * 64u + (uint32_t)(lane & 14) * 2u + (odd ? 32u : 0u);
   const auto rsrc = make_rsrc(a.data + sq * a.sq_stride + vec * a.vec_stride);
   const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
   const uint16_t* err = (const uint16_t*)(a.err + err_vec(a, v) * rs_err_bytes(K));
@@ -1068,25 +1160,31 @@ __global__ __launch_bounds__(kDec1k) __attribute__((amdgpu_waves_per_eu(4, 4))) 
   const uint64_t pm = __builtin_amdgcn_ballot_w64(pres[(long)my_shard * a.p_shard_stride] != 0);
   const uint32_t my_err = err[my_i];
   W1k w;
+  const int q_ld = opaque_s(q);
 #pragma unroll
   for (int j = 0; j < 64; j++) {
-    const int i = 64 * q + j;
+    const int i = 64 * q_ld + j;
     const int shard = i < K ? K + i : i - K;
     const uint32_t so = (uint32_t)shard * (uint32_t)a.shard_stride;
-    const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b16(rsrc, col, so, 0);
-    const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b16(rsrc, col + 32u, so, 0);
-    w.v[j] = ((pm >> j) & 1) ? (lo | (hi << 16)) : 0u;
+    // one dword per lane (even lanes the low bytes, odd lanes the high bytes
+    // of symbols 4m .. 4m+3), paired with the neighbour lane's dword:
+    // one VGPR per element in flight (two 16-bit loads per element kept two
+    // and spilled the load loop, serialising its loads)
+    const uint32_t mine = __builtin_amdgcn_raw_buffer_load_b32(rsrc, wcol, so, 0);
+    const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mine, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    w.v[j] = odd ? __builtin_amdgcn_perm(mine, other, 0x07060302u) : __builtin_amdgcn_perm(other, mine, 0x05040100u);
   }
   // work *= errLocs: thread i builds element i's tables in LDS (the premultiply
   // one in the transpose buffer, free until the first transpose; the erasure
   // one kept to the end), each wave then reads its 64 elements' tables
-  mul16_table_to(lds + threadIdx.x * 16, my_err);
+  mul16_table_to(lds + threadIdx.x * 16, my_err, !((pm >> lane) & 1));
   mul16_table_to(post_tab + threadIdx.x * 16, kMod16 - my_err);
   __syncthreads();
+  const int q_pm = opaque_s(q);
 #pragma unroll
   for (int j = 0; j < 64; j++) {
     uint32_t t[16];
-    mul16_table_from(lds, 64 * q + j, t);
+    mul16_table_from(lds, 64 * q_pm + j, t);
     w.v[j] = mulp(w.v[j], t);
     __builtin_amdgcn_sched_barrier(0);  // one element's table live at a time
   }
@@ -1095,63 +1193,44 @@ __global__ __launch_bounds__(kDec1k) __attribute__((amdgpu_waves_per_eu(4, 4))) 
   ifftp_block<1>(w, -1 + 64 * q);  // bits 0-5
   xposep(w, lds, q, lane);
 #pragma unroll
-  for (int hr = 0; hr < 4; hr++) {  // radix-4 dist 64 (bits 6, 7), r = 256 hr
-    const int p01 = 256 * hr + 63, p02 = p01 + 64, p23 = p01 + 128;
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-      const int s0 = 16 * hr + b;
-      ifft2_p(w, s0, s0 + 4, p01);
-      ifft2_p(w, s0 + 8, s0 + 12, p23);
-      ifft2_p(w, s0, s0 + 8, p02);
-      ifft2_p(w, s0 + 4, s0 + 12, p02);
-      __builtin_amdgcn_sched_barrier(0);
-    }
+  for (int hr = 0; hr < 4; hr++) {  // radix-4 dist 64 (bits 6, 7), r = 256 hr: slots 16 hr + b, b < 4
+    const int p01 = opaque_s(256 * hr + 63);
+    ifftp_r4<4, 1, 4>(w, 16 * hr, p01, p01 + 64, p01 + 128);
   }
-#pragma unroll
-  for (int s0 = 0; s0 < 16; s0++) {  // radix-4 dist 256 (bits 8, 9)
-    ifft2_p(w, s0, s0 + 16, 255);
-    ifft2_p(w, s0 + 32, s0 + 48, 767);
-    ifft2_p(w, s0, s0 + 32, 511);
-    ifft2_p(w, s0 + 16, s0 + 48, 511);
-    __builtin_amdgcn_sched_barrier(0);
+  {  // radix-4 dist 256 (bits 8, 9): slots s0 < 16
+    const int p01 = opaque_s(255);
+    ifftp_r4<16, 1, 16>(w, 0, p01, p01 + 256, p01 + 512);
   }
   derivativep(w, lds, q, lane);
   // ---- FFT (fftDIT, skew index iend - 1) ----
-#pragma unroll
-  for (int s0 = 0; s0 < 16; s0++) {  // dist 256
-    fft2_p(w, s0, s0 + 32, 511);
-    fft2_p(w, s0 + 16, s0 + 48, 511);
-    fft2_p(w, s0, s0 + 16, 255);
-    fft2_p(w, s0 + 32, s0 + 48, 767);
-    __builtin_amdgcn_sched_barrier(0);
+  {  // dist 256
+    const int p01 = opaque_s(255);
+    fftp_r4<16, 1, 16>(w, 0, p01, p01 + 256, p01 + 512);
   }
 #pragma unroll
   for (int hr = 0; hr < 4; hr++) {  // dist 64
-    const int p01 = 256 * hr + 63, p02 = p01 + 64, p23 = p01 + 128;
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-      const int s0 = 16 * hr + b;
-      fft2_p(w, s0, s0 + 8, p02);
-      fft2_p(w, s0 + 4, s0 + 12, p02);
-      fft2_p(w, s0, s0 + 4, p01);
-      fft2_p(w, s0 + 8, s0 + 12, p23);
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    const int p01 = opaque_s(256 * hr + 63);
+    fftp_r4<4, 1, 4>(w, 16 * hr, p01, p01 + 64, p01 + 128);
   }
   xposep(w, lds, q, lane);
   fftp_block<16>(w, 64 * q);  // dist 16, 4, 1 (bits 5 .. 0)
-  // erased shards = work * (65535 - errLocs)
+  // erased shards = work * (65535 - errLocs); pm, q opaque as in leo16_decode_reg_kernel
+  uint64_t pm_e = pm;
+  int q_e = q;
+  asm volatile("" : "+s"(pm_e), "+s"(q_e));
 #pragma unroll
   for (int j = 0; j < 64; j++) {
-    if ((pm >> j) & 1) continue;  // uniform
-    const int i = 64 * q + j;
+    if ((pm_e >> j) & 1) continue;  // uniform
+    const int i = 64 * q_e + j;
     const int shard = i < K ? K + i : i - K;
     uint32_t t[16];
     mul16_table_from(post_tab, i, t);
     const uint32_t r = mulp(w.v[j], t);
     const uint32_t so = (uint32_t)shard * (uint32_t)a.shard_stride;
-    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(r & 0xFFFFu), rsrc, col, so, 0);
-    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(r >> 16), rsrc, col + 32u, so, 0);
+    // back to [low bytes of 4m..4m+3] (even lane) / [high bytes] (odd lane)
+    const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0xB1, 0xF, 0xF, false);
+    const uint32_t out = odd ? __builtin_amdgcn_perm(r, other, 0x07060302u) : __builtin_amdgcn_perm(other, r, 0x05040100u);
+    __builtin_amdgcn_raw_buffer_store_b32(out, rsrc, wcol, so, 0);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
