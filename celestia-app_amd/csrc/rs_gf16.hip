@@ -453,11 +453,26 @@ __global__ __launch_bounds__(256) void mark_present16_kernel(DecodeArgs a) {
 // Positions < 2m = 1024 cover every encoder skew index (IFFT m-1+iend+2d <
 // 2m, FFT iend-1 < m).  __constant__ so that the wave-uniform table reads
 // become scalar loads into SGPRs (64 KiB, the constant-segment limit).
+// a wave-uniform value the compiler cannot see through: values derived from it
+// in one phase are not kept live (in SGPRs, then spilled) for the next
+__device__ __forceinline__ int opaque_s(int x) {
+  asm volatile("" : "+s"(x));
+  return x;
+}
+
 constexpr int kTabPos = 1024;
 __constant__ uint32_t g_ptab16[kTabPos * 16];
 
-__device__ __forceinline__ void mul16_add(uint32_t& xlo, uint32_t& xhi, uint32_t ylo, uint32_t yhi, int pos) {
-  const uint32_t* t = g_ptab16 + pos * 16;
+// Encoder: the last IFFT layer and the first FFT layer butterfly the same
+// pairs (y ^= x; x ^= y A, then x ^= y B; y ^= x), so x ^= y (A ^ B) with one
+// table for the field element A ^ B: [0] M = 256 (positions 383 / 127), [1]
+// M = 512 (767 / 255) -- the same for the reverse fill, which swaps them.  One
+// multiply fewer per pair, and no selectors kept live from one layer to the
+// next (they spilled ~180 VGPRs).
+__constant__ uint32_t g_ptab16_merged[2 * 16];
+
+__device__ __forceinline__ void mul16_add_t(uint32_t& xlo, uint32_t& xhi, uint32_t ylo, uint32_t yhi,
+                                            const uint32_t* t) {
   uint32_t pl[8], ph[8];
 #pragma unroll
   for (int g = 0; g < 4; g++) {
@@ -471,6 +486,9 @@ __device__ __forceinline__ void mul16_add(uint32_t& xlo, uint32_t& xhi, uint32_t
   // 8 products + x per output byte plane: four 3-input XORs
   xlo = xor3(xor3(xor3(xlo, pl[0], pl[1]), xor3(pl[2], pl[3], pl[4]), pl[5]), pl[6], pl[7]);
   xhi = xor3(xor3(xor3(xhi, ph[0], ph[1]), xor3(ph[2], ph[3], ph[4]), ph[5]), ph[6], ph[7]);
+}
+__device__ __forceinline__ void mul16_add(uint32_t& xlo, uint32_t& xhi, uint32_t ylo, uint32_t yhi, int pos) {
+  mul16_add_t(xlo, xhi, ylo, yhi, g_ptab16 + pos * 16);
 }
 
 struct W16 {
@@ -490,6 +508,15 @@ __device__ __forceinline__ void fft2_16(W16& w, int i, int j, int pos) {
   w.hi[j] ^= w.hi[i];
 }
 
+// the merged last-IFFT / first-FFT butterfly: y ^= x; x ^= y (A ^ B); y ^= x
+__device__ __forceinline__ void ifft_fft2_16(W16& w, int i, int j, const uint32_t* t) {
+  w.lo[j] ^= w.lo[i];
+  w.hi[j] ^= w.hi[i];
+  mul16_add_t(w.lo[i], w.hi[i], w.lo[j], w.hi[j], t);
+  w.lo[j] ^= w.lo[i];
+  w.hi[j] ^= w.hi[i];
+}
+
 // Block layout, encoder IFFT radix-4 steps with dist D..16 (bits 0-5);
 // base = m - 1 + 64 q (ifftDITEncoder skew index m - 1 + iend).
 template <int D>
@@ -504,6 +531,8 @@ __device__ __forceinline__ void ifft16_block(W16& w, int base) {
       ifft2_16(w, i, i + 2 * D, p02);
       ifft2_16(w, i + D, i + 3 * D, p02);
     }
+    // per unit: otherwise every table of the block is loaded up front (SGPR spills)
+    __builtin_amdgcn_sched_barrier(0);
   }
   if constexpr (D * 16 <= 64) ifft16_block<D * 4>(w, base);
 }
@@ -524,12 +553,16 @@ __device__ __forceinline__ void fft16_block(W16& w, int base) {
       fft2_16(w, i, i + DIST, p01);
       fft2_16(w, i + 2 * DIST, i + 3 * DIST, p23);
     }
+    __builtin_amdgcn_sched_barrier(0);  // as in ifft16_block
   }
   if constexpr (DIST >= 4) {
     fft16_block<DIST / 4>(w, base);
   } else if constexpr (DIST == 2) {
 #pragma unroll
-    for (int r = 0; r < 64; r += 2) fft2_16(w, r, r + 1, base + r);
+    for (int r = 0; r < 64; r += 2) {
+      fft2_16(w, r, r + 1, base + r);
+      if (r % 8 == 6) __builtin_amdgcn_sched_barrier(0);
+    }
   }
 }
 
@@ -623,13 +656,13 @@ leo16_encode_reg_kernel(EncodeArgs a) {
         ifft2_16(w, s0 + 8, s0 + 24, p02);
       }
     }
+    // last IFFT layer (dist 256, skew IO - 1 + 256) merged with the first FFT
+    // layer (dist 256, skew FO + 255)
 #pragma unroll
-    for (int s0 = 0; s0 < 32; s0++) ifft2_16(w, s0, s0 + 32, IO - 1 + 256);  // last layer, dist 256
-    // ---- FFT (fftDIT, skew index FO + iend - 1) ----
+    for (int s0 = 0; s0 < 32; s0++) ifft_fft2_16(w, s0, s0 + 32, g_ptab16_merged + 16);
+    // ---- FFT (fftDIT, skew index FO + iend - 1), dist4 = 512: its dist 128 layer (bit 7) ----
 #pragma unroll
-    for (int s0 = 0; s0 < 16; s0++) {  // dist4 = 512, dist = 128 (bits 8, 7)
-      fft2_16(w, s0, s0 + 32, FO + 255);
-      fft2_16(w, s0 + 16, s0 + 48, FO + 255);
+    for (int s0 = 0; s0 < 16; s0++) {
       fft2_16(w, s0, s0 + 16, FO + 127);
       fft2_16(w, s0 + 32, s0 + 48, FO + 383);
     }
@@ -643,17 +676,16 @@ leo16_encode_reg_kernel(EncodeArgs a) {
     fft16_block<8>(w, FO + 64 * q);                                         // bits 4 .. 0
   } else {  // M == 256: slot 16a + b: a = bits 6-7, b = bits 0-3
     constexpr int p01 = IO - 1 + 64, p02 = p01 + 64, p23 = p01 + 128;
+    static_assert(p02 == IO + 127, "merged table: positions IO + 127 and FO + 127");
 #pragma unroll
-    for (int b = 0; b < 16; b++) {  // radix-4 dist 64 (bits 6, 7)
+    for (int b = 0; b < 16; b++) {  // radix-4 dist 64 (bits 6, 7); its dist 128 layer merged with the FFT's
       ifft2_16(w, b, 16 + b, p01);
       ifft2_16(w, 32 + b, 48 + b, p23);
-      ifft2_16(w, b, 32 + b, p02);
-      ifft2_16(w, 16 + b, 48 + b, p02);
+      ifft_fft2_16(w, b, 32 + b, g_ptab16_merged);
+      ifft_fft2_16(w, 16 + b, 48 + b, g_ptab16_merged);
     }
 #pragma unroll
-    for (int b = 0; b < 16; b++) {  // FFT dist4 = 256, dist = 64 (bits 7, 6)
-      fft2_16(w, b, 32 + b, FO + 127);
-      fft2_16(w, 16 + b, 48 + b, FO + 127);
+    for (int b = 0; b < 16; b++) {  // FFT dist4 = 256: its dist 64 layer (bit 6)
       fft2_16(w, b, 16 + b, FO + 63);
       fft2_16(w, 32 + b, 48 + b, FO + 191);
     }
@@ -977,13 +1009,6 @@ __device__ __forceinline__ uint32_t mulp(uint32_t y, const uint32_t (&t)[16]) { 
 // the position is made opaque so that each unit loads its tables afresh
 // (scalar-cache hits) instead of the compiler keeping every table of the
 // kernel live (1,100 SGPR spills through v_writelane / v_readlane).
-// a wave-uniform value the compiler cannot see through: values derived from it
-// in one phase are not kept live (in SGPRs, then spilled) for the next
-__device__ __forceinline__ int opaque_s(int x) {
-  asm volatile("" : "+s"(x));
-  return x;
-}
-
 struct PTab {
   uint32_t s[16];
   __device__ __forceinline__ uint32_t operator[](int i) const { return s[i]; }
@@ -1285,6 +1310,26 @@ hipError_t ensure_tables() {
         }
     }
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_ptab16), pt.data(), pt.size() * 4)) != hipSuccess) return e;
+    // merged encoder tables: the element exp(skew[p]) ^ exp(skew[q]) (skew kMod16 = element 0)
+    auto elem = [&](int pos) -> unsigned { return t.skew[pos] == kMod16 ? 0u : (unsigned)t.exp[t.skew[pos]]; };
+    std::vector<uint32_t> mt(2 * 16, 0u);
+    const int pairs[2][2] = {{383, 127}, {767, 255}};
+    for (int m = 0; m < 2; m++) {
+      const unsigned c = elem(pairs[m][0]) ^ elem(pairs[m][1]);
+      if (!c) continue;
+      const unsigned lc = t.log[c];
+      for (int g = 0; g < 8; g++)
+        for (int e2 = 1; e2 < 4; e2++) {
+          const unsigned x = (unsigned)e2 << (2 * g);
+          unsigned sidx = (unsigned)t.log[x] + lc;
+          sidx = (sidx + (sidx >> 16)) & 0xFFFFu;
+          const unsigned prod = t.exp[sidx];
+          const int lo_idx = g < 4 ? g : 4 + (g - 4), hi_idx = 8 + lo_idx;
+          mt[(size_t)m * 16 + lo_idx] |= (prod & 0xFFu) << (8 * e2);
+          mt[(size_t)m * 16 + hi_idx] |= ((prod >> 8) & 0xFFu) << (8 * e2);
+        }
+    }
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_ptab16_merged), mt.data(), mt.size() * 4)) != hipSuccess) return e;
   }
   // > 64 KiB of dynamic LDS (errlocs 128 KiB, k = 512 decode 128 KiB)
   if ((e = hipFuncSetAttribute((const void*)leo16_errlocs_kernel,
