@@ -491,25 +491,31 @@ __device__ __forceinline__ void mul16_add(uint32_t& xlo, uint32_t& xhi, uint32_t
   mul16_add_t(xlo, xhi, ylo, yhi, g_ptab16 + pos * 16);
 }
 
-struct W16 {
-  uint32_t lo[64], hi[64];
+// NS elements per lane, 4 symbols each as a low-byte and a high-byte dword
+template <int NS>
+struct W16n {
+  uint32_t lo[NS], hi[NS];
 };
+using W16 = W16n<64>;
 
 // ifftDIT2: y ^= x; x ^= y * skew[pos]
-__device__ __forceinline__ void ifft2_16(W16& w, int i, int j, int pos) {
+template <class W>
+__device__ __forceinline__ void ifft2_16(W& w, int i, int j, int pos) {
   w.lo[j] ^= w.lo[i];
   w.hi[j] ^= w.hi[i];
   mul16_add(w.lo[i], w.hi[i], w.lo[j], w.hi[j], pos);
 }
 // fftDIT2: x ^= y * skew[pos]; y ^= x
-__device__ __forceinline__ void fft2_16(W16& w, int i, int j, int pos) {
+template <class W>
+__device__ __forceinline__ void fft2_16(W& w, int i, int j, int pos) {
   mul16_add(w.lo[i], w.hi[i], w.lo[j], w.hi[j], pos);
   w.lo[j] ^= w.lo[i];
   w.hi[j] ^= w.hi[i];
 }
 
 // the merged last-IFFT / first-FFT butterfly: y ^= x; x ^= y (A ^ B); y ^= x
-__device__ __forceinline__ void ifft_fft2_16(W16& w, int i, int j, const uint32_t* t) {
+template <class W>
+__device__ __forceinline__ void ifft_fft2_16(W& w, int i, int j, const uint32_t* t) {
   w.lo[j] ^= w.lo[i];
   w.hi[j] ^= w.hi[i];
   mul16_add_t(w.lo[i], w.hi[i], w.lo[j], w.hi[j], t);
@@ -517,12 +523,12 @@ __device__ __forceinline__ void ifft_fft2_16(W16& w, int i, int j, const uint32_
   w.hi[j] ^= w.hi[i];
 }
 
-// Block layout, encoder IFFT radix-4 steps with dist D..16 (bits 0-5);
-// base = m - 1 + 64 q (ifftDITEncoder skew index m - 1 + iend).
-template <int D>
-__device__ __forceinline__ void ifft16_block(W16& w, int base) {
+// Block layout, encoder IFFT radix-4 steps with dist D.. (up to the NS slots:
+// bits 0-5 for 64); base = m - 1 + NS q (ifftDITEncoder skew index m - 1 + iend).
+template <int D, int NS = 64, class W>
+__device__ __forceinline__ void ifft16_block(W& w, int base) {
 #pragma unroll
-  for (int r = 0; r < 64; r += 4 * D) {
+  for (int r = 0; r < NS; r += 4 * D) {
     const int p01 = base + r + D, p02 = p01 + D, p23 = p01 + 2 * D;
 #pragma unroll
     for (int i = r; i < r + D; i++) {
@@ -534,16 +540,16 @@ __device__ __forceinline__ void ifft16_block(W16& w, int base) {
     // per unit: otherwise every table of the block is loaded up front (SGPR spills)
     __builtin_amdgcn_sched_barrier(0);
   }
-  if constexpr (D * 16 <= 64) ifft16_block<D * 4>(w, base);
+  if constexpr (D * 16 <= NS) ifft16_block<D * 4, NS>(w, base);
 }
 
 // Block layout, fftDIT radix-4 step with dist DIST (dist4 = 4 DIST) and the
-// ones below it; base = FO + 64 q (skew index FO + iend - 1).  The final radix-2 layer
+// ones below it; base = FO + NS q (skew index FO + iend - 1).  The final radix-2 layer
 // exists when the last dist4 is 2.
-template <int DIST>
-__device__ __forceinline__ void fft16_block(W16& w, int base) {
+template <int DIST, int NS = 64, class W>
+__device__ __forceinline__ void fft16_block(W& w, int base) {
 #pragma unroll
-  for (int r = 0; r < 64; r += 4 * DIST) {
+  for (int r = 0; r < NS; r += 4 * DIST) {
     const int iend = r + DIST;
     const int p01 = base + iend - 1, p02 = base + iend + DIST - 1, p23 = base + iend + 2 * DIST - 1;
 #pragma unroll
@@ -556,10 +562,10 @@ __device__ __forceinline__ void fft16_block(W16& w, int base) {
     __builtin_amdgcn_sched_barrier(0);  // as in ifft16_block
   }
   if constexpr (DIST >= 4) {
-    fft16_block<DIST / 4>(w, base);
+    fft16_block<DIST / 4, NS>(w, base);
   } else if constexpr (DIST == 2) {
 #pragma unroll
-    for (int r = 0; r < 64; r += 2) {
+    for (int r = 0; r < NS; r += 2) {
       fft2_16(w, r, r + 1, base + r);
       if (r % 8 == 6) __builtin_amdgcn_sched_barrier(0);
     }
@@ -567,10 +573,10 @@ __device__ __forceinline__ void fft16_block(W16& w, int base) {
 }
 
 // P x P block transpose: element (wave Q, slot (c << R) | l) <-> (wave c,
-// slot (Q << R) | l), R = 6 - log2 P, S group-slots per LDS round.
-template <int P, int S>
-__device__ __forceinline__ void xpose16(W16& w, uint32_t* lds, int q, int lane) {
-  constexpr int R = P == 8 ? 3 : 4;
+// slot (Q << R) | l), R = log2 NS - log2 P, S group-slots per LDS round.
+template <int P, int S, int NS = 64, class W>
+__device__ __forceinline__ void xpose16(W& w, uint32_t* lds, int q, int lane) {
+  constexpr int R = __builtin_ctz(NS) - __builtin_ctz(P);
   constexpr int G = 1 << R;
   // lds[(dst * P + src) * S + u][2][64]
 #pragma unroll
@@ -595,6 +601,78 @@ __device__ __forceinline__ void xpose16(W16& w, uint32_t* lds, int q, int lane) 
     __syncthreads();
   }
 }
+
+// Register encoders' data movement.  Element j of wave q is shard NS q + j;
+// lane: 64-B block (lane >> 3) of the 512-B chunk, symbols 4 (lane & 7) .. +3.
+template <int NS>
+__device__ __forceinline__ void enc16_load(const EncodeArgs& a, W16n<NS>& w, int q, long sq, long vec, uint32_t col,
+                                           uint32_t cl, bool active) {
+  const auto in_rsrc = make_rsrc(a.in + sq * a.in_sq_stride + vec * a.in_vec_stride);
+  const uint32_t in_stride = (uint32_t)a.in_shard_stride;
+#pragma unroll
+  for (int j = 0; j < NS; j++) {
+    const uint32_t so = (uint32_t)(NS * q + j) * in_stride;
+    w.lo[j] = __builtin_amdgcn_raw_buffer_load_b32(in_rsrc, cl, so, 0);
+    w.hi[j] = __builtin_amdgcn_raw_buffer_load_b32(in_rsrc, cl + 32u, so, 0);
+  }
+  if (a.copy && active) {
+    const auto cp = make_rsrc(a.copy + sq * a.copy_sq_stride + vec * a.copy_vec_stride);
+    const uint32_t cs = (uint32_t)a.copy_shard_stride;
+#pragma unroll
+    for (int j = 0; j < NS; j++) {
+      const uint32_t so = (uint32_t)(NS * q + j) * cs;
+      __builtin_amdgcn_raw_buffer_store_b32(w.lo[j], cp, col, so, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(w.hi[j], cp, col + 32u, so, 0);
+    }
+  }
+}
+
+// The encoders' three output modes: compare (prerepairSanityCheck), Repair
+// fill (store missing shards, compare given ones) and plain store.
+template <int NS>
+__device__ __forceinline__ void enc16_store(const EncodeArgs& a, const W16n<NS>& w, int q, long sq, long vec, long sv,
+                                            uint32_t col, bool active) {
+  if (!active) return;
+  const auto out_rsrc = make_rsrc(a.out + sq * a.out_sq_stride + vec * a.out_vec_stride);
+  const uint32_t os = (uint32_t)a.out_shard_stride;
+  if (a.mismatch) {  // prerepairSanityCheck: parity must equal Encode(data)
+    uint32_t diff = 0;
+#pragma unroll
+    for (int j = 0; j < NS; j++) {
+      const uint32_t so = (uint32_t)(NS * q + j) * os;
+      diff |= w.lo[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, col, so, 0);
+      diff |= w.hi[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, col + 32u, so, 0);
+    }
+    if (diff) {
+      atomicOr(&a.mismatch[sq], a.mismatch_bit);
+      if (a.mismatch_vec) a.mismatch_vec[sq * a.nvec + vec] = 1;
+    }
+    return;
+  }
+  if (a.out_present) {  // Repair fill: store the missing shards of the out half, compare given ones
+    uint32_t diff = 0;
+#pragma unroll
+    for (int j = 0; j < NS; j++) {
+      const uint32_t so = (uint32_t)(NS * q + j) * os;
+      if (fill_given(a, sq, vec, NS * q + j)) {  // wave-uniform
+        diff |= w.lo[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, col, so, 0);
+        diff |= w.hi[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, col + 32u, so, 0);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b32(w.lo[j], out_rsrc, col, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(w.hi[j], out_rsrc, col + 32u, so, 0);
+      }
+    }
+    if (diff) a.redo[sv] = 1;
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < NS; j++) {
+    const uint32_t so = (uint32_t)(NS * q + j) * os;
+    __builtin_amdgcn_raw_buffer_store_b32(w.lo[j], out_rsrc, col, so, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(w.hi[j], out_rsrc, col + 32u, so, 0);
+  }
+}
+
 
 // REV: the reverse fill (EncodeArgs.reverse): skew offsets IO = 0 for the IFFT
 // and FO = M for the FFT instead of M and 0 (positions stay below kTabPos).
@@ -621,25 +699,8 @@ leo16_encode_reg_kernel(EncodeArgs a) {
   const uint32_t col = (uint32_t)chunk * 512u + (uint32_t)(lane >> 3) * 64u + (uint32_t)(lane & 7) * 4u;
   const bool active = col < (uint32_t)a.shard_bytes;
   const uint32_t cl = active ? col : 0u;  // inactive lanes read valid memory, store nothing
-  const auto in_rsrc = make_rsrc(a.in + sq * a.in_sq_stride + vec * a.in_vec_stride);
-  const uint32_t in_stride = (uint32_t)a.in_shard_stride;
   W16 w;
-#pragma unroll
-  for (int j = 0; j < 64; j++) {
-    const uint32_t so = (uint32_t)(64 * q + j) * in_stride;
-    w.lo[j] = __builtin_amdgcn_raw_buffer_load_b32(in_rsrc, cl, so, 0);
-    w.hi[j] = __builtin_amdgcn_raw_buffer_load_b32(in_rsrc, cl + 32u, so, 0);
-  }
-  if (a.copy && active) {
-    const auto cp = make_rsrc(a.copy + sq * a.copy_sq_stride + vec * a.copy_vec_stride);
-    const uint32_t cs = (uint32_t)a.copy_shard_stride;
-#pragma unroll
-    for (int j = 0; j < 64; j++) {
-      const uint32_t so = (uint32_t)(64 * q + j) * cs;
-      __builtin_amdgcn_raw_buffer_store_b32(w.lo[j], cp, col, so, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(w.hi[j], cp, col + 32u, so, 0);
-    }
-  }
+  enc16_load(a, w, q, sq, vec, col, cl, active);
   // ---- IFFT (ifftDITEncoder, skew index IO - 1 + iend) ----
   ifft16_block<1>(w, IO - 1 + 64 * q);  // bits 0-5
   xpose16<P, S>(w, lds, q, lane);
@@ -692,45 +753,86 @@ leo16_encode_reg_kernel(EncodeArgs a) {
     xpose16<P, S>(w, lds, q, lane);
     fft16_block<16>(w, FO + 64 * q);  // bits 5 .. 0
   }
-  if (!active) return;
-  const auto out_rsrc = make_rsrc(a.out + sq * a.out_sq_stride + vec * a.out_vec_stride);
-  const uint32_t os = (uint32_t)a.out_shard_stride;
-  if (a.mismatch) {  // prerepairSanityCheck: parity must equal Encode(data)
-    uint32_t diff = 0;
+  enc16_store(a, w, q, sq, vec, sv, col, active);
+}
+
+// M = 512 over 16 waves of 32 elements (1,024 threads): 64 data VGPRs per lane
+// within the 128 of 4 waves per SIMD, against 8 waves of 64 elements at 2 per
+// SIMD in leo16_encode_reg_kernel<512>.  Block layout: wave q holds elements
+// 32 q + j (bits 0-4); after the 16 x 16 transpose wave c holds the elements
+// with bits 1-4 = c in slots 2 h + b (h = bits 5-8, b = bit 0).  128 KiB of
+// dynamic LDS for the transposes.
+constexpr int kEnc16Lds = 16 * 16 * 2 * 64 * 4;
+template <bool REV>
+__global__ __launch_bounds__(1024) void leo16_encode_reg16_kernel(EncodeArgs a) {
+  constexpr int M = 512, IO = REV ? 0 : M, FO = REV ? M : 0;
+  constexpr int P = 16, NS = 32;
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds16[];
+  const long blk = blockIdx.x;
+  const int chunk = (int)(blk % a.nchunk);
+  const long sv = blk / a.nchunk;
+  const long vec = sv % a.nvec;
+  const long sq = sv / a.nvec;
+  if (vec_skipped(a, sv)) return;  // uniform
+  const int lane = threadIdx.x & 63;
+  const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t col = (uint32_t)chunk * 512u + (uint32_t)(lane >> 3) * 64u + (uint32_t)(lane & 7) * 4u;
+  const bool active = col < (uint32_t)a.shard_bytes;
+  const uint32_t cl = active ? col : 0u;
+  W16n<NS> w;
+  enc16_load(a, w, q, sq, vec, col, cl, active);
+  // ---- IFFT (ifftDITEncoder, skew index IO - 1 + iend) ----
+  ifft16_block<1, NS>(w, IO - 1 + NS * q);  // bits 0-3
 #pragma unroll
-    for (int j = 0; j < 64; j++) {
-      const uint32_t so = (uint32_t)(64 * q + j) * os;
-      diff |= w.lo[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, col, so, 0);
-      diff |= w.hi[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, col + 32u, so, 0);
-    }
-    if (diff) {
-      atomicOr(&a.mismatch[sq], a.mismatch_bit);
-      if (a.mismatch_vec) a.mismatch_vec[sq * a.nvec + vec] = 1;
-    }
-    return;
-  }
-  if (a.out_present) {  // Repair fill: store the missing shards of the out half, compare given ones
-    uint32_t diff = 0;
+  for (int i = 0; i < 16; i++) ifft2_16(w, i, i + 16, IO - 1 + NS * q + 16);  // bit 4
+  __builtin_amdgcn_sched_barrier(0);
+  xpose16<P, 1, NS>(w, lds16, q, lane);
 #pragma unroll
-    for (int j = 0; j < 64; j++) {
-      const uint32_t so = (uint32_t)(64 * q + j) * os;
-      if (fill_given(a, sq, vec, 64 * q + j)) {  // wave-uniform
-        diff |= w.lo[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, col, so, 0);
-        diff |= w.hi[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, col + 32u, so, 0);
-      } else {
-        __builtin_amdgcn_raw_buffer_store_b32(w.lo[j], out_rsrc, col, so, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(w.hi[j], out_rsrc, col + 32u, so, 0);
-      }
-    }
-    if (diff) a.redo[sv] = 1;
-    return;
-  }
+  for (int hh = 0; hh < 4; hh++) {  // radix-4 bits 5, 6 (slot dist 2, 4), 128-blocks r = 128 hh
+    const int p01 = IO - 1 + 128 * hh + 32, p02 = p01 + 32, p23 = p01 + 64;
 #pragma unroll
-  for (int j = 0; j < 64; j++) {
-    const uint32_t so = (uint32_t)(64 * q + j) * os;
-    __builtin_amdgcn_raw_buffer_store_b32(w.lo[j], out_rsrc, col, so, 0);
-    __builtin_amdgcn_raw_buffer_store_b32(w.hi[j], out_rsrc, col + 32u, so, 0);
+    for (int b = 0; b < 2; b++) {
+      const int s0 = 8 * hh + b;
+      ifft2_16(w, s0, s0 + 2, p01);
+      ifft2_16(w, s0 + 4, s0 + 6, p23);
+      ifft2_16(w, s0, s0 + 4, p02);
+      ifft2_16(w, s0 + 2, s0 + 6, p02);
+    }
+    __builtin_amdgcn_sched_barrier(0);
   }
+  // radix-4 bits 7, 8 (slot dist 8, 16); its bit-8 layer (the last IFFT layer)
+  // merged with the first FFT layer (dist 256)
+#pragma unroll
+  for (int s0 = 0; s0 < 8; s0++) {
+    ifft2_16(w, s0, s0 + 8, IO - 1 + 128);
+    ifft2_16(w, s0 + 16, s0 + 24, IO - 1 + 384);
+    ifft_fft2_16(w, s0, s0 + 16, g_ptab16_merged + 16);
+    ifft_fft2_16(w, s0 + 8, s0 + 24, g_ptab16_merged + 16);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // ---- FFT (fftDIT, skew index FO + iend - 1) ----
+#pragma unroll
+  for (int s0 = 0; s0 < 8; s0++) {  // bit 7 (dist 128, slot dist 8)
+    fft2_16(w, s0, s0 + 8, FO + 127);
+    fft2_16(w, s0 + 16, s0 + 24, FO + 383);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int hh = 0; hh < 4; hh++) {  // radix-4 dist4 = 128 (bits 6, 5), 128-blocks r = 128 hh
+    const int p01 = FO + 128 * hh + 31, p02 = p01 + 32, p23 = p01 + 64;
+#pragma unroll
+    for (int b = 0; b < 2; b++) {
+      const int s0 = 8 * hh + b;
+      fft2_16(w, s0, s0 + 4, p02);
+      fft2_16(w, s0 + 2, s0 + 6, p02);
+      fft2_16(w, s0, s0 + 2, p01);
+      fft2_16(w, s0 + 4, s0 + 6, p23);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  xpose16<P, 1, NS>(w, lds16, q, lane);
+  fft16_block<8, NS>(w, FO + NS * q);  // bits 4 .. 0
+  enc16_store(a, w, q, sq, vec, sv, col, active);
 }
 
 // ---------------------------------------------------------------------------
@@ -1338,6 +1440,12 @@ hipError_t ensure_tables() {
   if ((e = hipFuncSetAttribute((const void*)leo16_decode_kernel,  // k <= 512 here (wider: rs_gf16_wide.hip)
                                hipFuncAttributeMaxDynamicSharedMemorySize, 512 * 256)) != hipSuccess)
     return e;
+  if ((e = hipFuncSetAttribute((const void*)leo16_encode_reg16_kernel<false>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, kEnc16Lds)) != hipSuccess)
+    return e;
+  if ((e = hipFuncSetAttribute((const void*)leo16_encode_reg16_kernel<true>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, kEnc16Lds)) != hipSuccess)
+    return e;
   g_tab_done[dev] = true;
   return hipSuccess;
 }
@@ -1352,6 +1460,12 @@ static bool use_wide(int k) {
   if (k > 512) return true;
   const char* e = getenv("DAGPU_GF16_WIDE");
   return e && e[0] == '1';
+}
+
+// k = 512 encoder: the 16-wave kernel unless DAGPU_GF16_ENC16=0 (A/B)
+static bool enc16_wide_wg() {
+  const char* e = getenv("DAGPU_GF16_ENC16");
+  return !(e && e[0] == '0');
 }
 
 hipError_t launch_leo16_encode(int k, const EncodeArgs& a, hipStream_t s) {
@@ -1369,6 +1483,11 @@ hipError_t launch_leo16_encode(int k, const EncodeArgs& a, hipStream_t s) {
     if (k == 256) {
       if (a.reverse) hipLaunchKernelGGL((leo16_encode_reg_kernel<256, true>), dim3((unsigned)blocks), dim3(256), 0, s, b);
       else hipLaunchKernelGGL((leo16_encode_reg_kernel<256, false>), dim3((unsigned)blocks), dim3(256), 0, s, b);
+    } else if (enc16_wide_wg()) {
+      if (a.reverse)
+        hipLaunchKernelGGL((leo16_encode_reg16_kernel<true>), dim3((unsigned)blocks), dim3(1024), kEnc16Lds, s, b);
+      else
+        hipLaunchKernelGGL((leo16_encode_reg16_kernel<false>), dim3((unsigned)blocks), dim3(1024), kEnc16Lds, s, b);
     } else {
       if (a.reverse) hipLaunchKernelGGL((leo16_encode_reg_kernel<512, true>), dim3((unsigned)blocks), dim3(512), 0, s, b);
       else hipLaunchKernelGGL((leo16_encode_reg_kernel<512, false>), dim3((unsigned)blocks), dim3(512), 0, s, b);
