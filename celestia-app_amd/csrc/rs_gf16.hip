@@ -756,18 +756,22 @@ leo16_encode_reg_kernel(EncodeArgs a) {
   enc16_store(a, w, q, sq, vec, sv, col, active);
 }
 
-// M = 512 over 16 waves of 32 elements (1,024 threads): 64 data VGPRs per lane
-// within the 128 of 4 waves per SIMD, against 8 waves of 64 elements at 2 per
-// SIMD in leo16_encode_reg_kernel<512>.  Block layout: wave q holds elements
-// 32 q + j (bits 0-4); after the 16 x 16 transpose wave c holds the elements
-// with bits 1-4 = c in slots 2 h + b (h = bits 5-8, b = bit 0).  128 KiB of
-// dynamic LDS for the transposes.
-constexpr int kEnc16Lds = 16 * 16 * 2 * 64 * 4;
-template <bool REV>
-__global__ __launch_bounds__(1024) void leo16_encode_reg16_kernel(EncodeArgs a) {
-  constexpr int M = 512, IO = REV ? 0 : M, FO = REV ? M : 0;
-  constexpr int P = 16, NS = 32;
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds16[];
+// 32 elements per wave: M = 512 over 16 waves (1,024 threads), M = 256 over 8
+// (512 threads); 64 data VGPRs per lane within the 128 of 4 waves per SIMD,
+// against 64 elements per wave at 2 waves per SIMD in leo16_encode_reg_kernel
+// (M = 256 then also fits two workgroups per CU).  Block layout: wave q holds
+// elements 32 q + j (bits 0-4).  After the P x P transpose, M = 512: wave c
+// holds the elements with bits 1-4 = c in slots 2 h + b (h = bits 5-8, b = bit
+// 0); M = 256: bits 2-4 = c, slots 4 h + l (h = bits 5-7, l = bits 0-1).
+template <int M>
+constexpr int enc32_lds_bytes() {
+  return M == 512 ? 16 * 16 * 2 * 64 * 4 : 8 * 8 * 2 * 2 * 64 * 4;  // S = 1 / 2 group-slots per round
+}
+template <int M, bool REV>
+__global__ __launch_bounds__(M * 2) void leo16_encode_reg32_kernel(EncodeArgs a) {
+  constexpr int IO = REV ? 0 : M, FO = REV ? M : 0;
+  constexpr int NS = 32, P = M / NS, S = M == 512 ? 1 : 2;
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
   const long blk = blockIdx.x;
   const int chunk = (int)(blk % a.nchunk);
   const long sv = blk / a.nchunk;
@@ -786,51 +790,85 @@ __global__ __launch_bounds__(1024) void leo16_encode_reg16_kernel(EncodeArgs a) 
 #pragma unroll
   for (int i = 0; i < 16; i++) ifft2_16(w, i, i + 16, IO - 1 + NS * q + 16);  // bit 4
   __builtin_amdgcn_sched_barrier(0);
-  xpose16<P, 1, NS>(w, lds16, q, lane);
+  xpose16<P, S, NS>(w, lds32, q, lane);
+  if constexpr (M == 512) {
 #pragma unroll
-  for (int hh = 0; hh < 4; hh++) {  // radix-4 bits 5, 6 (slot dist 2, 4), 128-blocks r = 128 hh
-    const int p01 = IO - 1 + 128 * hh + 32, p02 = p01 + 32, p23 = p01 + 64;
+    for (int hh = 0; hh < 4; hh++) {  // radix-4 bits 5, 6 (slot dist 2, 4), 128-blocks r = 128 hh
+      const int p01 = IO - 1 + 128 * hh + 32, p02 = p01 + 32, p23 = p01 + 64;
 #pragma unroll
-    for (int b = 0; b < 2; b++) {
-      const int s0 = 8 * hh + b;
-      ifft2_16(w, s0, s0 + 2, p01);
-      ifft2_16(w, s0 + 4, s0 + 6, p23);
-      ifft2_16(w, s0, s0 + 4, p02);
-      ifft2_16(w, s0 + 2, s0 + 6, p02);
+      for (int b = 0; b < 2; b++) {
+        const int s0 = 8 * hh + b;
+        ifft2_16(w, s0, s0 + 2, p01);
+        ifft2_16(w, s0 + 4, s0 + 6, p23);
+        ifft2_16(w, s0, s0 + 4, p02);
+        ifft2_16(w, s0 + 2, s0 + 6, p02);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // radix-4 bits 7, 8 (slot dist 8, 16); its bit-8 layer (the last IFFT
+    // layer) merged with the first FFT layer (dist 256)
+#pragma unroll
+    for (int s0 = 0; s0 < 8; s0++) {
+      ifft2_16(w, s0, s0 + 8, IO - 1 + 128);
+      ifft2_16(w, s0 + 16, s0 + 24, IO - 1 + 384);
+      ifft_fft2_16(w, s0, s0 + 16, g_ptab16_merged + 16);
+      ifft_fft2_16(w, s0 + 8, s0 + 24, g_ptab16_merged + 16);
     }
     __builtin_amdgcn_sched_barrier(0);
-  }
-  // radix-4 bits 7, 8 (slot dist 8, 16); its bit-8 layer (the last IFFT layer)
-  // merged with the first FFT layer (dist 256)
+    // ---- FFT (fftDIT, skew index FO + iend - 1) ----
 #pragma unroll
-  for (int s0 = 0; s0 < 8; s0++) {
-    ifft2_16(w, s0, s0 + 8, IO - 1 + 128);
-    ifft2_16(w, s0 + 16, s0 + 24, IO - 1 + 384);
-    ifft_fft2_16(w, s0, s0 + 16, g_ptab16_merged + 16);
-    ifft_fft2_16(w, s0 + 8, s0 + 24, g_ptab16_merged + 16);
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  // ---- FFT (fftDIT, skew index FO + iend - 1) ----
-#pragma unroll
-  for (int s0 = 0; s0 < 8; s0++) {  // bit 7 (dist 128, slot dist 8)
-    fft2_16(w, s0, s0 + 8, FO + 127);
-    fft2_16(w, s0 + 16, s0 + 24, FO + 383);
-  }
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int hh = 0; hh < 4; hh++) {  // radix-4 dist4 = 128 (bits 6, 5), 128-blocks r = 128 hh
-    const int p01 = FO + 128 * hh + 31, p02 = p01 + 32, p23 = p01 + 64;
-#pragma unroll
-    for (int b = 0; b < 2; b++) {
-      const int s0 = 8 * hh + b;
-      fft2_16(w, s0, s0 + 4, p02);
-      fft2_16(w, s0 + 2, s0 + 6, p02);
-      fft2_16(w, s0, s0 + 2, p01);
-      fft2_16(w, s0 + 4, s0 + 6, p23);
+    for (int s0 = 0; s0 < 8; s0++) {  // bit 7 (dist 128, slot dist 8)
+      fft2_16(w, s0, s0 + 8, FO + 127);
+      fft2_16(w, s0 + 16, s0 + 24, FO + 383);
     }
     __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int hh = 0; hh < 4; hh++) {  // radix-4 dist4 = 128 (bits 6, 5), 128-blocks r = 128 hh
+      const int p01 = FO + 128 * hh + 31, p02 = p01 + 32, p23 = p01 + 64;
+#pragma unroll
+      for (int b = 0; b < 2; b++) {
+        const int s0 = 8 * hh + b;
+        fft2_16(w, s0, s0 + 4, p02);
+        fft2_16(w, s0 + 2, s0 + 6, p02);
+        fft2_16(w, s0, s0 + 2, p01);
+        fft2_16(w, s0 + 4, s0 + 6, p23);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+#pragma unroll
+    for (int hh = 0; hh < 2; hh++) {  // radix-4 bits 5, 6 (slot dist 4, 8), 128-blocks r = 128 hh
+      const int p01 = IO - 1 + 128 * hh + 32, p02 = p01 + 32, p23 = p01 + 64;
+#pragma unroll
+      for (int l = 0; l < 4; l++) {
+        const int s0 = 16 * hh + l;
+        ifft2_16(w, s0, s0 + 4, p01);
+        ifft2_16(w, s0 + 8, s0 + 12, p23);
+        ifft2_16(w, s0, s0 + 8, p02);
+        ifft2_16(w, s0 + 4, s0 + 12, p02);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // bit 7 (slot dist 16): the last IFFT layer merged with the first FFT layer (dist 128)
+#pragma unroll
+    for (int s0 = 0; s0 < 16; s0++) ifft_fft2_16(w, s0, s0 + 16, g_ptab16_merged);
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- FFT (fftDIT, skew index FO + iend - 1): radix-4 dist4 = 128 (bits 6, 5) ----
+#pragma unroll
+    for (int hh = 0; hh < 2; hh++) {
+      const int p01 = FO + 128 * hh + 31, p02 = p01 + 32, p23 = p01 + 64;
+#pragma unroll
+      for (int l = 0; l < 4; l++) {
+        const int s0 = 16 * hh + l;
+        fft2_16(w, s0, s0 + 8, p02);
+        fft2_16(w, s0 + 4, s0 + 12, p02);
+        fft2_16(w, s0, s0 + 4, p01);
+        fft2_16(w, s0 + 8, s0 + 12, p23);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
-  xpose16<P, 1, NS>(w, lds16, q, lane);
+  xpose16<P, S, NS>(w, lds32, q, lane);
   fft16_block<8, NS>(w, FO + NS * q);  // bits 4 .. 0
   enc16_store(a, w, q, sq, vec, sv, col, active);
 }
@@ -1440,12 +1478,14 @@ hipError_t ensure_tables() {
   if ((e = hipFuncSetAttribute((const void*)leo16_decode_kernel,  // k <= 512 here (wider: rs_gf16_wide.hip)
                                hipFuncAttributeMaxDynamicSharedMemorySize, 512 * 256)) != hipSuccess)
     return e;
-  if ((e = hipFuncSetAttribute((const void*)leo16_encode_reg16_kernel<false>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, kEnc16Lds)) != hipSuccess)
-    return e;
-  if ((e = hipFuncSetAttribute((const void*)leo16_encode_reg16_kernel<true>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, kEnc16Lds)) != hipSuccess)
-    return e;
+  {
+    const void* f[4] = {(const void*)leo16_encode_reg32_kernel<512, false>, (const void*)leo16_encode_reg32_kernel<512, true>,
+                        (const void*)leo16_encode_reg32_kernel<256, false>, (const void*)leo16_encode_reg32_kernel<256, true>};
+    for (int i = 0; i < 4; i++)
+      if ((e = hipFuncSetAttribute(f[i], hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   i < 2 ? enc32_lds_bytes<512>() : enc32_lds_bytes<256>())) != hipSuccess)
+        return e;
+  }
   g_tab_done[dev] = true;
   return hipSuccess;
 }
@@ -1462,10 +1502,14 @@ static bool use_wide(int k) {
   return e && e[0] == '1';
 }
 
-// k = 512 encoder: the 16-wave kernel unless DAGPU_GF16_ENC16=0 (A/B)
-static bool enc16_wide_wg() {
-  const char* e = getenv("DAGPU_GF16_ENC16");
-  return !(e && e[0] == '0');
+// Register encoders: 32 elements per wave at k = 512, 64 at k = 256
+// (profiles/gf16_enc16_r04.log: k = 512 split 2.00 -> 1.92 ms, Q3 Repair
+// +7 %; k = 256 split 0.77 -> 0.75 ms but Q3 Repair -4.5 %).
+// DAGPU_GF16_ENC32=0 / 1 forces either at both widths (A/B).
+static bool enc32_waves(int k) {
+  const char* e = getenv("DAGPU_GF16_ENC32");
+  if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
+  return k == 512;
 }
 
 hipError_t launch_leo16_encode(int k, const EncodeArgs& a, hipStream_t s) {
@@ -1480,14 +1524,19 @@ hipError_t launch_leo16_encode(int k, const EncodeArgs& a, hipStream_t s) {
     b.nchunk = (a.shard_bytes + 511) / 512;
     const long blocks = b.nsq * b.nvec * b.nchunk;
     if (blocks <= 0) return hipSuccess;
-    if (k == 256) {
+    if (enc32_waves(k)) {
+      if (k == 256) {
+        constexpr int L = enc32_lds_bytes<256>();
+        if (a.reverse) hipLaunchKernelGGL((leo16_encode_reg32_kernel<256, true>), dim3((unsigned)blocks), dim3(512), L, s, b);
+        else hipLaunchKernelGGL((leo16_encode_reg32_kernel<256, false>), dim3((unsigned)blocks), dim3(512), L, s, b);
+      } else {
+        constexpr int L = enc32_lds_bytes<512>();
+        if (a.reverse) hipLaunchKernelGGL((leo16_encode_reg32_kernel<512, true>), dim3((unsigned)blocks), dim3(1024), L, s, b);
+        else hipLaunchKernelGGL((leo16_encode_reg32_kernel<512, false>), dim3((unsigned)blocks), dim3(1024), L, s, b);
+      }
+    } else if (k == 256) {
       if (a.reverse) hipLaunchKernelGGL((leo16_encode_reg_kernel<256, true>), dim3((unsigned)blocks), dim3(256), 0, s, b);
       else hipLaunchKernelGGL((leo16_encode_reg_kernel<256, false>), dim3((unsigned)blocks), dim3(256), 0, s, b);
-    } else if (enc16_wide_wg()) {
-      if (a.reverse)
-        hipLaunchKernelGGL((leo16_encode_reg16_kernel<true>), dim3((unsigned)blocks), dim3(1024), kEnc16Lds, s, b);
-      else
-        hipLaunchKernelGGL((leo16_encode_reg16_kernel<false>), dim3((unsigned)blocks), dim3(1024), kEnc16Lds, s, b);
     } else {
       if (a.reverse) hipLaunchKernelGGL((leo16_encode_reg_kernel<512, true>), dim3((unsigned)blocks), dim3(512), 0, s, b);
       else hipLaunchKernelGGL((leo16_encode_reg_kernel<512, false>), dim3((unsigned)blocks), dim3(512), 0, s, b);
