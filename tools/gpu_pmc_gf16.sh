@@ -1,7 +1,7 @@
 # GF(2^16) stress workloads (configs[4] widths): kernel-trace stats and SQ/GRBM counters per
 # launch of the GF(2^16) kernels, one rocprofv3 run per pass (counters never combined with
 # trace domains).  Summary: gpurun_out/p16/summary.txt
-#   bash tools/gpu_pmc_gf16.sh [workload ...]   (repair512 repair512q3 split512 repair256)
+#   bash tools/gpu_pmc_gf16.sh [workload ...]   (repair512 repair512q3 split512 repair256 repair128)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp; cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/p16; mkdir -p $OUT
@@ -12,6 +12,7 @@ for wl in "$@"; do
     repair512q3) A="--mode repair --k 512 --batch 2 --steps 3 --warmup 1 --pattern q3";;
     repair256) A="--mode repair --k 256 --batch 8 --steps 3 --warmup 1";;
     split512) A="--mode split --split-k 512 --steps 3 --warmup 1";;
+    repair128) A="--mode repair --k 128 --batch 256 --steps 3 --warmup 1";;
     *) echo "unknown $wl"; exit 2;;
   esac
   B="$GRAFT_REPO_ROOT/bench.py $A"
@@ -35,7 +36,7 @@ for wl in sys.argv[1:]:
     for p in glob.glob(f"gpurun_out/p16/{wl}/*/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(p)):
             n = kname(r["Kernel_Name"])
-            if "leo16" in n or "errloc" in n:
+            if "leo16" in n or "errloc" in n or "decode128" in n:
                 agg[n][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for n, d in sorted(agg.items()):
         a = {c: sum(v) / len(v) for c, v in d.items()}
