@@ -309,6 +309,38 @@ __device__ uint32_t* rfc_reduce(uint32_t* src, uint32_t* dst, int cur) {
   return src;
 }
 
+// RFC-6962 leaf digest of DAH item li (row roots, then column roots) of square sq
+__device__ __forceinline__ void dah_leaf(const SquareArgs& a, long sq, int li, uint32_t* out) {
+  const int w = 2 * a.k;
+  const uint8_t* root = (li < w ? a.row_roots + (sq * w + li) * kNodeSize
+                                : a.col_roots + (sq * w + (li - w)) * kNodeSize);
+  // message bytes: [0]=0x00, [1..90]=root, [91]=0x80, len=728 bits
+  uint32_t m[32];
+#pragma unroll
+  for (int j = 0; j < 32; j++) m[j] = 0;
+  const uint16_t* r16 = (const uint16_t*)root;  // 2-B aligned (90 B stride)
+#pragma unroll
+  for (int h = 0; h < 45; h++) {
+    const uint32_t v = r16[h];
+    const int off = 1 + 2 * h;  // byte offset of this halfword in the message
+    m[off >> 2] |= v << (8 * (off & 3));
+    if ((off & 3) == 3) m[(off >> 2) + 1] |= v >> 8;
+  }
+  m[91 >> 2] |= 0x80u << (8 * (91 & 3));
+  uint32_t st[8];
+  sha256_init(st);
+#pragma unroll
+  for (int blk = 0; blk < 2; blk++) {
+    uint32_t wv[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) wv[j] = bswap32(m[16 * blk + j]);
+    if (blk == 1) { wv[14] = 0; wv[15] = 91u * 8u; }
+    sha256_compress(st, wv);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; j++) out[j] = bswap32(st[j]);
+}
+
 __global__ __launch_bounds__(kDahThreads) void dah_kernel(SquareArgs a) {
   // (C + C/2) leaf / level slots, then n / C subtree digests (8 dwords each)
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -318,36 +350,7 @@ __global__ __launch_bounds__(kDahThreads) void dah_kernel(SquareArgs a) {
   const int C = n < kDahChunk ? n : kDahChunk;
   uint32_t* sub = lds + (C + C / 2) * 8;
   for (int c0 = 0; c0 < n; c0 += C) {
-    for (int i = threadIdx.x; i < C; i += kDahThreads) {
-      const int li = c0 + i;
-      const uint8_t* root = (li < w ? a.row_roots + (sq * w + li) * kNodeSize
-                                    : a.col_roots + (sq * w + (li - w)) * kNodeSize);
-      // message bytes: [0]=0x00, [1..90]=root, [91]=0x80, len=728 bits
-      uint32_t m[32];
-#pragma unroll
-      for (int j = 0; j < 32; j++) m[j] = 0;
-      const uint16_t* r16 = (const uint16_t*)root;  // 2-B aligned (90 B stride)
-#pragma unroll
-      for (int h = 0; h < 45; h++) {
-        const uint32_t v = r16[h];
-        const int off = 1 + 2 * h;  // byte offset of this halfword in the message
-        m[off >> 2] |= v << (8 * (off & 3));
-        if ((off & 3) == 3) m[(off >> 2) + 1] |= v >> 8;
-      }
-      m[91 >> 2] |= 0x80u << (8 * (91 & 3));
-      uint32_t st[8];
-      sha256_init(st);
-#pragma unroll
-      for (int blk = 0; blk < 2; blk++) {
-        uint32_t wv[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) wv[j] = bswap32(m[16 * blk + j]);
-        if (blk == 1) { wv[14] = 0; wv[15] = 91u * 8u; }
-        sha256_compress(st, wv);
-      }
-#pragma unroll
-      for (int j = 0; j < 8; j++) lds[i * 8 + j] = bswap32(st[j]);
-    }
+    for (int i = threadIdx.x; i < C; i += kDahThreads) dah_leaf(a, sq, c0 + i, lds + i * 8);
     __syncthreads();
     const uint32_t* r = rfc_reduce(lds, lds + C * 8, C);
     if (threadIdx.x < 8) sub[(c0 / C) * 8 + threadIdx.x] = r[threadIdx.x];
@@ -358,6 +361,68 @@ __global__ __launch_bounds__(kDahThreads) void dah_kernel(SquareArgs a) {
     uint32_t* out = (uint32_t*)(a.dah + sq * 32);
     out[threadIdx.x] = root[threadIdx.x];
   }
+}
+
+// Few wide squares (n >= 1024 items, under 64 squares): one workgroup per
+// square put the wide lower levels on one CU each (k = 512: 4,096 leaf and
+// 4,094 node compressions, ~0.13 ms).  Here the 64-item subtrees go to nsq * n
+// / 64 single-wave workgroups (their roots into the digest buffer, free once the
+// trees are built) and one workgroup per square reduces the n / 64 subtree roots.
+constexpr int kDahSub = 64;
+__global__ __launch_bounds__(kDahSub) void dah_sub_kernel(SquareArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t buf[2][kDahSub * 8];
+  const int n = 4 * a.k, per = n / kDahSub;
+  const long sq = blockIdx.x / per;
+  const int b = (int)(blockIdx.x % per);
+  const int i = threadIdx.x;
+  dah_leaf(a, sq, b * kDahSub + i, buf[0] + i * 8);
+  int cur = kDahSub, src = 0;
+  while (cur > 1) {
+    __syncthreads();  // one wave: orders the level's LDS writes before the next level's reads
+    const int next = cur / 2;
+    if (i < next) {
+      uint32_t m[32];
+#pragma unroll
+      for (int j = 0; j < 32; j++) m[j] = 0;
+      uint32_t lft[8], rgt[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        lft[j] = buf[src][(2 * i) * 8 + j];
+        rgt[j] = buf[src][(2 * i + 1) * 8 + j];
+      }
+      m[0] = 0x01u;
+      put_bytes<1>(m, lft);
+      put_bytes<33>(m, rgt);
+      m[65 >> 2] |= 0x80u << (8 * (65 & 3));
+      uint32_t st[8];
+      sha256_init(st);
+#pragma unroll
+      for (int blk = 0; blk < 2; blk++) {
+        uint32_t wv[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) wv[j] = bswap32(m[16 * blk + j]);
+        if (blk == 1) { wv[14] = 0; wv[15] = 65u * 8u; }
+        sha256_compress(st, wv);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; j++) buf[src ^ 1][i * 8 + j] = bswap32(st[j]);
+    }
+    src ^= 1;
+    cur = next;
+  }
+  __syncthreads();
+  if (i < 8) ((uint32_t*)a.digests)[blockIdx.x * 8 + i] = buf[src][i];
+}
+
+__global__ __launch_bounds__(kDahThreads) void dah_top_kernel(SquareArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const long sq = blockIdx.x;
+  const int per = 4 * a.k / kDahSub;
+  const uint32_t* sub = (const uint32_t*)a.digests + sq * per * 8;
+  for (int i = threadIdx.x; i < per * 8; i += kDahThreads) lds[i] = sub[i];
+  __syncthreads();
+  const uint32_t* root = rfc_reduce(lds, lds + per * 8, per);
+  if (threadIdx.x < 8) ((uint32_t*)(a.dah + sq * 32))[threadIdx.x] = root[threadIdx.x];
 }
 
 // DAGPU_LEAF_LDS_KB (experiments): dynamic LDS requested per leaf workgroup,
@@ -425,9 +490,24 @@ void nmt_workspace_carve(SquareArgs& a, void* ws) {
   a.rec_b = p;
 }
 
+static bool dah_split_enabled() {  // DAGPU_DAH_SPLIT=0: one workgroup per square always (A/B)
+  const char* e = getenv("DAGPU_DAH_SPLIT");
+  return !(e && e[0] == '0');
+}
+
 hipError_t launch_dah(const SquareArgs& a, hipStream_t s) {
   const int n = 4 * a.k;
   if (a.k > kMaxK) return hipErrorInvalidValue;
+  if (a.digests && n >= 1024 && a.nsq < 64 && dah_split_enabled()) {
+    // the digest buffer (w^2 * 32 B per square) holds the n / 64 subtree roots
+    const int per = n / kDahSub;
+    hipLaunchKernelGGL(dah_sub_kernel, dim3((unsigned)(a.nsq * per)), dim3(kDahSub), 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const size_t lds = (size_t)(per + per / 2) * 8 * sizeof(uint32_t);  // <= 24 KiB (k = 8192)
+    hipLaunchKernelGGL(dah_top_kernel, dim3((unsigned)a.nsq), dim3(kDahThreads), lds, s, a);
+    return hipGetLastError();
+  }
   const int C = n < kDahChunk ? n : kDahChunk;
   const size_t lds = ((size_t)(C + C / 2) + (size_t)(n / C)) * 8 * sizeof(uint32_t);  // <= 97 KiB
   if (lds > 65536) {

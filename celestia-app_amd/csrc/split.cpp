@@ -215,6 +215,7 @@ int dagpu_split_finish_device(dagpu_ctx* ctx, uint32_t k, uint32_t parts, const 
   sa.row_roots = d_row_roots;
   sa.col_roots = (uint8_t*)d_col_roots_all;
   sa.dah = d_dah;
+  sa.digests = ws.leaves;  // slab leaf records, consumed by now: scratch for the DAH's subtree roots
   sa.k = (int)k;
   sa.nsq = 1;
   {
