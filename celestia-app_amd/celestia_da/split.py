@@ -46,8 +46,10 @@ class SplitPart:
             raise DAError(_abi.ERR_ARG, f"invalid split k={k} parts={parts}")
         u8 = dict(dtype=torch.uint8, device=device)
         self.ws = torch.empty(ws, **u8)
-        self.send = torch.empty(self.rows * self.w * SHARE_SIZE, **u8)
         self.slab = torch.empty(self.w * self.W * SHARE_SIZE, **u8)
+        # one part: the rows' send block is the top of its own slab (no exchange)
+        self.send = (self.slab[: self.rows * self.w * SHARE_SIZE] if parts == 1
+                     else torch.empty(self.rows * self.w * SHARE_SIZE, **u8))
         self.col_roots = torch.empty(self.W * ROOT_SIZE, **u8)
         self.row_sub = torch.empty(self.w * REC, **u8)
         self.status = torch.zeros(1, dtype=torch.int32, device=device)
@@ -98,7 +100,9 @@ def extend_split_local(ods: torch.Tensor, k: int, parts: int, ctx: Context,
     blk = ps[0].rows * ps[0].W * SHARE_SIZE
     for h, ph in enumerate(ps):  # rank h receives block h of every rank g, in rank order
         for g, pg in enumerate(ps):
-            ph.slab_top[g * blk:(g + 1) * blk].copy_(pg.send[h * blk:(h + 1) * blk])
+            dst, src = ph.slab_top[g * blk:(g + 1) * blk], pg.send[h * blk:(h + 1) * blk]
+            if dst.data_ptr() != src.data_ptr():
+                dst.copy_(src)
     for p in ps:
         p.step_cols(stream)
     row_sub_all = torch.cat([p.row_sub for p in ps])
@@ -117,7 +121,8 @@ def all_to_all_blocks(dist, out: torch.Tensor, inp: torch.Tensor, group=None) ->
     the blocks of ranks 0..P-1 in rank order.  gloo stages through host memory;
     dist=None is the single-rank case."""
     if dist is None:
-        out.copy_(inp)
+        if out.data_ptr() != inp.data_ptr():  # one part: send block and slab top are one buffer
+            out.copy_(inp)
         return
     if dist.get_backend(group) == "nccl" or out.device.type == "cpu":
         dist.all_to_all_single(out, inp, group=group)

@@ -112,4 +112,19 @@ hipError_t forest_enqueue(const ForestPlan& p, const uint8_t* d_leaves, uint8_t*
                           int ignore_max, int check_order, int rfc, int32_t* d_status, uint8_t* d_roots,
                           int records, long roots_stride, hipStream_t s);
 
+// Two forests hashed level by level in shared launches (level L of both in
+// one grid): the column trees and the row subtrees of a split slab.
+struct ForestJob {
+  const ForestPlan* p;
+  const uint8_t* d_leaves;
+  uint8_t* d_inner;
+  int64_t* d_meta;
+  int ignore_max, check_order, rfc;
+  int32_t* d_status;
+  uint8_t* d_roots;
+  int records;
+  long roots_stride;
+};
+hipError_t forest_enqueue_pair(const ForestJob& x, const ForestJob& y, hipStream_t s);
+
 }  // namespace dagpu

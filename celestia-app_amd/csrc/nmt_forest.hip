@@ -211,9 +211,7 @@ __device__ __forceinline__ void rfc_inner(const uint32_t (&l)[8], const uint32_t
   for (int j = 0; j < 8; j++) out[j] = bswap32(st[j]);
 }
 
-__global__ __launch_bounds__(256) void forest_level_kernel(ForestLevelArgs a) {
-  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
-  if (gid >= a.total_out) return;
+__device__ __forceinline__ void forest_level_node(const ForestLevelArgs& a, long gid) {
   long t, j;
   if (a.out_off) {
     t = find_tree(a.out_off, a.ntrees, gid);
@@ -267,6 +265,18 @@ __global__ __launch_bounds__(256) void forest_level_kernel(ForestLevelArgs a) {
   store8(op, lmn);
   if (keep_left_max) store8(op + 32, lmx); else store8(op + 32, rmx);
   store8(op + 64, dg);
+}
+
+__global__ __launch_bounds__(256) void forest_level_kernel(ForestLevelArgs a) {
+  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+  if (gid < a.total_out) forest_level_node(a, gid);
+}
+
+// the same level of two forests in one launch (their nodes back to back)
+__global__ __launch_bounds__(256) void forest_level2_kernel(ForestLevelArgs a, ForestLevelArgs b) {
+  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+  if (gid < a.total_out) forest_level_node(a, gid);
+  else if (gid - a.total_out < b.total_out) forest_level_node(b, gid - a.total_out);
 }
 
 // ---------------------------------------------------------------------------
@@ -465,6 +475,34 @@ void ForestPlan::finalize() {
   meta.insert(meta.end(), root_idx.begin(), root_idx.end());
 }
 
+// level L (>= 1) of plan p as kernel arguments
+static ForestLevelArgs level_args(const ForestPlan& p, int L, const uint8_t* d_leaves, uint8_t* d_inner,
+                                  int64_t* d_meta, int ignore_max, int check_order, int rfc, int32_t* d_status) {
+  const int rec = rfc ? kRecRfc : kRecNmt;
+  ForestLevelArgs a{};
+  a.in = L == 1 ? d_leaves : d_inner + (long)p.base[L - 1] * rec;
+  a.out = d_inner + (long)p.base[L] * rec;
+  if (p.uniform) {
+    a.in_off = nullptr;
+    a.in_tstride = L == 1 ? p.tstride0 : p.per[L - 1];
+    a.in_lstride = L == 1 ? p.lstride0 : 1;
+    a.in_per = p.per[L - 1];
+    a.out_off = nullptr;
+    a.out_per = p.per[L];
+  } else {
+    a.in_off = d_meta + p.meta_off[L - 1];
+    a.in_lstride = 1;
+    a.out_off = d_meta + p.meta_off[L];
+  }
+  a.ntrees = p.ntrees;
+  a.total_out = p.total[L];
+  a.ignore_max = ignore_max;
+  a.check_order = check_order && L == 1;
+  a.rfc = rfc;
+  a.status = d_status;
+  return a;
+}
+
 hipError_t forest_enqueue(const ForestPlan& p, const uint8_t* d_leaves, uint8_t* d_inner, int64_t* d_meta,
                           int ignore_max, int check_order, int rfc, int32_t* d_status, uint8_t* d_roots,
                           int records, long roots_stride, hipStream_t s) {
@@ -472,34 +510,48 @@ hipError_t forest_enqueue(const ForestPlan& p, const uint8_t* d_leaves, uint8_t*
   hipError_t e = hipMemcpyAsync(d_meta, p.meta.data(), p.meta.size() * sizeof(int64_t),
                                 hipMemcpyHostToDevice, s);
   if (e != hipSuccess) return e;
-  const int rec = rfc ? kRecRfc : kRecNmt;
   for (int L = 1; L <= p.nlevels; L++) {
-    ForestLevelArgs a{};
-    a.in = L == 1 ? d_leaves : d_inner + (long)p.base[L - 1] * rec;
-    a.out = d_inner + (long)p.base[L] * rec;
-    if (p.uniform) {
-      a.in_off = nullptr;
-      a.in_tstride = L == 1 ? p.tstride0 : p.per[L - 1];
-      a.in_lstride = L == 1 ? p.lstride0 : 1;
-      a.in_per = p.per[L - 1];
-      a.out_off = nullptr;
-      a.out_per = p.per[L];
-    } else {
-      a.in_off = d_meta + p.meta_off[L - 1];
-      a.in_lstride = 1;
-      a.out_off = d_meta + p.meta_off[L];
-    }
-    a.ntrees = p.ntrees;
-    a.total_out = p.total[L];
-    a.ignore_max = ignore_max;
-    a.check_order = check_order && L == 1;
-    a.rfc = rfc;
-    a.status = d_status;
-    e = launch_forest_level(a, s);
+    e = launch_forest_level(level_args(p, L, d_leaves, d_inner, d_meta, ignore_max, check_order, rfc, d_status), s);
     if (e != hipSuccess) return e;
   }
   return launch_forest_roots(d_leaves, d_inner, d_meta + p.meta_root, p.ntrees, rfc, records, d_roots,
                              roots_stride, s);
+}
+
+hipError_t forest_enqueue_pair(const ForestJob& x, const ForestJob& y, hipStream_t s) {
+  const ForestJob* j[2] = {&x, &y};
+  for (int f = 0; f < 2; f++) {
+    if (j[f]->p->ntrees == 0) continue;
+    hipError_t e = hipMemcpyAsync(j[f]->d_meta, j[f]->p->meta.data(), j[f]->p->meta.size() * sizeof(int64_t),
+                                  hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return e;
+  }
+  const int nl = x.p->nlevels > y.p->nlevels ? x.p->nlevels : y.p->nlevels;
+  for (int L = 1; L <= nl; L++) {
+    ForestLevelArgs a[2];
+    int n = 0;
+    for (int f = 0; f < 2; f++)
+      if (j[f]->p->ntrees > 0 && L <= j[f]->p->nlevels && j[f]->p->total[L] > 0)
+        a[n++] = level_args(*j[f]->p, L, j[f]->d_leaves, j[f]->d_inner, j[f]->d_meta, j[f]->ignore_max,
+                            j[f]->check_order, j[f]->rfc, j[f]->d_status);
+    hipError_t e = hipSuccess;
+    if (n == 1) {
+      e = launch_forest_level(a[0], s);
+    } else if (n == 2) {
+      const long total = a[0].total_out + a[1].total_out;
+      hipLaunchKernelGGL(forest_level2_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a[0], a[1]);
+      e = hipGetLastError();
+    }
+    if (e != hipSuccess) return e;
+  }
+  for (int f = 0; f < 2; f++) {
+    const ForestJob& q = *j[f];
+    if (q.p->ntrees == 0) continue;
+    hipError_t e = launch_forest_roots(q.d_leaves, q.d_inner, q.d_meta + q.p->meta_root, q.p->ntrees, q.rfc,
+                                       q.records, q.d_roots, q.roots_stride, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace dagpu

@@ -109,14 +109,17 @@ int dagpu_split_rows_device(dagpu_ctx* ctx, uint32_t k, uint32_t parts, uint32_t
   // nmt push order over whole Q0 rows (a row's Q0 part spans several slabs)
   HIP_TRY(ctx, dagpu::launch_ns_order_check(d_ods_rows, rows, k, (long)k * kSS, kSS, d_status,
                                             dagpu::kStatusPushOrder, s));
+  // one part: the send block is the whole row-major [Q0 | Q1] of the rows, so
+  // the encoder writes it in place (no staging copy)
+  uint8_t* rows_out = parts == 1 ? d_send : ws.rows_tmp;
   EncodeArgs ea{};
   ea.in = d_ods_rows;
   ea.in_vec_stride = (long)k * kSS;
   ea.in_shard_stride = kSS;
-  ea.copy = ws.rows_tmp;
+  ea.copy = rows_out;
   ea.copy_vec_stride = w * kSS;
   ea.copy_shard_stride = kSS;
-  ea.out = ws.rows_tmp + (long)k * kSS;
+  ea.out = rows_out + (long)k * kSS;
   ea.out_vec_stride = w * kSS;
   ea.out_shard_stride = kSS;
   ea.nsq = 1;
@@ -128,7 +131,7 @@ int dagpu_split_rows_device(dagpu_ctx* ctx, uint32_t k, uint32_t parts, uint32_t
     HIP_TRY(ctx, launch_rs_encode((int)k, ea, s));
   }
   // send block h = rows x columns [h*W, (h+1)*W), row-major
-  for (uint32_t h = 0; h < parts; h++) {
+  for (uint32_t h = 0; parts > 1 && h < parts; h++) {
     HIP_TRY(ctx, hipMemcpy2DAsync(d_send + (size_t)h * rows * W * kSS, (size_t)W * kSS,
                                   ws.rows_tmp + (size_t)h * W * kSS, (size_t)w * kSS, (size_t)W * kSS,
                                   (size_t)rows, hipMemcpyDeviceToDevice, s));
@@ -183,12 +186,13 @@ int dagpu_split_cols_device(dagpu_ctx* ctx, uint32_t k, uint32_t parts, uint32_t
   }
   {
     ProfScope p(ctx, 3, s);
-    // full column trees (push order of Q0 columns checked at level 1)
-    HIP_TRY(ctx, dagpu::forest_enqueue(pl.cols, ws.leaves, ws.col_inner, ws.meta, 1, 1, 0, d_status, d_col_roots,
-                                       0, 0, s));
-    // row subtrees over this slab (row order was checked on the row owners)
-    HIP_TRY(ctx, dagpu::forest_enqueue(pl.rows, ws.leaves, ws.row_inner, ws.meta + pl.cols.meta.size(), 1, 0, 0,
-                                       nullptr, d_row_sub, 1, 0, s));
+    // full column trees (push order of Q0 columns checked at level 1) and the
+    // row subtrees over this slab (row order was checked on the row owners),
+    // each level of both in one launch
+    const dagpu::ForestJob cols{&pl.cols, ws.leaves, ws.col_inner, ws.meta, 1, 1, 0, d_status, d_col_roots, 0, 0};
+    const dagpu::ForestJob rows{&pl.rows, ws.leaves, ws.row_inner, ws.meta + pl.cols.meta.size(), 1, 0, 0,
+                                nullptr, d_row_sub, 1, 0};
+    HIP_TRY(ctx, dagpu::forest_enqueue_pair(cols, rows, s));
   }
   HIP_TRY(ctx, hipStreamSynchronize(s));  // plans' metadata uploads complete
   return DAGPU_OK;
