@@ -1188,51 +1188,43 @@ __device__ __forceinline__ void fft2_p(W1k& w, int i, int j, const PTab& t) {
 // p02; i over N butterflies starting at s0 with stride ST.
 template <int N, int ST, int D>
 __device__ __forceinline__ void ifftp_r4(W1k& w, int s0, int p01, int p02, int p23) {
-  {
-    const PTab t = ptab(p01);
-#pragma unroll
-    for (int u = 0; u < N; u++) ifft2_p(w, s0 + ST * u, s0 + ST * u + D, t);
-  }
+  // each phase's table is loaded before the previous phase runs (its scalar
+  // load latency hidden behind that phase's multiplies)
+  const PTab t01 = ptab(p01);
+  const PTab t23 = ptab(p23);
   __builtin_amdgcn_sched_barrier(0);
-  {
-    const PTab t = ptab(p23);
 #pragma unroll
-    for (int u = 0; u < N; u++) ifft2_p(w, s0 + ST * u + 2 * D, s0 + ST * u + 3 * D, t);
-  }
+  for (int u = 0; u < N; u++) ifft2_p(w, s0 + ST * u, s0 + ST * u + D, t01);
+  const PTab t02 = ptab(p02);
   __builtin_amdgcn_sched_barrier(0);
-  {
-    const PTab t = ptab(p02);
 #pragma unroll
-    for (int u = 0; u < N; u++) {
-      ifft2_p(w, s0 + ST * u, s0 + ST * u + 2 * D, t);
-      ifft2_p(w, s0 + ST * u + D, s0 + ST * u + 3 * D, t);
-    }
+  for (int u = 0; u < N; u++) ifft2_p(w, s0 + ST * u + 2 * D, s0 + ST * u + 3 * D, t23);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int u = 0; u < N; u++) {
+    ifft2_p(w, s0 + ST * u, s0 + ST * u + 2 * D, t02);
+    ifft2_p(w, s0 + ST * u + D, s0 + ST * u + 3 * D, t02);
   }
   __builtin_amdgcn_sched_barrier(0);
 }
 // FFT: (i, i+2D), (i+D, i+3D) at p02, then (i, i+D) at p01, (i+2D, i+3D) at p23
 template <int N, int ST, int D>
 __device__ __forceinline__ void fftp_r4(W1k& w, int s0, int p01, int p02, int p23) {
-  {
-    const PTab t = ptab(p02);
-#pragma unroll
-    for (int u = 0; u < N; u++) {
-      fft2_p(w, s0 + ST * u, s0 + ST * u + 2 * D, t);
-      fft2_p(w, s0 + ST * u + D, s0 + ST * u + 3 * D, t);
-    }
-  }
+  const PTab t02 = ptab(p02);
+  const PTab t01 = ptab(p01);
   __builtin_amdgcn_sched_barrier(0);
-  {
-    const PTab t = ptab(p01);
 #pragma unroll
-    for (int u = 0; u < N; u++) fft2_p(w, s0 + ST * u, s0 + ST * u + D, t);
+  for (int u = 0; u < N; u++) {
+    fft2_p(w, s0 + ST * u, s0 + ST * u + 2 * D, t02);
+    fft2_p(w, s0 + ST * u + D, s0 + ST * u + 3 * D, t02);
   }
+  const PTab t23 = ptab(p23);
   __builtin_amdgcn_sched_barrier(0);
-  {
-    const PTab t = ptab(p23);
 #pragma unroll
-    for (int u = 0; u < N; u++) fft2_p(w, s0 + ST * u + 2 * D, s0 + ST * u + 3 * D, t);
-  }
+  for (int u = 0; u < N; u++) fft2_p(w, s0 + ST * u, s0 + ST * u + D, t01);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int u = 0; u < N; u++) fft2_p(w, s0 + ST * u + 2 * D, s0 + ST * u + 3 * D, t23);
   __builtin_amdgcn_sched_barrier(0);
 }
 
