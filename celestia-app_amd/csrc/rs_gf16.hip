@@ -627,11 +627,21 @@ __device__ __forceinline__ void enc16_load(const EncodeArgs& a, W16n<NS>& w, int
   }
 }
 
+// Repair fill: which of the wave's NS out-half shards are given (bit j:
+// shard NS q + j), read before the transform so that the store loop does not
+// wait on presence loads.
+template <int NS>
+__device__ __forceinline__ uint64_t enc16_given(const EncodeArgs& a, int q, long sq, long vec, int lane) {
+  if (!a.out_present) return 0;
+  const bool g = lane < NS && fill_given(a, sq, vec, NS * q + (lane < NS ? lane : 0));
+  return __builtin_amdgcn_ballot_w64(g);
+}
+
 // The encoders' three output modes: compare (prerepairSanityCheck), Repair
 // fill (store missing shards, compare given ones) and plain store.
 template <int NS>
 __device__ __forceinline__ void enc16_store(const EncodeArgs& a, const W16n<NS>& w, int q, long sq, long vec, long sv,
-                                            uint32_t col, bool active) {
+                                            uint32_t col, bool active, uint64_t given) {
   if (!active) return;
   const auto out_rsrc = make_rsrc(a.out + sq * a.out_sq_stride + vec * a.out_vec_stride);
   const uint32_t os = (uint32_t)a.out_shard_stride;
@@ -654,7 +664,7 @@ __device__ __forceinline__ void enc16_store(const EncodeArgs& a, const W16n<NS>&
 #pragma unroll
     for (int j = 0; j < NS; j++) {
       const uint32_t so = (uint32_t)(NS * q + j) * os;
-      if (fill_given(a, sq, vec, NS * q + j)) {  // wave-uniform
+      if ((given >> j) & 1) {  // wave-uniform
         diff |= w.lo[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, col, so, 0);
         diff |= w.hi[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, col + 32u, so, 0);
       } else {
@@ -701,6 +711,7 @@ leo16_encode_reg_kernel(EncodeArgs a) {
   const uint32_t cl = active ? col : 0u;  // inactive lanes read valid memory, store nothing
   W16 w;
   enc16_load(a, w, q, sq, vec, col, cl, active);
+  const uint64_t given = enc16_given<64>(a, q, sq, vec, lane);
   // ---- IFFT (ifftDITEncoder, skew index IO - 1 + iend) ----
   ifft16_block<1>(w, IO - 1 + 64 * q);  // bits 0-5
   xpose16<P, S>(w, lds, q, lane);
@@ -753,7 +764,7 @@ leo16_encode_reg_kernel(EncodeArgs a) {
     xpose16<P, S>(w, lds, q, lane);
     fft16_block<16>(w, FO + 64 * q);  // bits 5 .. 0
   }
-  enc16_store(a, w, q, sq, vec, sv, col, active);
+  enc16_store(a, w, q, sq, vec, sv, col, active, given);
 }
 
 // 32 elements per wave: M = 512 over 16 waves (1,024 threads), M = 256 over 8
@@ -785,6 +796,7 @@ __global__ __launch_bounds__(M * 2) void leo16_encode_reg32_kernel(EncodeArgs a)
   const uint32_t cl = active ? col : 0u;
   W16n<NS> w;
   enc16_load(a, w, q, sq, vec, col, cl, active);
+  const uint64_t given = enc16_given<NS>(a, q, sq, vec, lane);
   // ---- IFFT (ifftDITEncoder, skew index IO - 1 + iend) ----
   ifft16_block<1, NS>(w, IO - 1 + NS * q);  // bits 0-3
 #pragma unroll
@@ -870,7 +882,7 @@ __global__ __launch_bounds__(M * 2) void leo16_encode_reg32_kernel(EncodeArgs a)
   }
   xpose16<P, S, NS>(w, lds32, q, lane);
   fft16_block<8, NS>(w, FO + NS * q);  // bits 4 .. 0
-  enc16_store(a, w, q, sq, vec, sv, col, active);
+  enc16_store(a, w, q, sq, vec, sv, col, active, given);
 }
 
 // ---------------------------------------------------------------------------
