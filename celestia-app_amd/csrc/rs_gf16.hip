@@ -1301,6 +1301,21 @@ __device__ __forceinline__ void derivativep(W1k& w, uint32_t* lds, int c, int la
   }
 }
 
+// DAGPU_PHASE_PROBE builds (tools/phase_probe_dec512.py, never the product
+// library): lane 0 of waves 0 and 15 stamp s_memtime at the decoder's phase
+// boundaries, [block][wave 0 / 15][phase].
+#ifdef DAGPU_PHASE_PROBE
+constexpr int kProbePhases = 12;
+__device__ uint64_t g_probe[8192 * 2 * kProbePhases];
+#define DEC_PROBE(i)                                                                            \
+  do {                                                                                          \
+    if ((threadIdx.x & 63) == 0 && (q == 0 || q == 15) && blk < 8192)                           \
+      g_probe[(blk * 2 + (q == 15)) * kProbePhases + (i)] = __builtin_amdgcn_s_memtime();       \
+  } while (0)
+#else
+#define DEC_PROBE(i) ((void)0)
+#endif
+
 __global__ __launch_bounds__(kDec1k) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_decode_reg1k_kernel(
     DecodeArgs a) {
   constexpr int K = kDec1k / 2;
@@ -1316,6 +1331,7 @@ __global__ __launch_bounds__(kDec1k) __attribute__((amdgpu_waves_per_eu(4, 4))) 
   const long sq = v / a.nvec, vec = v % a.nvec;
   const int lane = threadIdx.x & 63;
   const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  DEC_PROBE(0);
   // lane: 64-B block (lane >> 4) of this 256-B piece, symbols 2 (lane & 15) and +1
   // (memory: lane pair 2m, 2m+1 moves the dword of low bytes and the dword of
   // high bytes of symbols 4m .. 4m+3, even lane the low one)
@@ -1349,6 +1365,7 @@ __global__ __launch_bounds__(kDec1k) __attribute__((amdgpu_waves_per_eu(4, 4))) 
   mul16_table_to(lds + threadIdx.x * 16, my_err, !((pm >> lane) & 1));
   mul16_table_to(post_tab + threadIdx.x * 16, kMod16 - my_err);
   __syncthreads();
+  DEC_PROBE(1);
   const int q_pm = opaque_s(q);
 #pragma unroll
   for (int j = 0; j < 64; j++) {
@@ -1358,9 +1375,12 @@ __global__ __launch_bounds__(kDec1k) __attribute__((amdgpu_waves_per_eu(4, 4))) 
     __builtin_amdgcn_sched_barrier(0);  // one element's table live at a time
   }
   __syncthreads();  // the transpose reuses lds
+  DEC_PROBE(2);
   // ---- IFFT (ifftDITDecoder, skew index iend - 1) ----
   ifftp_block<1>(w, -1 + 64 * q);  // bits 0-5
+  DEC_PROBE(3);
   xposep(w, lds, q, lane);
+  DEC_PROBE(4);
 #pragma unroll
   for (int hr = 0; hr < 4; hr++) {  // radix-4 dist 64 (bits 6, 7), r = 256 hr: slots 16 hr + b, b < 4
     const int p01 = opaque_s(256 * hr + 63);
@@ -1370,7 +1390,9 @@ __global__ __launch_bounds__(kDec1k) __attribute__((amdgpu_waves_per_eu(4, 4))) 
     const int p01 = opaque_s(255);
     ifftp_r4<16, 1, 16>(w, 0, p01, p01 + 256, p01 + 512);
   }
+  DEC_PROBE(5);
   derivativep(w, lds, q, lane);
+  DEC_PROBE(6);
   // ---- FFT (fftDIT, skew index iend - 1) ----
   {  // dist 256
     const int p01 = opaque_s(255);
@@ -1381,8 +1403,11 @@ __global__ __launch_bounds__(kDec1k) __attribute__((amdgpu_waves_per_eu(4, 4))) 
     const int p01 = opaque_s(256 * hr + 63);
     fftp_r4<4, 1, 4>(w, 16 * hr, p01, p01 + 64, p01 + 128);
   }
+  DEC_PROBE(7);
   xposep(w, lds, q, lane);
+  DEC_PROBE(8);
   fftp_block<16>(w, 64 * q);  // dist 16, 4, 1 (bits 5 .. 0)
+  DEC_PROBE(9);
   // erased shards = work * (65535 - errLocs); pm, q opaque as in leo16_decode_reg_kernel
   uint64_t pm_e = pm;
   int q_e = q;
@@ -1402,6 +1427,7 @@ __global__ __launch_bounds__(kDec1k) __attribute__((amdgpu_waves_per_eu(4, 4))) 
     __builtin_amdgcn_raw_buffer_store_b32(out, rsrc, wcol, so, 0);
     __builtin_amdgcn_sched_barrier(0);
   }
+  DEC_PROBE(10);
 }
 
 // Tables are module globals: upload once per device.
@@ -1793,3 +1819,15 @@ hipError_t launch_rs_decode(const DecodeArgs& a, hipStream_t s, bool mark_presen
 }
 
 }  // namespace dagpu
+
+#ifdef DAGPU_PHASE_PROBE
+// probe builds only: op 0 clears the stamps, op 1 copies n of them to out
+extern "C" int dagpu_debug_probe(int op, uint64_t* out, size_t n) {
+  if (op == 0) {
+    static uint64_t zero[8192 * 2 * dagpu::kProbePhases];
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(dagpu::g_probe), zero, sizeof zero);
+  }
+  if (n > 8192 * 2 * (size_t)dagpu::kProbePhases) n = 8192 * 2 * (size_t)dagpu::kProbePhases;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(dagpu::g_probe), n * sizeof(uint64_t));
+}
+#endif
