@@ -904,13 +904,6 @@ __global__ __launch_bounds__(M * 2) void leo16_encode_reg32_kernel(EncodeArgs a)
 // ---------------------------------------------------------------------------
 constexpr int kDecN = 512;
 
-// x * exp(lm) for a field element x with log logx (0 for x = 0)
-__device__ __forceinline__ uint32_t mul16_prod(uint32_t x, uint32_t logx, uint32_t lm) {
-  uint32_t sidx = logx + lm;
-  sidx = (sidx + (sidx >> 16)) & 0xFFFFu;
-  return x ? (uint32_t)g_exp16[sidx] : 0u;
-}
-
 // (xlo, xhi) = (xlo, xhi) * exp(lm) with its 16-dword product table (mul16_table_to)
 __device__ __forceinline__ void mul16_by(uint32_t& xlo, uint32_t& xhi, const uint32_t (&t)[16]) {
   uint32_t pl[8], ph[8];
@@ -934,18 +927,31 @@ __device__ __forceinline__ void mul16_by(uint32_t& xlo, uint32_t& xhi, const uin
 // out[G] byte e2 = low byte of (e2 << 2G) * exp(lm), out[8 + G] its high byte.
 // zero: the all-zero table (multiply by 0: the decoders' premultiply of a
 // missing shard, whose bytes are then never selected out of the loaded word)
+// Round 4: only the 16 products (1 << b) * exp(lm) are gathered (the e2 = 3
+// entry of a group is the XOR of its e2 = 1 and e2 = 2 entries, the multiply
+// being GF(2)-linear), their logs come from g_logbit16 (scalar loads), and a
+// zero table gathers nothing: the workgroup's table phase was bound by its
+// random 2-B gathers (tools/phase_probe_dec512.py: 22 % of the k = 512 decoder).
+__constant__ uint16_t g_logbit16[16];  // log of the element 1 << b
 __device__ __forceinline__ void mul16_table_to(uint32_t* out, uint32_t lm, bool zero = false) {
+  uint32_t pb[16];
+  if (!zero) {
+#pragma unroll
+    for (int b = 0; b < 16; b++) {
+      uint32_t sidx = (uint32_t)g_logbit16[b] + lm;
+      sidx = (sidx + (sidx >> 16)) & 0xFFFFu;
+      pb[b] = g_exp16[sidx];
+    }
+  } else {
+#pragma unroll
+    for (int b = 0; b < 16; b++) pb[b] = 0u;
+  }
   uint32_t lo[8], hi[8];
 #pragma unroll
   for (int G = 0; G < 8; G++) {
-    lo[G] = hi[G] = 0u;
-#pragma unroll
-    for (int e2 = 1; e2 < 4; e2++) {
-      const uint32_t x = (uint32_t)e2 << (2 * G);
-      const uint32_t p = zero ? 0u : mul16_prod(x, (uint32_t)g_log16[x], lm);
-      lo[G] |= (p & 0xFFu) << (8 * e2);
-      hi[G] |= (p >> 8) << (8 * e2);
-    }
+    const uint32_t p1 = pb[2 * G], p2 = pb[2 * G + 1], p3 = p1 ^ p2;
+    lo[G] = ((p1 & 0xFFu) << 8) | ((p2 & 0xFFu) << 16) | ((p3 & 0xFFu) << 24);
+    hi[G] = ((p1 >> 8) << 8) | ((p2 >> 8) << 16) | ((p3 >> 8) << 24);
   }
   uint4* o = (uint4*)out;
   o[0] = make_uint4(lo[0], lo[1], lo[2], lo[3]);
@@ -1042,7 +1048,7 @@ __global__ __launch_bounds__(kDecN) __attribute__((amdgpu_waves_per_eu(2, 2))) v
   // one in the transpose buffer, free until the first transpose; the erasure
   // one kept to the end), each wave then reads its 64 elements' tables
   mul16_table_to(lds + threadIdx.x * 16, my_err, !((pm >> lane) & 1));
-  mul16_table_to(post_tab + threadIdx.x * 16, kMod16 - my_err);
+  mul16_table_to(post_tab + threadIdx.x * 16, kMod16 - my_err, (pm >> lane) & 1);  // read for missing shards only
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < 64; j++) {
@@ -1363,7 +1369,7 @@ __global__ __launch_bounds__(kDec1k) __attribute__((amdgpu_waves_per_eu(4, 4))) 
   // one in the transpose buffer, free until the first transpose; the erasure
   // one kept to the end), each wave then reads its 64 elements' tables
   mul16_table_to(lds + threadIdx.x * 16, my_err, !((pm >> lane) & 1));
-  mul16_table_to(post_tab + threadIdx.x * 16, kMod16 - my_err);
+  mul16_table_to(post_tab + threadIdx.x * 16, kMod16 - my_err, (pm >> lane) & 1);  // read for missing shards only
   __syncthreads();
   DEC_PROBE(1);
   const int q_pm = opaque_s(q);
@@ -1500,6 +1506,9 @@ hipError_t ensure_tables() {
         }
     }
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_ptab16_merged), mt.data(), mt.size() * 4)) != hipSuccess) return e;
+    uint16_t lb[16];
+    for (int b = 0; b < 16; b++) lb[b] = (uint16_t)t.log[1u << b];
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_logbit16), lb, sizeof lb)) != hipSuccess) return e;
   }
   // > 64 KiB of dynamic LDS (errlocs 128 KiB, k = 512 decode 128 KiB)
   if ((e = hipFuncSetAttribute((const void*)leo16_errlocs_kernel,

@@ -50,5 +50,9 @@ case "$1" in
     bash tools/gpu_ab.sh --tests "tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py tests/test_gpu_parity.py" --rounds 2 repair128 new= prev=lib:celestia-app_amd/libdagpu_prev.so && \
     bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 128 --batch 256 --steps 5 --warmup 1 --pattern q3" new= prev=lib:celestia-app_amd/libdagpu_prev.so
     ;;
-  *) echo "steps: async dec512 enc-merge forest-multi enc32 dah split-pair dec512-prefetch fill-given gf8-fill-given"; exit 2;;
+  tables)  # round 4: decoder product tables from 16 gathers (e2 = 3 by XOR), logs from constants, none for unused tables: tests, A/B vs the previous build
+    bash tools/gpu_ab.sh --tests "tests/test_gpu_gf16.py tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py tests/test_gpu_wide.py" --rounds 2 repair512 new= prev=lib:celestia-app_amd/libdagpu_prev.so && \
+    bash tools/gpu_ab.sh --rounds 1 "bench:--mode repair --k 256 --batch 8 --steps 5 --warmup 1" new= prev=lib:celestia-app_amd/libdagpu_prev.so
+    ;;
+  *) echo "steps: async dec512 enc-merge forest-multi enc32 dah split-pair dec512-prefetch fill-given gf8-fill-given tables"; exit 2;;
 esac
