@@ -54,5 +54,9 @@ case "$1" in
     bash tools/gpu_ab.sh --tests "tests/test_gpu_gf16.py tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py tests/test_gpu_wide.py" --rounds 2 repair512 new= prev=lib:celestia-app_amd/libdagpu_prev.so && \
     bash tools/gpu_ab.sh --rounds 1 "bench:--mode repair --k 256 --batch 8 --steps 5 --warmup 1" new= prev=lib:celestia-app_amd/libdagpu_prev.so
     ;;
-  *) echo "steps: async dec512 enc-merge forest-multi enc32 dah split-pair dec512-prefetch fill-given gf8-fill-given tables"; exit 2;;
+  tables-first)  # round 4: k = 512 decoder issues its table gathers before the data loads (the barrier no longer waits for the data): tests, A/B
+    bash tools/gpu_ab.sh --tests "tests/test_gpu_gf16.py tests/test_gpu_repair_fill.py" --rounds 3 repair512 new= prev=lib:celestia-app_amd/libdagpu_prev.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 256 --batch 8 --steps 5 --warmup 1" new= prev=lib:celestia-app_amd/libdagpu_prev.so
+    ;;
+  *) echo "steps: async dec512 enc-merge forest-multi enc32 dah split-pair dec512-prefetch fill-given gf8-fill-given tables tables-first"; exit 2;;
 esac
