@@ -130,6 +130,20 @@ __device__ __forceinline__ void dec_derivative_half(uint32_t (&v)[16][8], u32x4*
   if (!(w & 2)) add(8);
 }
 
+// DAGPU_PHASE_PROBE builds only (tools/phase_probe.py): lane 0 of waves 0 and 3
+// stamp s_memtime at the phase boundaries, [block][wave 0 / 3][phase].
+#ifdef DAGPU_PHASE_PROBE
+constexpr int kProbe8Phases = 14;
+__device__ uint64_t g_probe8[8192 * 2 * kProbe8Phases];
+#define DEC8_PROBE(i)                                                                           \
+  do {                                                                                          \
+    if ((threadIdx.x & 63) == 0 && (w == 0 || w == 3) && blk < 8192)                            \
+      g_probe8[(blk * 2 + (w == 3)) * kProbe8Phases + (i)] = __builtin_amdgcn_s_memtime();      \
+  } while (0)
+#else
+#define DEC8_PROBE(i) ((void)0)
+#endif
+
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void leo8_decode128_sliced_kernel(DecodeArgs a) {
   constexpr int K = 128;
@@ -150,6 +164,7 @@ void leo8_decode128_sliced_kernel(DecodeArgs a) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int t = lane & 15, eb = lane >> 4;
+  DEC8_PROBE(0);
   const long sq = v / a.nvec, vec = v % a.nvec;
   const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
   const uint8_t* err = a.err + err_vec(a, v) * 256;
@@ -184,21 +199,33 @@ void leo8_decode128_sliced_kernel(DecodeArgs a) {
     mul_packed(v_[j], mtab[ti], mtab2[ti]);
     transpose8(v_[j]);
   }
+  DEC8_PROBE(1);
   const uint32_t eb0mask = (eb & 1) ? 0xFFFFFFFFu : 0u, eb1mask = (eb & 2) ? 0xFFFFFFFFu : 0u;
   // layers 2..3 in A* instead of A: no lane terms (repair 19.5-19.7 -> 19.3 ms per 256 squares)
   dec_A<true, 2>(v_, w, eb0mask, eb1mask);
+  DEC8_PROBE(2);
   dec_transpose_wave<true>(v_, lds, w, eb, t);
+  DEC8_PROBE(3);
   dec_Astar<true>(v_, w);
+  DEC8_PROBE(4);
   dec_exchange<true>(v_, lds, w, eb, t);
+  DEC8_PROBE(5);
   dec_B<true>(v_);
+  DEC8_PROBE(6);
   dec_derivative_half<0>(v_, lds, w, eb, t);
   dec_derivative_half<1>(v_, lds, w, eb, t);
+  DEC8_PROBE(7);
   dec_B<false>(v_);
+  DEC8_PROBE(8);
   dec_exchange<false>(v_, lds, w, eb, t);
+  DEC8_PROBE(9);
   dec_Astar<false>(v_, w);
+  DEC8_PROBE(10);
   __syncthreads();  // other waves' last reads of this wave's quarter of lds are done
   dec_transpose_wave<false>(v_, lds, w, eb, t);
+  DEC8_PROBE(11);
   dec_A<false, 2>(v_, w, eb0mask, eb1mask);
+  DEC8_PROBE(12);
   // missing shard = work * exp(255 - errLocs)
 #pragma unroll
   for (int j = 0; j < 16; j++) {
@@ -213,6 +240,7 @@ void leo8_decode128_sliced_kernel(DecodeArgs a) {
                                              soff, 0);
     }
   }
+  DEC8_PROBE(13);
 }
 
 // DAGPU_DEC_SLICED=0 keeps k = 128 on the packed-byte decoder (A/B runs).
@@ -241,3 +269,14 @@ hipError_t launch_leo8_decode128_sliced(const DecodeArgs& a, hipStream_t s) {
 }
 
 }  // namespace dagpu
+
+#ifdef DAGPU_PHASE_PROBE
+extern "C" int dagpu_debug_probe8(int op, uint64_t* out, size_t n) {
+  if (op == 0) {
+    static uint64_t zero[8192 * 2 * dagpu::kProbe8Phases];
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(dagpu::g_probe8), zero, sizeof zero);
+  }
+  if (n > 8192 * 2 * (size_t)dagpu::kProbe8Phases) n = 8192 * 2 * (size_t)dagpu::kProbe8Phases;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(dagpu::g_probe8), n * sizeof(uint64_t));
+}
+#endif

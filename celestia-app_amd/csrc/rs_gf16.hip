@@ -931,7 +931,7 @@ __device__ __forceinline__ void mul16_by(uint32_t& xlo, uint32_t& xhi, const uin
 // entry of a group is the XOR of its e2 = 1 and e2 = 2 entries, the multiply
 // being GF(2)-linear), their logs come from g_logbit16 (scalar loads), and a
 // zero table gathers nothing: the workgroup's table phase was bound by its
-// random 2-B gathers (tools/phase_probe_dec512.py: 22 % of the k = 512 decoder).
+// random 2-B gathers (tools/phase_probe.py dec512: 22 % of the k = 512 decoder).
 __constant__ uint16_t g_logbit16[16];  // log of the element 1 << b
 __device__ __forceinline__ void mul16_table_to(uint32_t* out, uint32_t lm, bool zero = false) {
   uint32_t pb[16];
@@ -1308,7 +1308,7 @@ __device__ __forceinline__ void derivativep(W1k& w, uint32_t* lds, int c, int la
   }
 }
 
-// DAGPU_PHASE_PROBE builds (tools/phase_probe_dec512.py, never the product
+// DAGPU_PHASE_PROBE builds (tools/phase_probe.py dec512, never the product
 // library): lane 0 of waves 0 and 15 stamp s_memtime at the decoder's phase
 // boundaries, [block][wave 0 / 15][phase].
 #ifdef DAGPU_PHASE_PROBE
