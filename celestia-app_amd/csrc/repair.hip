@@ -75,9 +75,13 @@ __global__ __launch_bounds__(256) void axis_complete_rows_kernel(const uint8_t* 
 // Columns, w % 4 == 0 and 4-B aligned presence: block = (square, 256 columns);
 // lane j holds columns 4j..4j+3 (dword loads, coalesced along the row), the
 // four waves take every fourth row, AND-combined in LDS.
-__global__ __launch_bounds__(256) void axis_complete_cols_kernel(const uint8_t* present, int k, long nsq,
-                                                                 int32_t* complete, int32_t* ncomplete) {
-  __shared__ uint32_t acc_s[4][64];
+// 16 waves split the rows of a 256-column group, 16 loads in flight per lane
+// (4 waves walking all w rows one dependent load at a time took ~38 us for two
+// k = 512 squares: 8 workgroups on 8 CUs)
+constexpr int kColWaves = 16;
+__global__ __launch_bounds__(64 * kColWaves) void axis_complete_cols_kernel(const uint8_t* present, int k, long nsq,
+                                                                            int32_t* complete, int32_t* ncomplete) {
+  __shared__ uint32_t acc_s[kColWaves][64];
   const int w = 2 * k;
   const int ngrp = (w + 255) / 256;
   const long sq = blockIdx.x / ngrp;
@@ -87,12 +91,15 @@ __global__ __launch_bounds__(256) void axis_complete_cols_kernel(const uint8_t* 
   uint32_t acc = 0x80808080u;
   if (c < w) {
     const uint8_t* p = present + sq * (long)w * w + c;
-    for (int r = wave; r < w; r += 4) acc &= nonzero_bytes_hi(*(const uint32_t*)(p + (long)r * w));
+#pragma unroll 16
+    for (int r = wave; r < w; r += kColWaves) acc &= nonzero_bytes_hi(*(const uint32_t*)(p + (long)r * w));
   }
   acc_s[wave][lane] = acc;
   __syncthreads();
   if (wave == 0 && c < w) {
-    const uint32_t all = acc_s[0][lane] & acc_s[1][lane] & acc_s[2][lane] & acc_s[3][lane];
+    uint32_t all = acc_s[0][lane];
+#pragma unroll
+    for (int q = 1; q < kColWaves; q++) all &= acc_s[q][lane];
     int32_t* out = complete + nsq * w + sq * w + c;
     int nc = 0;
 #pragma unroll
@@ -114,8 +121,8 @@ hipError_t launch_axis_complete(const uint8_t* present, int k, long nsq, int32_t
     const long threads = nsq * w * (w / 16);
     hipLaunchKernelGGL(axis_complete_rows_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, present,
                        k, nsq, complete, ncomplete);
-    hipLaunchKernelGGL(axis_complete_cols_kernel, dim3((unsigned)(nsq * ((w + 255) / 256))), dim3(256), 0, s,
-                       present, k, nsq, complete, ncomplete);
+    hipLaunchKernelGGL(axis_complete_cols_kernel, dim3((unsigned)(nsq * ((w + 255) / 256))), dim3(64 * kColWaves),
+                       0, s, present, k, nsq, complete, ncomplete);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(axis_complete_kernel, dim3((unsigned)n), dim3(64), 0, s, present, k, nsq, complete, ncomplete);
@@ -329,6 +336,7 @@ __global__ __launch_bounds__(1024) void vec_count_cols_kernel(DecodeArgs a) {
   if (vec < a.nvec) {
     const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
     int sys = 0, tot = 0;
+#pragma unroll 8
     for (int i = wave; i < n; i += 16) {
       const int c = pres[(long)i * a.p_shard_stride] != 0;
       tot += c;

@@ -61,5 +61,10 @@ case "$1" in
   dec128-loads)  # round 4: k = 128 decoder issues its data loads before building the multiply tables: tests, A/B
     bash tools/gpu_ab.sh --tests "tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py tests/test_gpu_parity.py" --rounds 3 repair128 new= prev=lib:celestia-app_amd/libdagpu_prev.so
     ;;
-  *) echo "steps: async dec512 enc-merge forest-multi enc32 dah split-pair dec512-prefetch fill-given gf8-fill-given tables tables-first dec128-loads"; exit 2;;
+  col-maps)  # round 4: column presence-map kernels with more loads in flight (axis_complete_cols 16 waves, unrolled row loops): tests, A/B
+    bash tools/gpu_ab.sh --tests "tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py tests/test_gpu_parity.py tests/test_gpu_gf16.py" --rounds 2 repair512q3 new= prev=lib:celestia-app_amd/libdagpu_prev.so && \
+    bash tools/gpu_ab.sh --rounds 2 repair128 new= prev=lib:celestia-app_amd/libdagpu_prev.so && \
+    bash tools/gpu_ab.sh --rounds 1 repair512 new= prev=lib:celestia-app_amd/libdagpu_prev.so
+    ;;
+  *) echo "steps: async dec512 enc-merge forest-multi enc32 dah split-pair dec512-prefetch fill-given gf8-fill-given tables tables-first dec128-loads col-maps"; exit 2;;
 esac
