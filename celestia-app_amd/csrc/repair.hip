@@ -270,7 +270,7 @@ constexpr int kPlanThreads = 256;
 
 // Present shards per vector (all, and of the data half) -> flags, vec_counts,
 // *ndecodable.  The layouts of the locator-key kernels (rs_gf16.hip): contiguous
-// flags (p_shard_stride == 1, the row axis): one wave per vector, 16 flags per
+// flags (p_shard_stride == 1, the row axis): 16 lanes per vector, 16 flags per
 // lane load; otherwise (column axis) one lane per vector, the 2k flags split
 // over the 16 waves of the block and summed in LDS.  (One lane per vector
 // throughout took 0.1 ms per launch at k = 512, 2 squares: 2,048 lanes in all.)
@@ -283,40 +283,56 @@ __device__ __forceinline__ void vec_count_finish(const DecodeArgs& a, long v, in
   if (decode) atomicAdd(blk_cnt, 1);
 }
 
+// Rows of the presence map: 16 lanes per row (4 rows per wave) when the row's
+// 16-flag loads each lie inside one half (k >= 16, aligned), one row per wave
+// otherwise (a wave per row spent most of its time launching and reducing:
+// 35 us for 256 k = 128 squares).
 __global__ __launch_bounds__(1024) void vec_count_rows_kernel(DecodeArgs a) {
   __shared__ int blk_cnt;
   if (threadIdx.x == 0) blk_cnt = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const long v = (long)blockIdx.x * 16 + wave;  // wave-uniform
-  if (v < a.nsq * a.nvec) {
-    const long sq = v / a.nvec;
-    const uint8_t* pres = a.present + sq * a.p_sq_stride + (v - sq * a.nvec) * a.p_vec_stride;
-    const int k = a.k, n = 2 * k;
+  const int k = a.k, n = 2 * k;
+  const long nv = a.nsq * a.nvec;
+  if (k >= 16 && ((uintptr_t)a.present & 15) == 0 && (a.p_vec_stride & 15) == 0 && (a.p_sq_stride & 15) == 0) {
+    // a 16-flag load straddling index k would count parity flags as data: k >= 16
+    const long v = ((long)blockIdx.x * 16 + wave) * 4 + (lane >> 4);
+    const int sl = lane & 15;
     int sys = 0, tot = 0;
-    // 16-flag loads only where every load lies inside one half (k >= 16): a
-    // load straddling index k would count parity flags as data
-    if (k >= 16 && ((uintptr_t)pres & 15) == 0) {
-      const uint4* q = (const uint4*)pres;
-      for (int j = lane; j < n / 16; j += 64) {
+    if (v < nv) {
+      const long sq = v / a.nvec;
+      const uint4* q = (const uint4*)(a.present + sq * a.p_sq_stride + (v - sq * a.nvec) * a.p_vec_stride);
+      for (int j = sl; j < n / 16; j += 16) {
         const uint4 x = q[j];
         const int c = nonzero_bytes(x.x) + nonzero_bytes(x.y) + nonzero_bytes(x.z) + nonzero_bytes(x.w);
         tot += c;
         if (16 * j < k) sys += c;
       }
-    } else {
+    }
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) {  // within the 16-lane group
+      sys += __shfl_xor(sys, off);
+      tot += __shfl_xor(tot, off);
+    }
+    if (sl == 0 && v < nv) vec_count_finish(a, v, sys, tot, &blk_cnt);
+  } else {
+    const long v = (long)blockIdx.x * 16 + wave;  // wave-uniform
+    if (v < nv) {
+      const long sq = v / a.nvec;
+      const uint8_t* pres = a.present + sq * a.p_sq_stride + (v - sq * a.nvec) * a.p_vec_stride;
+      int sys = 0, tot = 0;
       for (int i = lane; i < n; i += 64) {
         const int c = pres[i] != 0;
         tot += c;
         if (i < k) sys += c;
       }
-    }
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      sys += __shfl_xor(sys, off);
-      tot += __shfl_xor(tot, off);
+      for (int off = 32; off > 0; off >>= 1) {
+        sys += __shfl_xor(sys, off);
+        tot += __shfl_xor(tot, off);
+      }
+      if (lane == 0) vec_count_finish(a, v, sys, tot, &blk_cnt);
     }
-    if (lane == 0) vec_count_finish(a, v, sys, tot, &blk_cnt);
   }
   __syncthreads();
   if (threadIdx.x == 0 && blk_cnt && a.ndecodable) atomicAdd(a.ndecodable, blk_cnt);
@@ -351,11 +367,17 @@ __global__ __launch_bounds__(1024) void vec_count_cols_kernel(DecodeArgs a) {
   if (threadIdx.x == 0 && blk_cnt && a.ndecodable) atomicAdd(a.ndecodable, blk_cnt);
 }
 
+// the 4-rows-per-wave layout of vec_count_rows_kernel (same condition as the kernel's)
+static bool vec_rows_packed(const DecodeArgs& a) {
+  return a.k >= 16 && ((uintptr_t)a.present & 15) == 0 && (a.p_vec_stride & 15) == 0 && (a.p_sq_stride & 15) == 0;
+}
+
 hipError_t launch_vec_count(const DecodeArgs& a, hipStream_t s) {
   const long nv = a.nsq * a.nvec;
   if (nv <= 0) return hipSuccess;
   if (a.p_shard_stride == 1)
-    hipLaunchKernelGGL(vec_count_rows_kernel, dim3((unsigned)((nv + 15) / 16)), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(vec_count_rows_kernel,
+                       dim3((unsigned)(vec_rows_packed(a) ? (nv + 63) / 64 : (nv + 15) / 16)), dim3(1024), 0, s, a);
   else
     hipLaunchKernelGGL(vec_count_cols_kernel, dim3((unsigned)(a.nsq * ((a.nvec + 63) / 64))), dim3(1024), 0, s,
                        a);

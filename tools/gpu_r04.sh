@@ -66,5 +66,9 @@ case "$1" in
     bash tools/gpu_ab.sh --rounds 2 repair128 new= prev=lib:celestia-app_amd/libdagpu_prev.so && \
     bash tools/gpu_ab.sh --rounds 1 repair512 new= prev=lib:celestia-app_amd/libdagpu_prev.so
     ;;
-  *) echo "steps: async dec512 enc-merge forest-multi enc32 dah split-pair dec512-prefetch fill-given gf8-fill-given tables tables-first dec128-loads col-maps"; exit 2;;
+  row-maps)  # round 4: row presence-map counts with 4 rows per wave (16 lanes per row): tests, A/B
+    bash tools/gpu_ab.sh --tests "tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py tests/test_gpu_parity.py tests/test_gpu_gf16.py tests/test_gpu_repair_async.py" --rounds 2 repair128 new= prev=lib:celestia-app_amd/libdagpu_prev.so && \
+    bash tools/gpu_ab.sh --rounds 1 repair512q3 new= prev=lib:celestia-app_amd/libdagpu_prev.so
+    ;;
+  *) echo "steps: async dec512 enc-merge forest-multi enc32 dah split-pair dec512-prefetch fill-given gf8-fill-given tables tables-first dec128-loads col-maps row-maps"; exit 2;;
 esac
