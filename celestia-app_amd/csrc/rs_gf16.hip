@@ -1186,9 +1186,21 @@ __device__ __forceinline__ PTab ptab(int pos) {
   return p;
 }
 
+// tok: a value written by the previous radix-4 unit's last phase.  A unit's
+// table positions pass through an asm that reads a value written just before
+// (tok for its first table, its own first phase's output for the next), so no
+// scalar table load can be hoisted above that point and at most two tables are
+// live: without the tokens every unit's tables of a step were loaded up front
+// and spilled to VGPR lanes (848 v_writelane + 848 v_readlane, 22,320 -> 20,624
+// static VALU; repair k = 512 +1.8 %, profiles/gf16_dec512_tok_r04.log).
 struct W1k {
   uint32_t v[64];
+  uint32_t tok;
 };
+__device__ __forceinline__ int opaque_tok(int x, uint32_t tok) {
+  asm volatile("" : "+s"(x) : "v"(tok));
+  return x;
+}
 
 // ifftDIT2: y ^= x; x ^= y * skew[pos]     fftDIT2: x ^= y * skew[pos]; y ^= x
 __device__ __forceinline__ void ifft2_p(W1k& w, int i, int j, const PTab& t) {
@@ -1201,49 +1213,48 @@ __device__ __forceinline__ void fft2_p(W1k& w, int i, int j, const PTab& t) {
 }
 
 // Radix-4 steps layer by layer: every butterfly of one skew position, then
-// the next position, so that one 16-SGPR table is live at a time (radix-4
-// units with their three tables live across the unit spilled ~850 SGPRs).
+// the next position; each phase's table is loaded during the phase before it.
 // IFFT: (i, i+D) at p01, (i+2D, i+3D) at p23, then (i, i+2D), (i+D, i+3D) at
 // p02; i over N butterflies starting at s0 with stride ST.
 template <int N, int ST, int D>
 __device__ __forceinline__ void ifftp_r4(W1k& w, int s0, int p01, int p02, int p23) {
-  // each phase's table is loaded before the previous phase runs (its scalar
-  // load latency hidden behind that phase's multiplies)
-  const PTab t01 = ptab(p01);
-  const PTab t23 = ptab(p23);
+  const PTab t01 = ptab(opaque_tok(p01, w.tok));
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int u = 0; u < N; u++) ifft2_p(w, s0 + ST * u, s0 + ST * u + D, t01);
-  const PTab t02 = ptab(p02);
+  const PTab t23 = ptab(opaque_tok(p23, w.v[s0 + D]));
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int u = 0; u < N; u++) ifft2_p(w, s0 + ST * u + 2 * D, s0 + ST * u + 3 * D, t23);
+  const PTab t02 = ptab(opaque_tok(p02, w.v[s0 + 3 * D]));
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int u = 0; u < N; u++) {
     ifft2_p(w, s0 + ST * u, s0 + ST * u + 2 * D, t02);
     ifft2_p(w, s0 + ST * u + D, s0 + ST * u + 3 * D, t02);
   }
+  w.tok = w.v[s0 + ST * (N - 1) + D];
   __builtin_amdgcn_sched_barrier(0);
 }
 // FFT: (i, i+2D), (i+D, i+3D) at p02, then (i, i+D) at p01, (i+2D, i+3D) at p23
 template <int N, int ST, int D>
 __device__ __forceinline__ void fftp_r4(W1k& w, int s0, int p01, int p02, int p23) {
-  const PTab t02 = ptab(p02);
-  const PTab t01 = ptab(p01);
+  const PTab t02 = ptab(opaque_tok(p02, w.tok));
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int u = 0; u < N; u++) {
     fft2_p(w, s0 + ST * u, s0 + ST * u + 2 * D, t02);
     fft2_p(w, s0 + ST * u + D, s0 + ST * u + 3 * D, t02);
   }
-  const PTab t23 = ptab(p23);
+  const PTab t01 = ptab(opaque_tok(p01, w.v[s0 + 2 * D]));
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int u = 0; u < N; u++) fft2_p(w, s0 + ST * u, s0 + ST * u + D, t01);
+  const PTab t23 = ptab(opaque_tok(p23, w.v[s0 + D]));
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int u = 0; u < N; u++) fft2_p(w, s0 + ST * u + 2 * D, s0 + ST * u + 3 * D, t23);
+  w.tok = w.v[s0 + ST * (N - 1) + 3 * D];
   __builtin_amdgcn_sched_barrier(0);
 }
 
@@ -1281,6 +1292,7 @@ __device__ __forceinline__ void xposep(W1k& w, uint32_t* lds, int q, int lane) {
     for (int c = 0; c < 16; c++) w.v[(c << 2) | l] = lds[(q * 16 + c) * 64 + lane];
     __syncthreads();
   }
+  w.tok = w.v[63];
 }
 
 // formal derivative in the transposed layout (wave c = element bits 2-5; slot
@@ -1306,6 +1318,7 @@ __device__ __forceinline__ void derivativep(W1k& w, uint32_t* lds, int c, int la
     }
     __syncthreads();
   }
+  w.tok = w.v[63];
 }
 
 // DAGPU_PHASE_PROBE builds (tools/phase_probe.py dec512, never the product
@@ -1383,6 +1396,7 @@ __global__ __launch_bounds__(kDec1k) __attribute__((amdgpu_waves_per_eu(4, 4))) 
     w.v[j] = mulp(odd ? __builtin_amdgcn_perm(mine, other, 0x07060302u) : __builtin_amdgcn_perm(other, mine, 0x05040100u), t);
     __builtin_amdgcn_sched_barrier(0);  // one element's table live at a time
   }
+  w.tok = w.v[63];
   __syncthreads();  // the transpose reuses lds
   DEC_PROBE(2);
   // ---- IFFT (ifftDITDecoder, skew index iend - 1) ----

@@ -70,5 +70,9 @@ case "$1" in
     bash tools/gpu_ab.sh --tests "tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py tests/test_gpu_parity.py tests/test_gpu_gf16.py tests/test_gpu_repair_async.py" --rounds 2 repair128 new= prev=lib:celestia-app_amd/libdagpu_prev.so && \
     bash tools/gpu_ab.sh --rounds 1 repair512q3 new= prev=lib:celestia-app_amd/libdagpu_prev.so
     ;;
-  *) echo "steps: async dec512 enc-merge forest-multi enc32 dah split-pair dec512-prefetch fill-given gf8-fill-given tables tables-first dec128-loads col-maps row-maps"; exit 2;;
+  dec512-tok)  # round 4: k = 512 decoder table loads ordered by tokens (new: each table during the previous phase, no SGPR spills; B: tokens at unit ends, 209 spills): tests, A/B
+    bash tools/gpu_ab.sh --tests "tests/test_gpu_gf16.py tests/test_gpu_wide.py tests/test_gpu_repair_fill.py" --rounds 3 repair512 new= B=lib:celestia-app_amd/libdagpu_varB.so prev=lib:celestia-app_amd/libdagpu_prev.so && \
+    bash tools/gpu_ab.sh --rounds 2 repair512q3 new= B=lib:celestia-app_amd/libdagpu_varB.so prev=lib:celestia-app_amd/libdagpu_prev.so
+    ;;
+  *) echo "steps: async dec512 enc-merge forest-multi enc32 dah split-pair dec512-prefetch fill-given gf8-fill-given tables tables-first dec128-loads col-maps row-maps dec512-tok"; exit 2;;
 esac
