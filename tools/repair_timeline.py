@@ -15,8 +15,10 @@ idx = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 if idx < 1 or idx >= len(fin):
     sys.exit(f"{len(fin)} repairs in the trace")
 seg = rows[fin[idx - 1] + 1:fin[idx] + 1]
-# the repair starts at its first dagpu kernel (the bench's input restore copies come before)
-first = next(i for i, r in enumerate(seg) if "dagpu" in r[2])
+# before the repair: the previous call's restore_presence_kernel, then the bench's
+# input restore (the damaged EDS copied back, the first copyBuffer); the repair
+# starts with the dispatch after that copy
+first = next(i for i, r in enumerate(seg) if "copyBuffer" in r[2]) + 1
 seg = seg[first:]
 t0 = seg[0][0]
 busy = sum(e - s for s, e, _ in seg)
