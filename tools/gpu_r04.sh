@@ -70,7 +70,7 @@ case "$1" in
     bash tools/gpu_ab.sh --tests "tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py tests/test_gpu_parity.py tests/test_gpu_gf16.py tests/test_gpu_repair_async.py" --rounds 2 repair128 new= prev=lib:celestia-app_amd/libdagpu_prev.so && \
     bash tools/gpu_ab.sh --rounds 1 repair512q3 new= prev=lib:celestia-app_amd/libdagpu_prev.so
     ;;
-  dec512-tok)  # round 4: k = 512 decoder table loads ordered by tokens (new: each table during the previous phase, no SGPR spills; B: tokens at unit ends, 209 spills): tests, A/B
+  dec512-tok)  # round 4: k = 512 decoder table loads ordered by tokens (new: each table during the previous phase, no SGPR spills; B: an intermediate build with tokens at unit ends only, 209 spills, not kept in git): tests, A/B
     bash tools/gpu_ab.sh --tests "tests/test_gpu_gf16.py tests/test_gpu_wide.py tests/test_gpu_repair_fill.py" --rounds 3 repair512 new= B=lib:celestia-app_amd/libdagpu_varB.so prev=lib:celestia-app_amd/libdagpu_prev.so && \
     bash tools/gpu_ab.sh --rounds 2 repair512q3 new= B=lib:celestia-app_amd/libdagpu_varB.so prev=lib:celestia-app_amd/libdagpu_prev.so
     ;;
