@@ -228,14 +228,47 @@ def cpu_baseline(seconds: float, threads: int):
 
 
 def load_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (profiles/pmc_*.json, FETCH_SIZE doubled per the gfx950 correction), if present."""
+    """(HBM bytes per launch of `kernel`, the profile's tag) from the committed
+    rocprofv3 PMC summary (profiles/pmc_traffic.json written by
+    tools/pmc_summary.py, FETCH_SIZE doubled per the gfx950 correction), or
+    (None, None).  The tag names the round/build the counters came from."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
-        d = json.load(open(path))
-        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+        e = json.load(open(path)).get(kernel, {})
+        return e.get("hbm_bytes_per_launch"), e.get("tag")
+    except Exception:
+        return None, None
+
+
+def load_stress_pmc(kernel: str):
+    """Committed counters of a GF(2^16) stress kernel (profiles/pmc_stress.json,
+    tools/pmc_stress.py over a tools/gpu_pmc_gf16.sh run): VALU wave-instructions
+    per clock per CU and the fraction of wave cycles parked on s_waitcnt, with
+    the profile's tag; None if absent."""
+    path = os.path.join(ROOT, "profiles", "pmc_stress.json")
+    try:
+        e = json.load(open(path))[kernel]
+        return {"valu_per_clk_per_cu": e["valu_per_clk_per_cu"], "wait_inst_frac": e.get("wait_inst_frac"),
+                "counters_tag": e.get("tag"), "counters_source": "profiles/pmc_stress.json (rocprofv3 --pmc, "
+                                                                   "separate passes)"}
     except Exception:
         return None
+
+
+def stress_roofline(kernel: str, alg_bytes: float, ms: float, launches: int, pmc_name: str, work: str):
+    """Roofline entry of a stress line's dominant kernel: algorithmic bytes per
+    launch over its average launch time (HIP events of the library's profiled
+    pass) against the HBM peak, plus the committed counters of that kernel."""
+    if not ms or not launches:
+        return None
+    avg = ms / launches
+    ach = alg_bytes / launches / (avg * 1e-3) / 1e9
+    r = {"kernel": kernel, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": ach / HBM_PEAK_GBS, "avg_launch_ms": avg, "launches": launches, "work": work}
+    pmc = load_stress_pmc(pmc_name)
+    if pmc:
+        r.update(pmc)
+    return r
 
 
 def valu_issue(k: int, B: int, ms_step: float, leaf_ms: float):
@@ -408,7 +441,10 @@ def main():
                 "unit": "Tint32op/s", "frac": ach / VALU_PEAK_TOPS,
                 "work": f"{comp} SHA-256 compressions x {OPS_PER_COMPRESSION} int32 ops",
                 "measured_ceiling": VALU_MEASURED_TOPS, "frac_of_measured": ach / VALU_MEASURED_TOPS}
-    roof["traffic"] = load_traffic(dom)
+    roof["traffic"], roof["traffic_tag"] = load_traffic(
+        {"rs_row": "rs_encode_sliced2", "rs_col": "rs_encode_sliced2"}.get(dom, dom))
+    roof["traffic_source"] = ("profiles/pmc_traffic.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of the "
+                              "headline step, per launch, tagged with the build they came from")
     roof["avg_launch_ms"] = per[dom]
 
     out = {
@@ -835,6 +871,24 @@ def bench_split(dist, rank, world, local, ctx, k, steps, warmup):
     torch.cuda.synchronize()
     barrier(dist)
     el = max_over_ranks(dist, time.perf_counter() - t0, local)
+    # one profiled pass (HIP events around each launch of this rank): the RS
+    # passes' roofline; the timed steps above run unprofiled
+    L = ctx._L
+    L.dagpu_profile_enable(ctx.handle, 1)
+    L.dagpu_profile_read(ctx.handle, None, None, 1)
+    split.extend_split_distributed(dist, part, mine)
+    torch.cuda.synchronize()
+    L.dagpu_profile_enable(ctx.handle, 0)
+    from celestia_da import _abi
+    tot = np.zeros(len(_abi.PROFILE_KERNELS), np.float64)
+    cnt = np.zeros(len(_abi.PROFILE_KERNELS), np.uint64)
+    L.dagpu_profile_read(ctx.handle, _abi.addr(tot), _abi.addr(cnt), 1)
+    prof = {n: float(tot[i]) for i, n in enumerate(_abi.PROFILE_KERNELS) if cnt[i]}
+    # this rank's column pass: 2k/P column vectors, each k shards read + k written
+    enc = {512: "leo16_encode_reg32_kernel<512, false>", 256: "leo16_encode_reg_kernel<256, false>"}.get(k)
+    roof = stress_roofline("rs_col (GF(2^16) column encode)", (2 * k // world) * 2 * k * SHARE,
+                           prof.get("rs_col"), int(cnt[1]), enc or f"leo16 encode k={k}",
+                           f"{2 * k // world} column vectors x (k read + k written) x 512 B") if cnt[1] else None
     ok = True
     if rank == 0:  # same square through the ordinary single-GPU pipeline
         ds = DeviceSquares(k, 1, device=local, ctx=ctx)
@@ -851,6 +905,7 @@ def bench_split(dist, rank, world, local, ctx, k, steps, warmup):
     _fail(dist, not ok, local, f"split square k={k}: DAH differs from the single-GPU pipeline")
     return {"k": k, "parts": world, "squares_per_s": steps / el, "ms_per_square": el / steps * 1e3,
             "rs_gbs": rs_bytes(k) * steps / el / 1e9, "dah_matches_single_gpu": ok,
+            "kernel_ms_profiled_pass": prof, "roofline": roof,
             "collective": f"all_to_all_single over {world} ranks, {dist.get_backend() if dist else 'none'}"}
 
 
@@ -1042,11 +1097,42 @@ def run_repair(ctx, k, B, steps, warmup, distinct=None, pattern="subgrid", slice
         print(f"FATAL: repair k={k} did not restore the extended square", file=sys.stderr)
         raise SystemExit(3)
     ms = sum(a.elapsed_time(b) for a, b in ev) / steps
+    # one more step, profiled (HIP events around every decode / fill launch),
+    # for the decoder's roofline; checked like the timed ones
+    from celestia_da import _abi
+    L = ctx._L
+    ds.eds.copy_(damaged)
+    present.copy_(pres_t)
+    torch.cuda.synchronize()
+    L.dagpu_profile_enable(ctx.handle, 1)
+    L.dagpu_profile_read(ctx.handle, None, None, 1)
+    repair_step()
+    torch.cuda.synchronize()
+    L.dagpu_profile_enable(ctx.handle, 0)
+    tot = np.zeros(len(_abi.PROFILE_KERNELS), np.float64)
+    cnt = np.zeros(len(_abi.PROFILE_KERNELS), np.uint64)
+    L.dagpu_profile_read(ctx.handle, _abi.addr(tot), _abi.addr(cnt), 1)
+    sched = ctx.repair_stats()
+    if not (torch.equal(ds.eds, ref) and int(status.abs().sum()) == 0):
+        print(f"FATAL: profiled repair k={k} did not restore the extended square", file=sys.stderr)
+        raise SystemExit(3)
+    idec = _abi.PROFILE_KERNELS.index("decode")
+    ifil = _abi.PROFILE_KERNELS.index("repair_fill")
+    prof = {"decode_ms": float(tot[idec]), "decode_launches": int(cnt[idec]),
+            "fill_ms": float(tot[ifil]), "fill_launches": int(cnt[ifil]), "schedule": sched}
+    # a decoded vector reads its k given shards and writes its k missing ones
+    dec_name = {128: "leo8_decode128_sliced_kernel", 256: "leo16_decode_reg_kernel",
+                512: "leo16_decode_reg1k_kernel"}.get(k, f"decoder k={k}")
+    roof = stress_roofline(f"decode ({dec_name})", sched["decodes"] * 2 * k * SHARE, prof["decode_ms"],
+                           prof["decode_launches"], dec_name,
+                           f"{sched['decodes']} decoded vectors x (k read + k written) x 512 B") \
+        if sched["decodes"] and prof["decode_launches"] else None
     del ds, ref, damaged, ws
     torch.cuda.empty_cache()
     return {"k": k, "squares": B, "pattern": pattern, "slices": slices, "squares_per_s": B / (ms * 1e-3),
             "ms_per_step": ms,
-            "steps": steps, "bit_exact": ok, "decode_gbs": rs_bytes(k) * B / (ms * 1e-3) / 1e9}
+            "steps": steps, "bit_exact": ok, "decode_gbs": rs_bytes(k) * B / (ms * 1e-3) / 1e9,
+            "profiled_pass": prof, "roofline": roof}
 
 
 def bench_repair(args):

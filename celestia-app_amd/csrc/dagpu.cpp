@@ -1149,7 +1149,7 @@ hipError_t read_small(void* dst, const void* src, size_t bytes, Mailbox& mb, hip
 // a stream that is itself waiting for the worker).
 int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t* d_present,
                   const uint8_t* d_rr, const uint8_t* d_cr, int32_t* d_status, int32_t* d_byz, void* d_ws,
-                  hipStream_t s, Mailbox* mb_in = nullptr) {
+                  hipStream_t s, Mailbox* mb_in = nullptr, int64_t* stats_out = nullptr) {
   const long w = 2L * k;
   RepairWs r = carve_repair(k, n, d_ws);
   HIP_TRY(ctx, hipMemcpyAsync(r.p0, d_present, n * w * w, hipMemcpyDeviceToDevice, s));
@@ -1228,13 +1228,16 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
       HIP_TRY(ctx, launch_vec_count(dc, s));
       int32_t cnt[11] = {};
       HIP_TRY(ctx, read_small(cnt, r.counters, sizeof cnt, mb, s));
-      {  // schedule totals so far (diagnostics): plans of the earlier rounds are complete
-        std::lock_guard<std::mutex> g(ctx->prof_mu);
-        ctx->rep_stats[0] = rounds_run;
-        ctx->rep_stats[1] = cnt[8];
-        ctx->rep_stats[2] = cnt[9];
-        ctx->rep_stats[3] = cnt[10];
-        ctx->rep_stats[4] = deferred_run + cnt[2];
+      {  // schedule totals so far (diagnostics): plans of the earlier rounds are complete;
+         // a started Repair writes its slot's copy (published at its join)
+        std::unique_lock<std::mutex> g(ctx->prof_mu, std::defer_lock);
+        if (!stats_out) g.lock();
+        int64_t* st = stats_out ? stats_out : ctx->rep_stats;
+        st[0] = rounds_run;
+        st[1] = cnt[8];
+        st[2] = cnt[9];
+        st[3] = cnt[10];
+        st[4] = deferred_run + cnt[2];
       }
       if (pass == 0 && round == 0 && cnt[5] > 0) {
         const int prc = prerepair();
@@ -1449,25 +1452,45 @@ int dagpu_repair_start(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uin
   HIP_TRY(ctx, async_init_slot(sl));
   HIP_TRY(ctx, launch_rs_prepare((int)k));  // first-use table uploads here, not on the worker
   HIP_TRY(ctx, hipEventRecord(sl.fork, s));
-  if (++ctx->async_gen == 0) ++ctx->async_gen;
-  sl.busy = true;
-  sl.gen = ctx->async_gen;
   sl.rc = DAGPU_OK;
-  auto mb = std::make_shared<Mailbox>(ctx);
+  sl.err.clear();
+  for (auto& x : sl.stats) x = 0;
   hipStream_t ws = sl.stream;
   hipEvent_t fork = sl.fork, fin = sl.finished;
-  int* rc_out = &sl.rc;
+  dagpu_ctx::AsyncSlot* slp = &sl;
   const int dev = ctx->device;
-  sl.worker = std::thread([=]() {
-    (void)hipSetDevice(dev);
-    int r = hipStreamWaitEvent(ws, fork, 0) == hipSuccess ? DAGPU_OK : DAGPU_ERR_DEVICE;
-    if (r == DAGPU_OK && n)
-      r = repair_device(ctx, k, n, d_eds, d_present, d_row_roots, d_col_roots, d_status, nullptr, d_workspace, ws,
-                        mb.get());
-    if (r != DAGPU_OK) (void)hipMemsetD32Async((hipDeviceptr_t)d_status, (int)DAGPU_ERR_DEVICE, n, ws);
-    (void)hipEventRecord(fin, ws);
-    *rc_out = r;
-  });
+  // std::thread / make_shared may throw (no threads or memory left): nothing
+  // may escape an extern "C" entry point, and the slot stays free
+  try {
+    auto mb = std::make_shared<Mailbox>(ctx);
+    sl.worker = std::thread([=]() {
+      on_repair_worker() = true;
+      (void)hipSetDevice(dev);
+      int r = hipStreamWaitEvent(ws, fork, 0) == hipSuccess ? DAGPU_OK : DAGPU_ERR_DEVICE;
+      // DAGPU_TEST_WORKER_FAIL=1 (tests/test_gpu_repair_async.py): the worker
+      // fails before its first kernel, so the join's error path is exercised
+      const char* inj = getenv("DAGPU_TEST_WORKER_FAIL");
+      if (r == DAGPU_OK && inj && inj[0] == '1') r = set_err(ctx, DAGPU_ERR_DEVICE, "injected worker failure");
+      if (r == DAGPU_OK && n)
+        r = repair_device(ctx, k, n, d_eds, d_present, d_row_roots, d_col_roots, d_status, nullptr, d_workspace, ws,
+                          mb.get(), slp->stats);
+      if (r != DAGPU_OK) {
+        // the worker's own message (set_err wrote it to this thread's state);
+        // the join re-raises it on the caller's thread
+        const ThreadErr& te = thread_err();
+        slp->err = te.own && !te.msg.empty() ? te.msg : "started repair failed on the device";
+        (void)hipMemsetD32Async((hipDeviceptr_t)d_status, (int)DAGPU_ERR_DEVICE, n, ws);
+      }
+      (void)hipEventRecord(fin, ws);
+      slp->rc = r;
+    });
+  } catch (...) {
+    return set_err(ctx, DAGPU_ERR_DEVICE, "could not start the repair worker thread");
+  }
+  if (++ctx->async_gen == 0) ++ctx->async_gen;
+  sl.busy = true;
+  sl.joining = false;
+  sl.gen = ctx->async_gen;
   *handle = ((uint64_t)sl.gen << 8) | (uint64_t)si;
   return DAGPU_OK;
 }
@@ -1475,15 +1498,29 @@ int dagpu_repair_start(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uin
 int dagpu_repair_join(dagpu_ctx* ctx, uint64_t handle, void* stream) {
   if (!ctx) return DAGPU_ERR_ARG;
   const int si = (int)(handle & 0xFF);
+  std::thread worker;
+  {  // claim the slot under the lock, wait for its worker without it
+    std::lock_guard<std::mutex> g(ctx->async_mu);
+    if (si >= dagpu_ctx::kAsyncSlots || !ctx->async_slot[si].busy || ctx->async_slot[si].joining ||
+        ctx->async_slot[si].gen != (uint32_t)(handle >> 8))
+      return set_err(ctx, DAGPU_ERR_ARG, "unknown or already joined repair handle");
+    ctx->async_slot[si].joining = true;
+    worker = std::move(ctx->async_slot[si].worker);
+  }
+  if (worker.joinable()) worker.join();  // its last command is queued
   std::lock_guard<std::mutex> g(ctx->async_mu);
-  if (si >= dagpu_ctx::kAsyncSlots || !ctx->async_slot[si].busy ||
-      ctx->async_slot[si].gen != (uint32_t)(handle >> 8))
-    return set_err(ctx, DAGPU_ERR_ARG, "unknown or already joined repair handle");
   dagpu_ctx::AsyncSlot& sl = ctx->async_slot[si];
-  if (sl.worker.joinable()) sl.worker.join();  // its last command is queued
+  const int rc = sl.rc;
+  {
+    std::lock_guard<std::mutex> gp(ctx->prof_mu);
+    for (int i = 0; i < DAGPU_REPAIR_STATS; i++) ctx->rep_stats[i] = sl.stats[i];
+  }
+  const hipError_t e = hipStreamWaitEvent((hipStream_t)stream, sl.finished, 0);
   sl.busy = false;
-  HIP_TRY(ctx, hipStreamWaitEvent((hipStream_t)stream, sl.finished, 0));
-  return sl.rc;
+  sl.joining = false;
+  if (e != hipSuccess) return hip_fail(ctx, e, "hipStreamWaitEvent(stream, finished)");
+  if (rc != DAGPU_OK) return set_err(ctx, rc, sl.err);
+  return DAGPU_OK;
 }
 
 // Start + join on the same stream: returns once every kernel of the repair is

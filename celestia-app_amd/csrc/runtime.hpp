@@ -117,7 +117,8 @@ struct dagpu_ctx {
   std::vector<ProfRec> pending;
   std::vector<hipEvent_t> pool;
   double prof_ms[DAGPU_PROFILE_KERNELS] = {};
-  // the last Repair call's schedule (dagpu_repair_stats), under prof_mu
+  // the last Repair call's schedule (dagpu_repair_stats), under prof_mu; a
+  // started Repair keeps its own in its slot and publishes them at its join
   int64_t rep_stats[DAGPU_REPAIR_STATS] = {};
   uint64_t prof_n[DAGPU_PROFILE_KERNELS] = {};
   // Started Repairs (dagpu_repair_start / dagpu_repair_join): each runs its
@@ -125,10 +126,17 @@ struct dagpu_ctx {
   // from the caller's stream; the join waits for the worker (all commands
   // queued) and makes a stream wait for the slot's `finished` event.
   static constexpr int kAsyncSlots = 64;
+  // async_mu guards the slot table only: a join marks its slot `joining` under
+  // the lock and waits for the worker without it, so starts and joins from
+  // other host threads never queue behind one repair's crossword.
   struct AsyncSlot {
     bool busy = false;
+    bool joining = false;
     uint32_t gen = 0;
+    // written by the worker, read by the join after std::thread::join
     int rc = 0;
+    std::string err;  // the worker's failure message (set_err on its own thread)
+    int64_t stats[DAGPU_REPAIR_STATS] = {};
     hipStream_t stream = nullptr;
     hipEvent_t fork = nullptr, finished = nullptr;
     std::thread worker;
@@ -194,6 +202,14 @@ inline uint64_t next_ctx_gen() {
   return ++g;
 }
 
+// True on a started Repair's worker thread: it runs without the caller's
+// ctx->mu, so it records no stage marks or profile brackets (their event
+// state belongs to host-path calls under ctx->mu).
+inline bool& on_repair_worker() {
+  static thread_local bool w = false;
+  return w;
+}
+
 inline hipEvent_t pool_get(dagpu_ctx* c) {
   if (!c->pool.empty()) {
     hipEvent_t e = c->pool.back();
@@ -207,7 +223,7 @@ inline hipEvent_t pool_get(dagpu_ctx* c) {
 
 // Stage mark of a host-path call (see DAGPU_STAGE_* in dagpu.h).
 inline void stage_mark(dagpu_ctx* c, int i, hipStream_t s) {
-  if (!c->stages_on || !c->stage_ev[i]) return;
+  if (!c->stages_on || !c->stage_ev[i] || on_repair_worker()) return;
   if (hipEventRecord(c->stage_ev[i], s) == hipSuccess) c->stage_mask |= 1u << i;
 }
 
@@ -218,7 +234,7 @@ struct ProfScope {
   hipStream_t s;
   hipEvent_t a = nullptr, b = nullptr;
   ProfScope(dagpu_ctx* c_, int id_, hipStream_t s_) : c(c_), id(id_), s(s_) {
-    if (!c->prof) return;
+    if (!c->prof || on_repair_worker()) return;
     std::lock_guard<std::mutex> g(c->prof_mu);
     a = pool_get(c);
     b = pool_get(c);

@@ -208,7 +208,11 @@ int dagpu_repair_batch_device_ex(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* 
  * repair's call status (per-square results in d_status).  Repairs started back
  * to back (slices of a batch, squares of several blocks) run side by side; a
  * context serves 64 started, not yet joined repairs.  The buffers must stay
- * valid until the joined stream has passed the repair. */
+ * valid until the joined stream has passed the repair.  Joins from several
+ * host threads wait side by side (the slot table is locked only to claim a
+ * slot); a failed repair's message is re-raised on the joining thread
+ * (dagpu_last_error), and a worker that cannot be started returns
+ * DAGPU_ERR_DEVICE with no slot taken. */
 int dagpu_repair_start(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t* d_present,
                        const uint8_t* d_row_roots, const uint8_t* d_col_roots, int32_t* d_status,
                        void* d_workspace, void* stream, uint64_t* handle);
@@ -242,7 +246,9 @@ int dagpu_profile_read(dagpu_ctx* ctx, double* total_ms, uint64_t* launches, int
 #define DAGPU_STAGE_EDS_BOTTOM 9 /* [Q2|Q3] halves downloaded (copy stream) */
 int dagpu_profile_stages(dagpu_ctx* ctx, float* ms);
 
-/* Schedule of the last Repair on this context (diagnostics): out[0] crossword
+/* Schedule of the last Repair on this context (diagnostics; a started repair's
+ * schedule becomes "the last" at its join, so started repairs in flight never
+ * mix their counters): out[0] crossword
  * rounds that rebuilt something, out[1] vectors re-encoded from a complete data
  * half (fill), out[2] vectors rebuilt from a complete parity half (reverse
  * fill), out[3] vectors planned for the decoder, out[4] decodes deferred to the

@@ -112,3 +112,21 @@ def test_codec_decode_without_any_shard_is_too_few():
     # call is reached: the shard size cannot even be known)
     with pytest.raises(da.ErrTooFewShards):
         da.LeoRSCodec().decode([None] * 8)
+
+
+def test_no_device_wait_on_later_queued_signals():
+    # Invariant (DESIGN.md §4 "Started Repairs"): nothing on the device waits
+    # for work queued later.  A stream wait on a signal word that a later
+    # command releases hung once when two streams shared a hardware queue
+    # (GPU_MAX_HW_QUEUES = 4); the library may only wait on events that are
+    # already recorded.  Comments may name the primitive, code may not call it.
+    csrc = os.path.join(ROOT, "celestia-app_amd", "csrc")
+    bad = []
+    for name in sorted(os.listdir(csrc)):
+        if not name.endswith((".cpp", ".hip", ".hpp")):
+            continue
+        for no, line in enumerate(open(os.path.join(csrc, name)), 1):
+            code = line.split("//", 1)[0]
+            if re.search(r"hipStreamWait(Value|Write)|hipStreamWriteValue|hipStreamBatchMemOp", code):
+                bad.append(f"{name}:{no}: {line.strip()}")
+    assert not bad, bad

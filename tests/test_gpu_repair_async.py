@@ -4,8 +4,6 @@ stream of its own; the join makes a stream wait for the repair.  Outputs
 (status, every EDS byte, the presence map) must equal dagpu_repair_batch_device's
 for the same inputs; slices started back to back run side by side; handles
 are checked; a context closed with repairs in flight stays correct."""
-import time
-
 import numpy as np
 import pytest
 import torch
@@ -73,20 +71,72 @@ def test_started_equals_batch_call(ctx, k, n, kind):
 
 
 def test_start_returns_at_once_and_slices_run_side_by_side(ctx):
+    # Structural, not wall-clock: the caller's stream is held by a GPU sleep
+    # queued before the starts, so no repair kernel can have run when the three
+    # starts return; the sleep's completion event must still be pending then
+    # (a start that waited for its repair could only return after it).
     k, n = 128, 64
     ds, pres_t, ref, damaged = _setup(ctx, k, n, 4242)
     present, status = _inputs(ds, pres_t, damaged)
     cut = [0, 16, 40, 64]  # uneven slices
     wss = [ds.repair_workspace(cut[j + 1] - cut[j]) for j in range(3)]
-    t0 = time.perf_counter()
+    s = torch.cuda.current_stream()
+    torch.cuda._sleep(int(2e8))
+    held = torch.cuda.Event()
+    held.record(s)
     hs = [ds.repair_start(present, status, wss[j], first=cut[j], count=cut[j + 1] - cut[j]) for j in range(3)]
-    t_start = time.perf_counter() - t0
+    assert not held.query(), "a start waited for device work queued before it"
     for h in hs:
         ds.repair_join(h)
     torch.cuda.synchronize()
-    t_all = time.perf_counter() - t0
     assert torch.equal(ds.eds, ref) and (status.cpu().numpy() == 0).all() and bool(present.all())
-    assert t_start < 0.5 * t_all, (t_start, t_all)
+
+
+def test_worker_failure_reaches_the_joining_thread(ctx, monkeypatch):
+    # the worker's message is re-raised on the caller's thread at the join,
+    # and the slot is free again afterwards
+    k, n = 8, 2
+    ds, pres_t, ref, damaged = _setup(ctx, k, n, 32)
+    present, status = _inputs(ds, pres_t, damaged)
+    monkeypatch.setenv("DAGPU_TEST_WORKER_FAIL", "1")
+    h = ds.repair_start(present, status, ds.repair_workspace())
+    with pytest.raises(da.DAError, match="injected worker failure"):
+        ds.repair_join(h)
+    torch.cuda.synchronize()
+    assert (status.cpu().numpy() == _abi.ERR_DEVICE).all()
+    monkeypatch.delenv("DAGPU_TEST_WORKER_FAIL")
+    present, status = _inputs(ds, pres_t, damaged)
+    h = ds.repair_start(present, status, ds.repair_workspace())
+    ds.repair_join(h)
+    torch.cuda.synchronize()
+    assert torch.equal(ds.eds, ref) and (status.cpu().numpy() == 0).all()
+
+
+def test_joins_from_threads_run_side_by_side(ctx):
+    # two host threads each start and join their own repair on one context;
+    # a join holds the slot table only to claim its slot (advisor r04)
+    import threading
+
+    k, n = 128, 16
+    ds, pres_t, ref, damaged = _setup(ctx, k, n, 515)
+    present, status = _inputs(ds, pres_t, damaged)
+    errs = []
+
+    def run(j):
+        try:
+            h = ds.repair_start(present, status, ds.repair_workspace(8), first=8 * j, count=8)
+            ds.repair_join(h)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ts = [threading.Thread(target=run, args=(j,)) for j in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    torch.cuda.synchronize()
+    assert not errs, errs
+    assert torch.equal(ds.eds, ref) and (status.cpu().numpy() == 0).all()
 
 
 def test_handles_are_checked(ctx):

@@ -186,3 +186,116 @@ def _axis_root(vec: np.ndarray, idx: int, k: int) -> bytes:
         ns = share[:29] if (j < k and idx < k) else b"\xff" * 29
         leaves.append(oracle.nmt_leaf(ns, share))
     return oracle.nmt_root(leaves)
+
+
+def test_dah_chunked_kernel_k1024(ctx, monkeypatch):
+    """The one-workgroup DAH kernel's chunked path (C = 2048 items per chunk
+    < n = 4k = 4096, then the chunk roots) -- taken when the two-stage DAH is
+    off (DAGPU_DAH_SPLIT=0) -- equals the two-stage DAH and the oracle."""
+    k = 1024
+    ds = DeviceSquares(k, 1, ctx=ctx, in_place=True)
+    ds.load_ods(synth.blob_squares(k, 4096, 0, 1))
+    ds.extend()
+    torch.cuda.synchronize()
+    split = bytes(ds.dah[0].cpu().numpy())
+    rr, cr = ds.row_roots[0].cpu().numpy(), ds.col_roots[0].cpu().numpy()
+    monkeypatch.setenv("DAGPU_DAH_SPLIT", "0")
+    ds.dah.zero_()
+    ds.extend()
+    torch.cuda.synchronize()
+    assert int(ds.status[0]) == 0
+    assert bytes(ds.dah[0].cpu().numpy()) == split == oracle.dah_hash(rr, cr)
+    del ds
+    torch.cuda.empty_cache()
+
+
+def _wide_square_checks(ds, ods, k, rng, n_rows=2, n_cols=2):
+    """Sampled rows and columns of every quadrant against the oracle's encoder,
+    sampled roots against the oracle's wrapper tree, the DAH from all roots."""
+    w = 2 * k
+    e = ds.eds.view(w, w, 512)
+    q0 = ods.reshape(k, k, 512)
+    for r in rng.choice(k, n_rows, replace=False):  # Q0 placed, Q1 rows = Encode(Q0 rows)
+        assert (e[r, :k].cpu().numpy() == q0[r]).all(), r
+        assert (e[r, k:].cpu().numpy() == oracle.encode(q0[r])).all(), r
+    for c in list(rng.choice(k, n_cols // 2, replace=False)) + list(k + rng.choice(k, n_cols - n_cols // 2, replace=False)):
+        col = e[:, c].cpu().numpy()  # Q2 / Q3 columns = Encode([Q0|Q1] columns)
+        assert (col[k:] == oracle.encode(np.ascontiguousarray(col[:k]))).all(), c
+    rr = ds.row_roots[0].cpu().numpy()
+    cr = ds.col_roots[0].cpu().numpy()
+    assert bytes(ds.dah[0].cpu().numpy()) == oracle.dah_hash(rr, cr)
+    for ax, idx in ((0, 1), (0, w - 2), (1, 0), (1, w - 1)):
+        vec = (e[idx] if ax == 0 else e[:, idx]).cpu().numpy()
+        assert (rr if ax == 0 else cr)[idx].tobytes() == _axis_root(vec, idx, k), (ax, idx)
+
+
+def _max_erasure_repair(ctx, ds, k, rng, ref=None):
+    """Keep a random k x k sub-grid (the maximal recoverable erasure), zero the
+    rest in place, repair on the device; every root is re-verified by the
+    repair itself (status 0), and with `ref` every EDS byte is compared."""
+    w = 2 * k
+    keep_r = torch.from_numpy(rng.choice(w, k, replace=False)).cuda()
+    keep_c = torch.from_numpy(rng.choice(w, k, replace=False)).cuda()
+    present = torch.zeros((w, w), dtype=torch.uint8, device="cuda")
+    present[keep_r[:, None], keep_c[None, :]] = 1
+    e = ds.eds.view(w, w, 512)
+    for r0 in range(0, w, 1024):  # in place, a row slab at a time
+        e[r0:r0 + 1024].mul_(present[r0:r0 + 1024, :, None])
+    status = torch.full((1,), 99, dtype=torch.int32, device="cuda")
+    ws = ds.repair_workspace()
+    ds.repair(present.view(1, -1), status, ws)
+    torch.cuda.synchronize()
+    assert int(status[0]) == 0, int(status[0])
+    assert bool(present.all())
+    if ref is not None:
+        assert torch.equal(ds.eds, ref)
+    del ws
+
+
+def test_wide_k4096_square(ctx):
+    """k = 4096 (32 GiB EDS, device-resident, ODS in place): sampled vectors of
+    every quadrant and sampled roots against the oracle, the DAH from all 16,384
+    roots, then a maximal-erasure Repair (a random 4096 x 4096 sub-grid kept)
+    that restores every EDS byte and re-verifies every root."""
+    k = 4096
+    ds = DeviceSquares(k, 1, ctx=ctx, in_place=True)
+    ods = synth.blob_squares(k, 4096, 0, 1)
+    ds.load_ods(ods)
+    ds.extend()
+    torch.cuda.synchronize()
+    assert int(ds.status[0]) == 0
+    rng = np.random.default_rng(4096)
+    _wide_square_checks(ds, ods, k, rng)
+    ref = ds.eds.clone()
+    ds.workspace = None  # the repair brings its own
+    torch.cuda.empty_cache()
+    _max_erasure_repair(ctx, ds, k, rng, ref)
+    del ds, ref
+    torch.cuda.empty_cache()
+
+
+def test_wide_k8192_square(ctx):
+    """k = 8192, the widest square one MI355X serves (128 GiB EDS): sampled
+    vectors of every quadrant and sampled roots against the oracle, the DAH
+    from all 32,768 roots; then a maximal-erasure Repair in place whose status
+    proves every root re-verified, and sampled rows against the ODS / oracle."""
+    k = 8192
+    w = 2 * k
+    ds = DeviceSquares(k, 1, ctx=ctx, in_place=True)
+    ods = synth.blob_squares(k, 8192, 0, 1)
+    ds.load_ods(ods)
+    ds.extend()
+    torch.cuda.synchronize()
+    assert int(ds.status[0]) == 0
+    rng = np.random.default_rng(8192)
+    _wide_square_checks(ds, ods, k, rng, n_rows=1, n_cols=2)
+    ds.workspace = None
+    torch.cuda.empty_cache()
+    _max_erasure_repair(ctx, ds, k, rng)
+    e = ds.eds.view(w, w, 512)
+    q0 = ods.reshape(k, k, 512)
+    for r in rng.choice(k, 2, replace=False):
+        assert (e[r, :k].cpu().numpy() == q0[r]).all(), r
+        assert (e[r, k:].cpu().numpy() == oracle.encode(q0[r])).all(), r
+    del ds
+    torch.cuda.empty_cache()

@@ -21,36 +21,5 @@ for wl in "$@"; do
   timeout -s KILL 150 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d $OUT/$wl/grbm -o run -- python3 $B > $OUT/$wl.grbm.log 2>&1 || { echo "$wl pmc grbm failed"; exit 1; }
   echo "$wl done"
 done
-python3 - "$@" > $OUT/summary.txt <<'PY'
-import csv, glob, collections, re, sys
-def kname(n):
-    return n.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
-for wl in sys.argv[1:]:
-    print(f"== {wl}")
-    s = glob.glob(f"gpurun_out/p16/{wl}/trace/**/*kernel_stats.csv", recursive=True)
-    if s:
-        rows = list(csv.DictReader(open(s[0])))
-        for r in rows[:14]:
-            print(f"  stats {kname(r['Name'])[:70]:70s} calls {r['Calls']:>5s} avg_ms {float(r['AverageNs'])/1e6:.4f} pct {float(r['Percentage']):.1f}")
-    agg = collections.defaultdict(lambda: collections.defaultdict(list))
-    for p in glob.glob(f"gpurun_out/p16/{wl}/*/**/*counter_collection.csv", recursive=True):
-        for r in csv.DictReader(open(p)):
-            n = kname(r["Kernel_Name"])
-            if "leo16" in n or "errloc" in n or "decode128" in n:
-                agg[n][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    for n, d in sorted(agg.items()):
-        a = {c: sum(v) / len(v) for c, v in d.items()}
-        cyc = a.get("GRBM_GUI_ACTIVE", 0) / 8
-        valu = a.get("SQ_INSTS_VALU", 0)
-        waves = a.get("SQ_WAVES", 0)
-        out = {c: round(v) for c, v in a.items()}
-        if cyc and valu:
-            out["valu_per_clk_per_cu"] = round(valu / cyc / 256, 3)
-        if waves:
-            out["valu_per_wave"] = round(valu / waves)
-        if a.get("SQ_WAVE_CYCLES"):
-            out["wait_inst_frac"] = round(a.get("SQ_WAIT_INST_ANY", 0) / a["SQ_WAVE_CYCLES"], 3)
-            out["wait_any_frac"] = round(a.get("SQ_WAIT_ANY", 0) / a["SQ_WAVE_CYCLES"], 3)
-        print(f"  pmc {n[:80]} {out}")
-PY
+python3 tools/pmc_stress.py "$@" > $OUT/summary.txt
 cat $OUT/summary.txt
