@@ -487,9 +487,53 @@ __device__ __forceinline__ void mul16_add_t(uint32_t& xlo, uint32_t& xhi, uint32
   xlo = xor3(xor3(xor3(xlo, pl[0], pl[1]), xor3(pl[2], pl[3], pl[4]), pl[5]), pl[6], pl[7]);
   xhi = xor3(xor3(xor3(xhi, ph[0], ph[1]), xor3(ph[2], ph[3], ph[4]), ph[5]), ph[6], ph[7]);
 }
+
+// 3/3/2 split (round 5): each byte of y in groups of 3, 3 and 2 bits, so a
+// symbol takes 6 lookups per output byte instead of 8.  A 3-bit group indexes
+// an 8-byte pool, i.e. two table dwords (perm(t[2i+1], t[2i], sel): selector
+// bytes 0-3 pick from t[2i], 4-7 from t[2i+1]); the 2-bit group a 4-byte one
+// (the same SGPR twice, no VGPR copy).  Per 4 symbols: 12 v_perm, 6 selectors
+// from 4 shift / and pairs (2 plain ands), 6 xor3 = 28 ops (the 2-bit split:
+// 16 v_perm, 14 selector ops, 8 xor3 = 38) plus, per table and phase, a VGPR
+// copy of one dword of each of the 8 two-dword pools (a VOP3 reads one SGPR).
+// Table (20 dwords per skew position, kTab16x):
+//   [0,1] group 0 (y bits 0-2) -> product lo byte   [2,3] -> hi byte
+//   [4,5] group 1 (bits 3-5) lo / [6,7] hi           [8] group 2 (bits 6-7) lo, [9] hi
+//   [10..13] group 3 (bits 8-10), [14..17] group 4 (bits 11-13), [18, 19] group 5 (bits 14-15)
+// entry e of a group at byte e of its pool: product (e << shift) * c.
+constexpr int kTab16x = 20;
+__constant__ uint32_t g_ptab16x[kTabPos * kTab16x];
+__constant__ uint32_t g_ptab16x_merged[2 * kTab16x];
+
+__device__ __forceinline__ void mul16x_add_t(uint32_t& xlo, uint32_t& xhi, uint32_t ylo, uint32_t yhi,
+                                             const uint32_t* t) {
+  const uint32_t s0 = ylo & 0x07070707u, s1 = (ylo >> 3) & 0x07070707u, s2 = (ylo >> 6) & 0x03030303u;
+  const uint32_t s3 = yhi & 0x07070707u, s4 = (yhi >> 3) & 0x07070707u, s5 = (yhi >> 6) & 0x03030303u;
+  using B = uint32_t;
+  const B l0 = __builtin_amdgcn_perm(t[1], t[0], s0), h0 = __builtin_amdgcn_perm(t[3], t[2], s0);
+  const B l1 = __builtin_amdgcn_perm(t[5], t[4], s1), h1 = __builtin_amdgcn_perm(t[7], t[6], s1);
+  const B l2 = __builtin_amdgcn_perm(t[8], t[8], s2), h2 = __builtin_amdgcn_perm(t[9], t[9], s2);
+  const B l3 = __builtin_amdgcn_perm(t[11], t[10], s3), h3 = __builtin_amdgcn_perm(t[13], t[12], s3);
+  const B l4 = __builtin_amdgcn_perm(t[15], t[14], s4), h4 = __builtin_amdgcn_perm(t[17], t[16], s4);
+  const B l5 = __builtin_amdgcn_perm(t[18], t[18], s5), h5 = __builtin_amdgcn_perm(t[19], t[19], s5);
+  xlo = xor3(xor3(xor3(xlo, l0, l1), l2, l3), l4, l5);
+  xhi = xor3(xor3(xor3(xhi, h0, h1), h2, h3), h4, h5);
+}
+
+// DAGPU_GF16_MUL2 builds keep the 2-bit split everywhere (A/B of round 5)
+#ifdef DAGPU_GF16_MUL2
 __device__ __forceinline__ void mul16_add(uint32_t& xlo, uint32_t& xhi, uint32_t ylo, uint32_t yhi, int pos) {
   mul16_add_t(xlo, xhi, ylo, yhi, g_ptab16 + pos * 16);
 }
+#define MERGED_TAB(m) (g_ptab16_merged + 16 * (m))
+#define MERGED_MUL mul16_add_t
+#else
+__device__ __forceinline__ void mul16_add(uint32_t& xlo, uint32_t& xhi, uint32_t ylo, uint32_t yhi, int pos) {
+  mul16x_add_t(xlo, xhi, ylo, yhi, g_ptab16x + pos * kTab16x);
+}
+#define MERGED_TAB(m) (g_ptab16x_merged + kTab16x * (m))
+#define MERGED_MUL mul16x_add_t
+#endif
 
 // NS elements per lane, 4 symbols each as a low-byte and a high-byte dword
 template <int NS>
@@ -518,7 +562,7 @@ template <class W>
 __device__ __forceinline__ void ifft_fft2_16(W& w, int i, int j, const uint32_t* t) {
   w.lo[j] ^= w.lo[i];
   w.hi[j] ^= w.hi[i];
-  mul16_add_t(w.lo[i], w.hi[i], w.lo[j], w.hi[j], t);
+  MERGED_MUL(w.lo[i], w.hi[i], w.lo[j], w.hi[j], t);
   w.lo[j] ^= w.lo[i];
   w.hi[j] ^= w.hi[i];
 }
@@ -529,11 +573,15 @@ template <int D, int NS = 64, class W>
 __device__ __forceinline__ void ifft16_block(W& w, int base) {
 #pragma unroll
   for (int r = 0; r < NS; r += 4 * D) {
-    const int p01 = base + r + D, p02 = p01 + D, p23 = p01 + 2 * D;
+    // per unit, an opaque base: the unit's tables are loaded at the unit, not
+    // hoisted (with the 20-dword tables, hoisting spilled SGPRs and VGPRs)
+    const int p01 = opaque_s(base) + r + D, p02 = p01 + D, p23 = p01 + 2 * D;
+#pragma unroll
+    for (int i = r; i < r + D; i++) ifft2_16(w, i, i + D, p01);  // layer by layer: one table's
+#pragma unroll                                                      // VGPR copies live at a time
+    for (int i = r; i < r + D; i++) ifft2_16(w, i + 2 * D, i + 3 * D, p23);
 #pragma unroll
     for (int i = r; i < r + D; i++) {
-      ifft2_16(w, i, i + D, p01);
-      ifft2_16(w, i + 2 * D, i + 3 * D, p23);
       ifft2_16(w, i, i + 2 * D, p02);
       ifft2_16(w, i + D, i + 3 * D, p02);
     }
@@ -551,14 +599,17 @@ __device__ __forceinline__ void fft16_block(W& w, int base) {
 #pragma unroll
   for (int r = 0; r < NS; r += 4 * DIST) {
     const int iend = r + DIST;
-    const int p01 = base + iend - 1, p02 = base + iend + DIST - 1, p23 = base + iend + 2 * DIST - 1;
+    const int b = opaque_s(base);  // as in ifft16_block
+    const int p01 = b + iend - 1, p02 = b + iend + DIST - 1, p23 = b + iend + 2 * DIST - 1;
 #pragma unroll
-    for (int i = r; i < r + DIST; i++) {
+    for (int i = r; i < r + DIST; i++) {  // layer by layer, as in ifft16_block
       fft2_16(w, i, i + 2 * DIST, p02);
       fft2_16(w, i + DIST, i + 3 * DIST, p02);
-      fft2_16(w, i, i + DIST, p01);
-      fft2_16(w, i + 2 * DIST, i + 3 * DIST, p23);
     }
+#pragma unroll
+    for (int i = r; i < r + DIST; i++) fft2_16(w, i, i + DIST, p01);
+#pragma unroll
+    for (int i = r; i < r + DIST; i++) fft2_16(w, i + 2 * DIST, i + 3 * DIST, p23);
     __builtin_amdgcn_sched_barrier(0);  // as in ifft16_block
   }
   if constexpr (DIST >= 4) {
@@ -566,7 +617,7 @@ __device__ __forceinline__ void fft16_block(W& w, int base) {
   } else if constexpr (DIST == 2) {
 #pragma unroll
     for (int r = 0; r < NS; r += 2) {
-      fft2_16(w, r, r + 1, base + r);
+      fft2_16(w, r, r + 1, opaque_s(base) + r);
       if (r % 8 == 6) __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -731,7 +782,7 @@ leo16_encode_reg_kernel(EncodeArgs a) {
     // last IFFT layer (dist 256, skew IO - 1 + 256) merged with the first FFT
     // layer (dist 256, skew FO + 255)
 #pragma unroll
-    for (int s0 = 0; s0 < 32; s0++) ifft_fft2_16(w, s0, s0 + 32, g_ptab16_merged + 16);
+    for (int s0 = 0; s0 < 32; s0++) ifft_fft2_16(w, s0, s0 + 32, MERGED_TAB(1));
     // ---- FFT (fftDIT, skew index FO + iend - 1), dist4 = 512: its dist 128 layer (bit 7) ----
 #pragma unroll
     for (int s0 = 0; s0 < 16; s0++) {
@@ -753,8 +804,8 @@ leo16_encode_reg_kernel(EncodeArgs a) {
     for (int b = 0; b < 16; b++) {  // radix-4 dist 64 (bits 6, 7); its dist 128 layer merged with the FFT's
       ifft2_16(w, b, 16 + b, p01);
       ifft2_16(w, 32 + b, 48 + b, p23);
-      ifft_fft2_16(w, b, 32 + b, g_ptab16_merged);
-      ifft_fft2_16(w, 16 + b, 48 + b, g_ptab16_merged);
+      ifft_fft2_16(w, b, 32 + b, MERGED_TAB(0));
+      ifft_fft2_16(w, 16 + b, 48 + b, MERGED_TAB(0));
     }
 #pragma unroll
     for (int b = 0; b < 16; b++) {  // FFT dist4 = 256: its dist 64 layer (bit 6)
@@ -823,8 +874,8 @@ __global__ __launch_bounds__(M * 2) void leo16_encode_reg32_kernel(EncodeArgs a)
     for (int s0 = 0; s0 < 8; s0++) {
       ifft2_16(w, s0, s0 + 8, IO - 1 + 128);
       ifft2_16(w, s0 + 16, s0 + 24, IO - 1 + 384);
-      ifft_fft2_16(w, s0, s0 + 16, g_ptab16_merged + 16);
-      ifft_fft2_16(w, s0 + 8, s0 + 24, g_ptab16_merged + 16);
+      ifft_fft2_16(w, s0, s0 + 16, MERGED_TAB(1));
+      ifft_fft2_16(w, s0 + 8, s0 + 24, MERGED_TAB(1));
     }
     __builtin_amdgcn_sched_barrier(0);
     // ---- FFT (fftDIT, skew index FO + iend - 1) ----
@@ -863,7 +914,7 @@ __global__ __launch_bounds__(M * 2) void leo16_encode_reg32_kernel(EncodeArgs a)
     }
     // bit 7 (slot dist 16): the last IFFT layer merged with the first FFT layer (dist 128)
 #pragma unroll
-    for (int s0 = 0; s0 < 16; s0++) ifft_fft2_16(w, s0, s0 + 16, g_ptab16_merged);
+    for (int s0 = 0; s0 < 16; s0++) ifft_fft2_16(w, s0, s0 + 16, MERGED_TAB(0));
     __builtin_amdgcn_sched_barrier(0);
     // ---- FFT (fftDIT, skew index FO + iend - 1): radix-4 dist4 = 128 (bits 6, 5) ----
 #pragma unroll
@@ -1453,6 +1504,305 @@ __global__ __launch_bounds__(kDec1k) __attribute__((amdgpu_waves_per_eu(4, 4))) 
   DEC_PROBE(10);
 }
 
+// ---------------------------------------------------------------------------
+// k = 512 decoder, round 5 (leo16_decode_h1k_kernel): unpacked symbols with
+// the 3/3/2 multiply (mul16x_add_t, 28 ops per 4 symbols) instead of the
+// packed 2-bit one (22 ops per 2 symbols).  Unpacked, a lane holds 4 symbols of
+// an element in 2 VGPRs, so 1,024 elements x 64 lanes would need the CU's
+// whole register file; instead each register holds TWO elements, one per half
+// wave (lanes 0-31 / 32-63, both halves the same 256 B of their shards):
+// 16 waves x 32 register pairs x 2 halves = 1,024 elements, 64 data VGPRs.
+// The half is element bit 0, so every layer but bit 0's has one skew position
+// per register (the position depends on the bits above the layer's only).
+// Layouts (q = wave, j = register pair, hl = lane half):
+//   B  e = 64 q + 2 j + hl            layers on bits 1-5 (register bits 0-4)
+//   T  e = hl | (j & 1) << 1 | q << 2 | (j >> 1) << 6
+//                                     layers on bits 6-9, the formal derivative
+//   S  e = 64 q + 2 (j & 15) + (j >> 4) + 32 hl
+//                                     loads, stores, pre/post multiplies and the
+//                                     bit-0 layer: pair (j, j + 16) is (x, y)
+// S <-> B is one v_permlane32_swap per register pair (j, j + 16); B <-> T a
+// 16 x 16 LDS transpose of q with j >> 1.  In S the two halves of a register
+// belong to different bit-0 butterflies, so that layer's tables are per lane:
+// 20 dwords read from g_ptab16x with vector loads (the other layers' come
+// from SGPRs).  Pre/post multiplies: the decoders' 16-dword LDS tables
+// (mul16_table_to), read per lane.
+// ---------------------------------------------------------------------------
+constexpr int kDecH = 1024;
+using W32 = W16n<32>;
+
+// e of register j, lane half hl, in layout S (within the wave's 64 elements)
+__device__ __forceinline__ constexpr int s_local(int j, int hl) { return 2 * (j & 15) + (j >> 4) + 32 * hl; }
+
+// layout S <-> B: halves between registers j and j + 16
+__device__ __forceinline__ void swap_sb(W32& w) {
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    const auto l = __builtin_amdgcn_permlane32_swap(w.lo[j], w.lo[j + 16], false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(w.hi[j], w.hi[j + 16], false, false);
+    w.lo[j] = l[0];
+    w.lo[j + 16] = l[1];
+    w.hi[j] = h[0];
+    w.hi[j + 16] = h[1];
+  }
+}
+
+// a skew position's 3/3/2 table into VGPRs (pos differs between the halves)
+__device__ __forceinline__ void lane_tab(int pos, uint32_t (&t)[kTab16x]) {
+  const uint4* p = (const uint4*)(g_ptab16x + pos * kTab16x);
+#pragma unroll
+  for (int i = 0; i < kTab16x / 4; i++) {
+    const uint4 v = p[i];
+    t[4 * i] = v.x;
+    t[4 * i + 1] = v.y;
+    t[4 * i + 2] = v.z;
+    t[4 * i + 3] = v.w;
+  }
+}
+
+// bit-0 layer in layout S: x = register j, y = register j + 16 (j < 16), the
+// pair's position = e of x (ifftDITDecoder / fftDIT: iend - 1 = block start)
+// (the position passes through an asm that reads the pair's data: the IFFT's
+// and the FFT's loads of the same tables are neither merged nor hoisted, which
+// kept all 16 tables live through the kernel)
+__device__ __forceinline__ int opaque_v(int x, uint32_t tok) {
+  asm volatile("" : "+v"(x) : "v"(tok));
+  return x;
+}
+template <bool INV>
+__device__ __forceinline__ void layer0_s(W32& w, int q, int hl) {
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    uint32_t t[kTab16x];
+    // pair j's table is loaded once pair j - 1 is done: one table live at a time
+    lane_tab(opaque_v(64 * q + 2 * j + 32 * hl, w.lo[j > 0 ? j - 1 : 0]), t);
+    if constexpr (INV) {  // ifftDIT2: y ^= x; x ^= y * skew
+      w.lo[j + 16] ^= w.lo[j];
+      w.hi[j + 16] ^= w.hi[j];
+      mul16x_add_t(w.lo[j], w.hi[j], w.lo[j + 16], w.hi[j + 16], t);
+    } else {  // fftDIT2: x ^= y * skew; y ^= x
+      mul16x_add_t(w.lo[j], w.hi[j], w.lo[j + 16], w.hi[j + 16], t);
+      w.lo[j + 16] ^= w.lo[j];
+      w.hi[j + 16] ^= w.hi[j];
+    }
+    // computed here: otherwise the compiler sinks each pair's multiply to the
+    // first use of its result and keeps the loaded tables live until then
+    asm volatile("" : "+v"(w.lo[j]), "+v"(w.hi[j]), "+v"(w.lo[j + 16]), "+v"(w.hi[j + 16]));
+  }
+}
+
+// a butterfly's results computed where it stands (the scheduler otherwise
+// sinks multiplies toward their consumers and spills their operands)
+__device__ __forceinline__ void pin_pair(W32& w, int i, int j) {
+  asm volatile("" : "+v"(w.lo[i]), "+v"(w.hi[i]), "+v"(w.lo[j]), "+v"(w.hi[j]));
+}
+
+// One layer on element bit b >= 1 in layout B (dist D = 1 << b, registers j
+// and j + D / 2): butterflies grouped by skew position (block of 2 D elements,
+// position = block start + D - 1), one table per group.
+template <bool INV, int D>
+__device__ __forceinline__ void layer_b(W32& w, int q) {
+  constexpr int RD = D / 2;
+#pragma unroll
+  for (int r = 0; r < 64; r += 2 * D) {
+    const int pos = opaque_tok(64 * q + r + D - 1, w.lo[r / 2]);
+#pragma unroll
+    for (int e = r; e < r + D; e += 2) {
+      if constexpr (INV) ifft2_16(w, e / 2, e / 2 + RD, pos);
+      else fft2_16(w, e / 2, e / 2 + RD, pos);
+      pin_pair(w, e / 2, e / 2 + RD);
+    }
+  }
+}
+
+// One layer on element bit b in 6..9 in layout T (register bit b - 5):
+// positions are compile-time (bits above b are register bits).
+template <bool INV, int D>
+__device__ __forceinline__ void layer_t(W32& w) {
+  constexpr int RD = 2 * (D / 64);
+#pragma unroll
+  for (int blk = 0; blk < 1024; blk += 2 * D) {  // element block start (bits > b)
+    constexpr int j0 = 0;
+    const int jf = (blk >> 6) << 1;  // first register of the block
+    const int pos = opaque_tok(blk + D - 1, w.lo[jf + j0]);  // loaded here, not hoisted / merged
+#pragma unroll
+    for (int j = 0; j < 32; j++) {
+      if (j & RD) continue;
+      if ((((j >> 1) << 6) & ~(2 * D - 1)) != blk) continue;
+      if constexpr (INV) ifft2_16(w, j, j + RD, pos);
+      else fft2_16(w, j, j + RD, pos);
+      pin_pair(w, j, j + RD);
+    }
+  }
+}
+
+// B <-> T: wave q, register (jj << 1) | r0  <->  wave jj, register (q << 1) | r0
+__device__ __forceinline__ void xpose_bt(W32& w, uint32_t* lds, int q, int lane) {
+#pragma unroll
+  for (int r0 = 0; r0 < 2; r0++) {
+#pragma unroll
+    for (int lh = 0; lh < 2; lh++) {
+#pragma unroll
+      for (int c = 0; c < 16; c++) lds[(c * 16 + q) * 64 + lane] = lh ? w.hi[(c << 1) | r0] : w.lo[(c << 1) | r0];
+      __syncthreads();
+#pragma unroll
+      for (int c = 0; c < 16; c++) {
+        const uint32_t v = lds[(q * 16 + c) * 64 + lane];
+        if (lh) w.hi[(c << 1) | r0] = v;
+        else w.lo[(c << 1) | r0] = v;
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Formal derivative in layout T, D(x)_e = x_e ^ XOR_{s: bit s of e = 0} x_{e | 2^s}:
+// register bits (element bits 1, 6-9) in place in ascending register order,
+// wave bits (2-5) and the half bit (0, lanes 0-31 read lane + 32) from the
+// originals staged in LDS, 8 register pairs per round.
+__device__ __forceinline__ void derivative_t(W32& w, uint32_t* lds, int c, int lane, uint32_t lowmask) {
+  constexpr int B = 8;
+#pragma unroll
+  for (int s0 = 0; s0 < 32; s0 += B) {
+#pragma unroll
+    for (int u = 0; u < B; u++) {
+      lds[((c * B + u) * 2) * 64 + lane] = w.lo[s0 + u];
+      lds[((c * B + u) * 2 + 1) * 64 + lane] = w.hi[s0 + u];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < B; u++) {
+      const int j = s0 + u;
+      uint32_t alo = w.lo[j], ahi = w.hi[j];
+#pragma unroll
+      for (int bit = 1; bit < 32; bit <<= 1)
+        if ((j & bit) == 0) {
+          alo ^= w.lo[j | bit];
+          ahi ^= w.hi[j | bit];
+        }
+#pragma unroll
+      for (int wb = 1; wb < 16; wb <<= 1)
+        if ((c & wb) == 0) {
+          alo ^= lds[(((c | wb) * B + u) * 2) * 64 + lane];
+          ahi ^= lds[(((c | wb) * B + u) * 2 + 1) * 64 + lane];
+        }
+      // bit 0: lanes 0-31 (hl = 0) add their partner's (lane + 32) original
+      alo ^= lds[((c * B + u) * 2) * 64 + (lane ^ 32)] & lowmask;
+      ahi ^= lds[((c * B + u) * 2 + 1) * 64 + (lane ^ 32)] & lowmask;
+      asm volatile("" : "+v"(alo), "+v"(ahi));  // one register's partner reads in flight at a time
+      w.lo[j] = alo;
+      w.hi[j] = ahi;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kDecH) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_decode_h1k_kernel(
+    DecodeArgs a) {
+  constexpr int K = kDecH / 2;
+  // dynamic LDS (kDecHLds): [0, 64 KiB) premultiply tables, then transposes and
+  // derivative staging; [64, 128 KiB) the erased elements' tables
+  extern __shared__ __attribute__((aligned(16))) uint32_t dyn_lds[];
+  uint32_t* lds = dyn_lds;
+  uint32_t* post_tab = dyn_lds + 16 * 16 * 64;
+  const long blk = blockIdx.x;
+  const int piece = (int)(blk % a.nchunk);  // nchunk = 256-B pieces of the shard
+  const long v = blk / a.nchunk;
+  if (a.flags[v] == 0) return;  // uniform
+  const long sq = v / a.nvec, vec = v % a.nvec;
+  const int lane = threadIdx.x & 63;
+  const int hl = lane >> 5;
+  const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lowmask = hl ? 0u : 0xFFFFFFFFu;
+  // lane (hl, c): 64-B block c >> 3 of this 256-B piece, symbols 4 (c & 7) .. +3
+  const uint32_t col = (uint32_t)piece * 256u + (uint32_t)((lane & 31) >> 3) * 64u + (uint32_t)(lane & 7) * 4u;
+  const uint32_t voff = col + (uint32_t)hl * 32u * (uint32_t)a.shard_stride;  // upper half: shard + 32
+  const auto rsrc = make_rsrc(a.data + sq * a.sq_stride + vec * a.vec_stride);
+  const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
+  const uint16_t* err = (const uint16_t*)(a.err + err_vec(a, v) * rs_err_bytes(K));
+  // thread t builds element t's tables (pre: zero if missing; post: read for missing only)
+  const int my_i = 64 * q + lane;
+  const int my_shard = my_i < K ? K + my_i : my_i - K;
+  const uint64_t pm = __builtin_amdgcn_ballot_w64(pres[(long)my_shard * a.p_shard_stride] != 0);
+  const uint32_t my_err = err[my_i];
+  mul16_table_to(lds + threadIdx.x * 16, my_err, !((pm >> lane) & 1));
+  mul16_table_to(post_tab + threadIdx.x * 16, kMod16 - my_err, (pm >> lane) & 1);
+  W32 w;
+  const int q_ld = opaque_s(q);
+#pragma unroll
+  for (int j = 0; j < 32; j++) {
+    const int i = 64 * q_ld + s_local(j, 0);
+    const int shard = i < K ? K + i : i - K;
+    const uint32_t so = (uint32_t)shard * (uint32_t)a.shard_stride;
+    w.lo[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, so, 0);
+    w.hi[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff + 32u, so, 0);
+  }
+  __syncthreads();
+  const int q_pm = opaque_s(q);
+#pragma unroll
+  for (int j = 0; j < 32; j++) {
+    uint32_t t[16];
+    mul16_table_from(lds, 64 * q_pm + s_local(j, 0) + 32 * hl, t);
+    uint32_t xl = w.lo[j], xh = w.hi[j];
+    mul16_by(xl, xh, t);
+    asm volatile("" : "+v"(xl), "+v"(xh));  // one element's table live at a time
+    w.lo[j] = xl;
+    w.hi[j] = xh;
+  }
+  __syncthreads();  // the transposes reuse the premultiply tables' LDS
+  // ---- IFFT (ifftDITDecoder, skew index iend - 1) ----
+  layer0_s<true>(w, q, hl);
+  swap_sb(w);
+  layer_b<true, 2>(w, q);
+  layer_b<true, 4>(w, q);
+  layer_b<true, 8>(w, q);
+  layer_b<true, 16>(w, q);
+  layer_b<true, 32>(w, q);
+  xpose_bt(w, lds, q, lane);
+  layer_t<true, 64>(w);
+  layer_t<true, 128>(w);
+  layer_t<true, 256>(w);
+  layer_t<true, 512>(w);
+  derivative_t(w, lds, q, lane, lowmask);
+  // ---- FFT (fftDIT, skew index iend - 1) ----
+  layer_t<false, 512>(w);
+  layer_t<false, 256>(w);
+  layer_t<false, 128>(w);
+  layer_t<false, 64>(w);
+  xpose_bt(w, lds, q, lane);
+  layer_b<false, 32>(w, q);
+  layer_b<false, 16>(w, q);
+  layer_b<false, 8>(w, q);
+  layer_b<false, 4>(w, q);
+  layer_b<false, 2>(w, q);
+  swap_sb(w);
+  layer0_s<false>(w, q, hl);
+  // erased shards = work * (65535 - errLocs), per lane; a register whose two
+  // elements are both given is skipped (wave-uniform)
+  uint64_t pm_e = pm;
+  int q_e = q;
+  asm volatile("" : "+s"(pm_e), "+s"(q_e));
+  const uint32_t pmh = hl ? (uint32_t)(pm_e >> 32) : (uint32_t)pm_e;
+#pragma unroll
+  for (int j = 0; j < 32; j++) {
+    const int l0 = s_local(j, 0);
+    if (((pm_e >> l0) & 1) && ((pm_e >> (l0 + 32)) & 1)) continue;  // uniform
+    uint32_t t[16];
+    mul16_table_from(post_tab, 64 * q_e + l0 + 32 * hl, t);
+    uint32_t xl = w.lo[j], xh = w.hi[j];
+    mul16_by(xl, xh, t);
+    asm volatile("" : "+v"(xl), "+v"(xh));
+    const int i = 64 * q_e + l0;
+    const int shard = i < K ? K + i : i - K;
+    const uint32_t so = (uint32_t)shard * (uint32_t)a.shard_stride;
+    if (!((pmh >> l0) & 1)) {
+      __builtin_amdgcn_raw_buffer_store_b32(xl, rsrc, voff, so, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(xh, rsrc, voff + 32u, so, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // Tables are module globals: upload once per device.
 std::mutex g_tab_mu;
 bool g_tab_done[64];
@@ -1523,6 +1873,32 @@ hipError_t ensure_tables() {
         }
     }
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_ptab16_merged), mt.data(), mt.size() * 4)) != hipSuccess) return e;
+    // 3/3/2-split tables (mul16x_add_t): per skew position and for the two merged elements
+    auto tab332 = [&](unsigned c, uint32_t* out) {  // c = field element (0: zero table)
+      for (int i = 0; i < kTab16x; i++) out[i] = 0;
+      if (!c) return;
+      const unsigned lc = t.log[c];
+      static const int shift[6] = {0, 3, 6, 8, 11, 14}, width[6] = {3, 3, 2, 3, 3, 2};
+      static const int base[6] = {0, 4, 8, 10, 14, 18};
+      for (int g = 0; g < 6; g++)
+        for (int e2 = 1; e2 < (1 << width[g]); e2++) {
+          const unsigned x = (unsigned)e2 << shift[g];
+          unsigned sidx = (unsigned)t.log[x] + lc;
+          sidx = (sidx + (sidx >> 16)) & 0xFFFFu;
+          const unsigned prod = t.exp[sidx];
+          const int lo_dw = width[g] == 3 ? base[g] + (e2 >> 2) : base[g];
+          const int hi_dw = width[g] == 3 ? base[g] + 2 + (e2 >> 2) : base[g] + 1;
+          out[lo_dw] |= (prod & 0xFFu) << (8 * (e2 & 3));
+          out[hi_dw] |= ((prod >> 8) & 0xFFu) << (8 * (e2 & 3));
+        }
+    };
+    std::vector<uint32_t> px((size_t)kTabPos * kTab16x, 0u);
+    for (int pos = 0; pos < kTabPos; pos++)
+      if (t.skew[pos] != kMod16) tab332((unsigned)t.exp[t.skew[pos]], px.data() + (size_t)pos * kTab16x);
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_ptab16x), px.data(), px.size() * 4)) != hipSuccess) return e;
+    std::vector<uint32_t> mx(2 * kTab16x, 0u);
+    for (int m = 0; m < 2; m++) tab332(elem(pairs[m][0]) ^ elem(pairs[m][1]), mx.data() + (size_t)m * kTab16x);
+    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_ptab16x_merged), mx.data(), mx.size() * 4)) != hipSuccess) return e;
     uint16_t lb[16];
     for (int b = 0; b < 16; b++) lb[b] = (uint16_t)t.log[1u << b];
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_logbit16), lb, sizeof lb)) != hipSuccess) return e;
@@ -1626,6 +2002,7 @@ hipError_t launch_leo16_errlocs(const DecodeArgs& a, hipStream_t s) {
 // dynamic LDS of the register-resident decoders: staging + erasure tables
 constexpr size_t kDecLds = (8 * 16 * 2 * 64 + kDecN * 16) * sizeof(uint32_t);    // 96 KiB
 constexpr size_t kDec1kLds = (16 * 16 * 64 + kDec1k * 16) * sizeof(uint32_t);     // 128 KiB
+constexpr size_t kDecHLds = (16 * 16 * 64 + kDecH * 16) * sizeof(uint32_t);       // 128 KiB
 static hipError_t dec_lds_attr() {  // above the 64 KiB default: once per process
   static std::once_flag once;
   static hipError_t err = hipSuccess;
@@ -1635,8 +2012,21 @@ static hipError_t dec_lds_attr() {  // above the 64 KiB default: once per proces
     if (err == hipSuccess)
       err = hipFuncSetAttribute((const void*)leo16_decode_reg1k_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDec1kLds);
+    if (err == hipSuccess)
+      err = hipFuncSetAttribute((const void*)leo16_decode_h1k_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDecHLds);
   });
   return err;
+}
+
+// k = 512 decoder: the half-lane unpacked kernel (round 5); DAGPU_DEC1K_PACKED=1
+// selects the packed one of rounds 2-4 (A/B)
+static bool dec1k_packed() {
+  static const bool v = [] {
+    const char* e = getenv("DAGPU_DEC1K_PACKED");
+    return e && e[0] == '1';
+  }();
+  return v;
 }
 
 hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mark_present) {
@@ -1656,7 +2046,10 @@ hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mar
     DecodeArgs b = a;
     b.nchunk = a.shard_bytes / 256;
     if ((e = dec_lds_attr()) != hipSuccess) return e;
-    hipLaunchKernelGGL(leo16_decode_reg1k_kernel, dim3((unsigned)(nv * b.nchunk)), dim3(kDec1k), kDec1kLds, s, b);
+    if (dec1k_packed())
+      hipLaunchKernelGGL(leo16_decode_reg1k_kernel, dim3((unsigned)(nv * b.nchunk)), dim3(kDec1k), kDec1kLds, s, b);
+    else
+      hipLaunchKernelGGL(leo16_decode_h1k_kernel, dim3((unsigned)(nv * b.nchunk)), dim3(kDecH), kDecHLds, s, b);
   } else
 #endif
   {

@@ -286,12 +286,15 @@ def test_wide_k8192_square(ctx):
     ds.load_ods(ods)
     ds.extend()
     torch.cuda.synchronize()
+    print("k=8192: extended", flush=True)
     assert int(ds.status[0]) == 0
     rng = np.random.default_rng(8192)
     _wide_square_checks(ds, ods, k, rng, n_rows=1, n_cols=2)
+    print("k=8192: sampled vectors, roots and DAH checked", flush=True)
     ds.workspace = None
     torch.cuda.empty_cache()
     _max_erasure_repair(ctx, ds, k, rng)
+    print("k=8192: repaired", flush=True)
     e = ds.eds.view(w, w, 512)
     q0 = ods.reshape(k, k, 512)
     for r in rng.choice(k, 2, replace=False):

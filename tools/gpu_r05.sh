@@ -1,0 +1,30 @@
+# Round-5 GPU steps (each: its GPU tests, then an interleaved A/B through
+# tools/gpu_ab.sh).  Steps comparing against the previous build expect it in
+# celestia-app_amd/libdagpu_prev.so (built from the parent commit; .so files are
+# not in git).  Results: the profiles/*_r05.log named in DESIGN.md.
+#   bash tools/gpu_r05.sh <step>
+set -o pipefail
+mkdir -p gpurun_out
+case "$1" in
+  base)  # round 5 start: new tests (started-repair structure, k = 1024 chunked DAH, k = 4096 / 8192 squares), default bench, stress counters
+    timeout -k 10 900 python -u -m pytest -x -v -s --timeout 400 --timeout-method thread tests/test_gpu_repair_async.py tests/test_gpu_wide.py > gpurun_out/r05_base_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r05_base_tests.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 400 python -u bench.py > gpurun_out/r05_base_bench.log 2>&1 || { echo "bench failed"; tail -5 gpurun_out/r05_base_bench.log; exit 1; }
+    bash tools/gpu_pmc_gf16.sh repair512 split512 repair128
+    ;;
+  mul332)  # round 5: GF(2^16) multiply with a 3/3/2 bit split (12 v_perm per 4 symbols instead of 16), units layer by layer: tests, A/B vs the previous build
+    bash tools/gpu_ab.sh --tests "tests/test_gpu_gf16.py tests/test_gpu_repair_fill.py tests/test_gpu_split.py tests/test_gpu_wide.py tests/test_gpu_repair_byz.py" --rounds 2 split512 new= prev=lib:celestia-app_amd/libdagpu_prev.so && \
+    bash tools/gpu_ab.sh --rounds 2 repair512q3 new= prev=lib:celestia-app_amd/libdagpu_prev.so && \
+    bash tools/gpu_ab.sh --rounds 1 "bench:--mode repair --k 256 --batch 8 --steps 5 --warmup 1" new= prev=lib:celestia-app_amd/libdagpu_prev.so && \
+    bash tools/gpu_ab.sh --rounds 1 repair512 new= prev=lib:celestia-app_amd/libdagpu_prev.so
+    ;;
+  first)  # round 5 first GPU pass: correctness of everything new (3/3/2 multiply, half-lane k = 512 decoder, started-repair fixes, wide squares), then A/Bs
+    timeout -k 10 900 python -u -m pytest -x -v -s --timeout 400 --timeout-method thread tests/test_gpu_gf16.py tests/test_gpu_repair_async.py tests/test_gpu_wide.py tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py > gpurun_out/r05_first_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r05_first_tests.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 2 repair512 new= packed=DAGPU_DEC1K_PACKED=1 prev=lib:celestia-app_amd/libdagpu_prev.so && \
+    bash tools/gpu_ab.sh --rounds 2 split512 new= prev=lib:celestia-app_amd/libdagpu_prev.so && \
+    bash tools/gpu_ab.sh --rounds 1 repair512q3 new= prev=lib:celestia-app_amd/libdagpu_prev.so && \
+    bash tools/gpu_pmc_gf16.sh repair512 split512
+    ;;
+  *) echo "steps: base mul332 first"; exit 2;;
+esac
