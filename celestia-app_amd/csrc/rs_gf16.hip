@@ -1569,13 +1569,15 @@ __device__ __forceinline__ int opaque_v(int x, uint32_t tok) {
   asm volatile("" : "+v"(x) : "v"(tok));
   return x;
 }
-template <bool INV>
+// OFF: skew offset of the transform (decoder 0; encoder IFFT IO, FFT FO --
+// ifftDITEncoder's index IO - 1 + iend is OFF + block start + dist - 1 too)
+template <bool INV, int OFF = 0>
 __device__ __forceinline__ void layer0_s(W32& w, int q, int hl) {
 #pragma unroll
   for (int j = 0; j < 16; j++) {
     uint32_t t[kTab16x];
     // pair j's table is loaded once pair j - 1 is done: one table live at a time
-    lane_tab(opaque_v(64 * q + 2 * j + 32 * hl, w.lo[j > 0 ? j - 1 : 0]), t);
+    lane_tab(opaque_v(OFF + 64 * q + 2 * j + 32 * hl, w.lo[j > 0 ? j - 1 : 0]), t);
     if constexpr (INV) {  // ifftDIT2: y ^= x; x ^= y * skew
       w.lo[j + 16] ^= w.lo[j];
       w.hi[j + 16] ^= w.hi[j];
@@ -1600,12 +1602,12 @@ __device__ __forceinline__ void pin_pair(W32& w, int i, int j) {
 // One layer on element bit b >= 1 in layout B (dist D = 1 << b, registers j
 // and j + D / 2): butterflies grouped by skew position (block of 2 D elements,
 // position = block start + D - 1), one table per group.
-template <bool INV, int D>
+template <bool INV, int D, int OFF = 0>
 __device__ __forceinline__ void layer_b(W32& w, int q) {
   constexpr int RD = D / 2;
 #pragma unroll
   for (int r = 0; r < 64; r += 2 * D) {
-    const int pos = opaque_tok(64 * q + r + D - 1, w.lo[r / 2]);
+    const int pos = opaque_tok(OFF + 64 * q + r + D - 1, w.lo[r / 2]);
 #pragma unroll
     for (int e = r; e < r + D; e += 2) {
       if constexpr (INV) ifft2_16(w, e / 2, e / 2 + RD, pos);
@@ -1615,20 +1617,22 @@ __device__ __forceinline__ void layer_b(W32& w, int q) {
   }
 }
 
-// One layer on element bit b in 6..9 in layout T (register bit b - 5):
+// One layer on element bit b >= 6 in layout T (LR low register bits stay
+// element bits 1..LR, the wave holds the next 5 - LR, register bits LR.. are
+// element bits 6..; decoder n = 1024: LR = 1, encoder m = 512: LR = 2):
 // positions are compile-time (bits above b are register bits).
-template <bool INV, int D>
+template <bool INV, int D, int LR = 1, int OFF = 0>
 __device__ __forceinline__ void layer_t(W32& w) {
-  constexpr int RD = 2 * (D / 64);
+  constexpr int RD = (D / 64) << LR;
+  constexpr int N = 64 << (5 - LR);  // elements of the transform
 #pragma unroll
-  for (int blk = 0; blk < 1024; blk += 2 * D) {  // element block start (bits > b)
-    constexpr int j0 = 0;
-    const int jf = (blk >> 6) << 1;  // first register of the block
-    const int pos = opaque_tok(blk + D - 1, w.lo[jf + j0]);  // loaded here, not hoisted / merged
+  for (int blk = 0; blk < N; blk += 2 * D) {  // element block start (bits > b)
+    const int jf = (blk >> 6) << LR;  // first register of the block
+    const int pos = opaque_tok(OFF + blk + D - 1, w.lo[jf]);  // loaded here, not hoisted / merged
 #pragma unroll
     for (int j = 0; j < 32; j++) {
       if (j & RD) continue;
-      if ((((j >> 1) << 6) & ~(2 * D - 1)) != blk) continue;
+      if ((((j >> LR) << 6) & ~(2 * D - 1)) != blk) continue;
       if constexpr (INV) ifft2_16(w, j, j + RD, pos);
       else fft2_16(w, j, j + RD, pos);
       pin_pair(w, j, j + RD);
@@ -1636,21 +1640,29 @@ __device__ __forceinline__ void layer_t(W32& w) {
   }
 }
 
-// B <-> T: wave q, register (jj << 1) | r0  <->  wave jj, register (q << 1) | r0
+// B <-> T: wave q, register (jj << LR) | r  <->  wave jj, register (q << LR) | r
+// (NQ = 32 >> LR waves); RPR values of r per LDS round (NQ * NQ * RPR * 256 B)
+template <int LR = 1, int RPR = 1>
 __device__ __forceinline__ void xpose_bt(W32& w, uint32_t* lds, int q, int lane) {
+  constexpr int NQ = 32 >> LR;
 #pragma unroll
-  for (int r0 = 0; r0 < 2; r0++) {
+  for (int r0 = 0; r0 < (1 << LR); r0 += RPR) {
 #pragma unroll
     for (int lh = 0; lh < 2; lh++) {
 #pragma unroll
-      for (int c = 0; c < 16; c++) lds[(c * 16 + q) * 64 + lane] = lh ? w.hi[(c << 1) | r0] : w.lo[(c << 1) | r0];
+      for (int c = 0; c < NQ; c++)
+#pragma unroll
+        for (int u = 0; u < RPR; u++)
+          lds[((c * NQ + q) * RPR + u) * 64 + lane] = lh ? w.hi[(c << LR) | (r0 + u)] : w.lo[(c << LR) | (r0 + u)];
       __syncthreads();
 #pragma unroll
-      for (int c = 0; c < 16; c++) {
-        const uint32_t v = lds[(q * 16 + c) * 64 + lane];
-        if (lh) w.hi[(c << 1) | r0] = v;
-        else w.lo[(c << 1) | r0] = v;
-      }
+      for (int c = 0; c < NQ; c++)
+#pragma unroll
+        for (int u = 0; u < RPR; u++) {
+          const uint32_t v = lds[((q * NQ + c) * RPR + u) * 64 + lane];
+          if (lh) w.hi[(c << LR) | (r0 + u)] = v;
+          else w.lo[(c << LR) | (r0 + u)] = v;
+        }
       __syncthreads();
     }
   }
@@ -1803,6 +1815,137 @@ __global__ __launch_bounds__(kDecH) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   }
 }
 
+// ---------------------------------------------------------------------------
+// k = 512 encoder, round 5 (leo16_encode_h_kernel): the half-lane layouts of
+// leo16_decode_h1k_kernel over m = 512 elements -- 8 waves (512 threads) x 32
+// register pairs x 2 halves, 64 data VGPRs within the 128 of 4 waves per SIMD
+// -- so TWO workgroups share a CU and one's loads and stores overlap the
+// other's transform (leo16_encode_reg32_kernel's 16 waves filled a CU alone
+// and left its load and store phases bare).  A workgroup covers 256 B of its
+// vector's shards.  Layouts as the decoder's, with T for LR = 2:
+//   T  e = hl | (j & 3) << 1 | q << 3 | (j >> 2) << 6.
+// The last IFFT layer and the first FFT layer (both dist 256, registers j and
+// j + 16 in T) are merged as in the other encoders.
+// ---------------------------------------------------------------------------
+constexpr int kEncH = 512;
+template <bool REV>
+__global__ __launch_bounds__(kEncH) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_encode_h_kernel(
+    EncodeArgs a) {
+  constexpr int M = 512, IO = REV ? 0 : M, FO = REV ? M : 0;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[8 * 8 * 2 * 64];  // 32 KiB per transpose round
+  const long blk = blockIdx.x;
+  const int piece = (int)(blk % a.nchunk);  // nchunk = 256-B pieces of the shard
+  const long sv = blk / a.nchunk;
+  const long vec = sv % a.nvec;
+  const long sq = sv / a.nvec;
+  if (vec_skipped(a, sv)) return;  // uniform
+  const int lane = threadIdx.x & 63;
+  const int hl = lane >> 5;
+  const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t col = (uint32_t)piece * 256u + (uint32_t)((lane & 31) >> 3) * 64u + (uint32_t)(lane & 7) * 4u;
+  const bool active = col < (uint32_t)a.shard_bytes;
+  const uint32_t cl = active ? col : 0u;  // inactive lanes read valid memory, store nothing
+  W32 w;
+  {
+    const auto in_rsrc = make_rsrc(a.in + sq * a.in_sq_stride + vec * a.in_vec_stride);
+    const uint32_t vin = cl + (uint32_t)hl * 32u * (uint32_t)a.in_shard_stride;  // upper half: shard + 32
+    const int q_ld = opaque_s(q);
+#pragma unroll
+    for (int j = 0; j < 32; j++) {
+      const uint32_t so = (uint32_t)(64 * q_ld + s_local(j, 0)) * (uint32_t)a.in_shard_stride;
+      w.lo[j] = __builtin_amdgcn_raw_buffer_load_b32(in_rsrc, vin, so, 0);
+      w.hi[j] = __builtin_amdgcn_raw_buffer_load_b32(in_rsrc, vin + 32u, so, 0);
+    }
+    if (a.copy && active) {  // Q0 placement
+      const auto cp = make_rsrc(a.copy + sq * a.copy_sq_stride + vec * a.copy_vec_stride);
+      const uint32_t vcp = col + (uint32_t)hl * 32u * (uint32_t)a.copy_shard_stride;
+#pragma unroll
+      for (int j = 0; j < 32; j++) {
+        const uint32_t so = (uint32_t)(64 * q_ld + s_local(j, 0)) * (uint32_t)a.copy_shard_stride;
+        __builtin_amdgcn_raw_buffer_store_b32(w.lo[j], cp, vcp, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(w.hi[j], cp, vcp + 32u, so, 0);
+      }
+    }
+  }
+  // Repair fill: which out-half shards are given (element 64 q + lane), read
+  // before the transform so that the store loop does not wait on presence loads
+  const uint64_t given = a.out_present ? __builtin_amdgcn_ballot_w64(fill_given(a, sq, vec, 64 * q + lane)) : 0ull;
+  // ---- IFFT (ifftDITEncoder, skew index IO - 1 + iend) ----
+  layer0_s<true, IO>(w, q, hl);
+  swap_sb(w);
+  layer_b<true, 2, IO>(w, q);
+  layer_b<true, 4, IO>(w, q);
+  layer_b<true, 8, IO>(w, q);
+  layer_b<true, 16, IO>(w, q);
+  layer_b<true, 32, IO>(w, q);
+  xpose_bt<2, 2>(w, lds, q, lane);
+  layer_t<true, 64, 2, IO>(w);
+  layer_t<true, 128, 2, IO>(w);
+  // last IFFT layer (dist 256, skew IO - 1 + 256) merged with the first FFT
+  // layer (dist 256, skew FO + 255): registers j, j + 16
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    ifft_fft2_16(w, j, j + 16, MERGED_TAB(1));
+    pin_pair(w, j, j + 16);
+  }
+  // ---- FFT (fftDIT, skew index FO + iend - 1) ----
+  layer_t<false, 128, 2, FO>(w);
+  layer_t<false, 64, 2, FO>(w);
+  xpose_bt<2, 2>(w, lds, q, lane);
+  layer_b<false, 32, FO>(w, q);
+  layer_b<false, 16, FO>(w, q);
+  layer_b<false, 8, FO>(w, q);
+  layer_b<false, 4, FO>(w, q);
+  layer_b<false, 2, FO>(w, q);
+  swap_sb(w);
+  layer0_s<false, FO>(w, q, hl);
+  if (!active) return;
+  // ---- store: compare (prerepairSanityCheck), Repair fill, or plain ----
+  const auto out_rsrc = make_rsrc(a.out + sq * a.out_sq_stride + vec * a.out_vec_stride);
+  const uint32_t vout = col + (uint32_t)hl * 32u * (uint32_t)a.out_shard_stride;
+  const int q_st = opaque_s(q);
+  if (a.mismatch) {
+    uint32_t diff = 0;
+#pragma unroll
+    for (int j = 0; j < 32; j++) {
+      const uint32_t so = (uint32_t)(64 * q_st + s_local(j, 0)) * (uint32_t)a.out_shard_stride;
+      diff |= w.lo[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, vout, so, 0);
+      diff |= w.hi[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, vout + 32u, so, 0);
+    }
+    if (diff) {
+      atomicOr(&a.mismatch[sq], a.mismatch_bit);
+      if (a.mismatch_vec) a.mismatch_vec[sq * a.nvec + vec] = 1;
+    }
+    return;
+  }
+  if (a.out_present) {  // store the missing shards of the out half, compare given ones
+    uint64_t g = given;
+    asm volatile("" : "+s"(g));
+    const uint32_t gh = hl ? (uint32_t)(g >> 32) : (uint32_t)g;
+    uint32_t diff = 0;
+#pragma unroll
+    for (int j = 0; j < 32; j++) {
+      const int l0 = s_local(j, 0);
+      const uint32_t so = (uint32_t)(64 * q_st + l0) * (uint32_t)a.out_shard_stride;
+      if ((gh >> l0) & 1) {
+        diff |= w.lo[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, vout, so, 0);
+        diff |= w.hi[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, vout + 32u, so, 0);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b32(w.lo[j], out_rsrc, vout, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(w.hi[j], out_rsrc, vout + 32u, so, 0);
+      }
+    }
+    if (diff) a.redo[sv] = 1;
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 32; j++) {
+    const uint32_t so = (uint32_t)(64 * q_st + s_local(j, 0)) * (uint32_t)a.out_shard_stride;
+    __builtin_amdgcn_raw_buffer_store_b32(w.lo[j], out_rsrc, vout, so, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(w.hi[j], out_rsrc, vout + 32u, so, 0);
+  }
+}
+
 // Tables are module globals: upload once per device.
 std::mutex g_tab_mu;
 bool g_tab_done[64];
@@ -1944,6 +2087,16 @@ static bool enc32_waves(int k) {
   return k == 512;
 }
 
+// k = 512 encoder: the half-lane kernel (round 5); DAGPU_GF16_ENCH=0 selects
+// leo16_encode_reg32_kernel (A/B)
+static bool ench_on() {
+  static const bool v = [] {
+    const char* e = getenv("DAGPU_GF16_ENCH");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 hipError_t launch_leo16_encode(int k, const EncodeArgs& a, hipStream_t s) {
   if (use_wide(k)) return launch_leo16w_encode(k, a, s);
   if (!gf16_k_ok(k) || a.shard_bytes % 64) return hipErrorInvalidValue;
@@ -1956,7 +2109,12 @@ hipError_t launch_leo16_encode(int k, const EncodeArgs& a, hipStream_t s) {
     b.nchunk = (a.shard_bytes + 511) / 512;
     const long blocks = b.nsq * b.nvec * b.nchunk;
     if (blocks <= 0) return hipSuccess;
-    if (enc32_waves(k)) {
+    if (k == 512 && ench_on()) {  // half-lane kernel, 256-B pieces
+      b.nchunk = (a.shard_bytes + 255) / 256;
+      const long hb = b.nsq * b.nvec * b.nchunk;
+      if (a.reverse) hipLaunchKernelGGL((leo16_encode_h_kernel<true>), dim3((unsigned)hb), dim3(kEncH), 0, s, b);
+      else hipLaunchKernelGGL((leo16_encode_h_kernel<false>), dim3((unsigned)hb), dim3(kEncH), 0, s, b);
+    } else if (enc32_waves(k)) {
       if (k == 256) {
         constexpr int L = enc32_lds_bytes<256>();
         if (a.reverse) hipLaunchKernelGGL((leo16_encode_reg32_kernel<256, true>), dim3((unsigned)blocks), dim3(512), L, s, b);
