@@ -1548,11 +1548,14 @@ __device__ __forceinline__ void swap_sb(W32& w) {
 }
 
 // a skew position's 3/3/2 table into VGPRs (pos differs between the halves)
+// (buffer loads: one 32-bit offset per lane instead of a 64-bit address)
 __device__ __forceinline__ void lane_tab(int pos, uint32_t (&t)[kTab16x]) {
-  const uint4* p = (const uint4*)(g_ptab16x + pos * kTab16x);
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const auto r = make_rsrc(g_ptab16x);
+  const uint32_t off = (uint32_t)pos * (uint32_t)(kTab16x * 4);
 #pragma unroll
   for (int i = 0; i < kTab16x / 4; i++) {
-    const uint4 v = p[i];
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off + 16u * i, 0, 0);
     t[4 * i] = v.x;
     t[4 * i + 1] = v.y;
     t[4 * i + 2] = v.z;

@@ -22,8 +22,8 @@ case "$1" in
     timeout -k 10 900 python -u -m pytest -x -v -s --timeout 400 --timeout-method thread tests/test_gpu_gf16.py tests/test_gpu_repair_async.py tests/test_gpu_wide.py tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py > gpurun_out/r05_first_tests.log 2>&1
     rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r05_first_tests.log; [ $rc -eq 0 ] || exit $rc
     bash tools/gpu_ab.sh --rounds 2 repair512 new= packed=DAGPU_DEC1K_PACKED=1 prev=lib:celestia-app_amd/libdagpu_prev.so && \
-    bash tools/gpu_ab.sh --rounds 2 split512 new= prev=lib:celestia-app_amd/libdagpu_prev.so && \
-    bash tools/gpu_ab.sh --rounds 1 repair512q3 new= prev=lib:celestia-app_amd/libdagpu_prev.so && \
+    bash tools/gpu_ab.sh --rounds 2 split512 new= reg32=DAGPU_GF16_ENCH=0 prev=lib:celestia-app_amd/libdagpu_prev.so && \
+    bash tools/gpu_ab.sh --rounds 1 repair512q3 new= reg32=DAGPU_GF16_ENCH=0 prev=lib:celestia-app_amd/libdagpu_prev.so && \
     bash tools/gpu_pmc_gf16.sh repair512 split512
     ;;
   *) echo "steps: base mul332 first"; exit 2;;
