@@ -1,0 +1,282 @@
+"""Host emulation of the round-5 half-lane GF(2^16) kernels' data movement
+(csrc/rs_gf16.hip leo16_decode_h1k_kernel, k = 512 decode over n = 1024
+elements, and leo16_encode_h_kernel, k = 512 encode over m = 512): the same
+layouts S / B / T (two elements per register, one per half wave), the
+permlane32 swap S <-> B, the LDS transpose B <-> T, the skew position of
+every butterfly, the closed-form formal derivative with its half-bit term and
+the merged last-IFFT / first-FFT encoder layer -- on one symbol column, against
+the plain Leopard loops (klauspost/reedsolomon v1.11.8 leopard.go
+ifftDITDecoder / ifftDITEncoder, formalDerivative, fftDIT; SURVEY.md Appendix
+A.5-A.6).  The field arithmetic is the same on every symbol column, so one
+column pins the index mapping; the kernels themselves are checked bit-exact
+against the oracle on the GPU (tests/test_gpu_gf16.py)."""
+import numpy as np
+import pytest
+
+MOD = 65535
+
+
+def _tables():
+    # leopard.go initLUTs / initFFTSkew for GF(2^16) (as csrc/gf16_host.hpp)
+    cantor = [0x0001, 0xACCA, 0x3C0E, 0x163E, 0xC582, 0xED2E, 0x914C, 0x4012,
+              0x6C98, 0x10D8, 0x6A72, 0xB900, 0xFDB8, 0xFB34, 0xFF38, 0x991E]
+    exp = np.zeros(65536, np.int64)
+    log = np.zeros(65536, np.int64)
+    state = 1
+    for i in range(MOD):
+        exp[state] = i
+        state <<= 1
+        if state >= 65536:
+            state ^= 0x1002D
+    exp[0] = MOD
+    log[0] = 0
+    for i in range(16):
+        width = 1 << i
+        log[width:2 * width] = log[:width] ^ cantor[i]
+    log = exp[log]
+    exp2 = np.zeros(65536, np.int64)
+    exp2[log] = np.arange(65536)
+    exp2[MOD] = exp2[0]
+    exp = exp2
+
+    def add_mod(a, b):
+        s = a + b
+        return (s + (s >> 16)) & 0xFFFF
+
+    def mullog(a, lb):
+        return 0 if a == 0 else int(exp[add_mod(int(log[a]), lb)])
+
+    skew = np.zeros(65536, np.int64)
+    temp = [1 << i for i in range(1, 16)]
+    for m in range(15):
+        step = 1 << (m + 1)
+        skew[(1 << m) - 1] = 0
+        for i in range(m, 15):
+            s = 1 << (i + 1)
+            for j in range((1 << m) - 1, s, step):
+                skew[j + s] = skew[j] ^ temp[i]
+        temp[m] = MOD - int(log[mullog(temp[m], int(log[temp[m] ^ 1]))])
+        for i in range(m + 1, 15):
+            temp[i] = mullog(temp[i], add_mod(int(log[temp[i] ^ 1]), temp[m]))
+    skew[:MOD] = log[skew[:MOD]]
+    return log, exp, skew
+
+
+LOG, EXP, SKEW = _tables()
+
+
+def mul(a: int, lm: int) -> int:
+    if a == 0:
+        return 0
+    s = int(LOG[a]) + lm
+    return int(EXP[(s + (s >> 16)) & 0xFFFF])
+
+
+def bfly(w, i, j, pos, inv):
+    lm = int(SKEW[pos])
+    if inv:  # ifftDIT2: y ^= x; x ^= y * skew
+        w[j] ^= w[i]
+        if lm != MOD:
+            w[i] ^= mul(w[j], lm)
+    else:  # fftDIT2: x ^= y * skew; y ^= x
+        if lm != MOD:
+            w[i] ^= mul(w[j], lm)
+        w[j] ^= w[i]
+
+
+def ref_ifft(w, off):
+    """ifftDITDecoder (off = 0) / ifftDITEncoder (off = m), radix-2 layers:
+    butterfly (e, e + d) at skew index off + block start + d - 1."""
+    n = len(w)
+    d = 1
+    while d < n:
+        for r in range(0, n, 2 * d):
+            for i in range(r, r + d):
+                bfly(w, i, i + d, off + r + d - 1, True)
+        d *= 2
+
+
+def ref_fft(w, off):
+    n = len(w)
+    d = n // 2
+    while d >= 1:
+        for r in range(0, n, 2 * d):
+            for i in range(r, r + d):
+                bfly(w, i, i + d, off + r + d - 1, False)
+        d //= 2
+
+
+def ref_derivative(w):  # leopard.go formalDerivative
+    n = len(w)
+    for i in range(1, n):
+        width = ((i ^ (i - 1)) + 1) >> 1
+        for t in range(width):
+            w[i - width + t] ^= w[i + t]
+
+
+# --- the half-lane kernels' layouts: R[q][j][hl] ---
+def e_s(q, j, hl):
+    return 64 * q + 2 * (j & 15) + (j >> 4) + 32 * hl
+
+
+def e_b(q, j, hl):
+    return 64 * q + 2 * j + hl
+
+
+def e_t(q, j, hl, lr):
+    return hl | (j & ((1 << lr) - 1)) << 1 | q << (lr + 1) | (j >> lr) << 6
+
+
+def swap_sb(R):
+    for reg in R:
+        for j in range(16):
+            a, b = reg[j], reg[j + 16]
+            reg[j], reg[j + 16] = [a[0], b[0]], [a[1], b[1]]
+
+
+def xpose_bt(R, lr):
+    nq = len(R)
+    S = [[[None, None] for _ in range(32)] for _ in range(nq)]
+    for q in range(nq):
+        for jj in range(nq):
+            for r in range(1 << lr):
+                S[jj][(q << lr) | r] = list(R[q][(jj << lr) | r])
+    return S
+
+
+def layer0_s(R, off, inv):
+    for q, reg in enumerate(R):
+        for j in range(16):
+            for hl in range(2):
+                pos = off + 64 * q + 2 * j + 32 * hl
+                w = [reg[j][hl], reg[j + 16][hl]]
+                bfly(w, 0, 1, pos, inv)
+                reg[j][hl], reg[j + 16][hl] = w
+
+
+def layer_b(R, d, off, inv):
+    rd = d // 2
+    for q, reg in enumerate(R):
+        for r in range(0, 64, 2 * d):
+            pos = off + 64 * q + r + d - 1
+            for e in range(r, r + d, 2):
+                for hl in range(2):
+                    w = [reg[e // 2][hl], reg[e // 2 + rd][hl]]
+                    bfly(w, 0, 1, pos, inv)
+                    reg[e // 2][hl], reg[e // 2 + rd][hl] = w
+
+
+def layer_t(R, d, lr, off, inv):
+    rd = (d // 64) << lr
+    n = 64 << (5 - lr)
+    for reg in R:
+        for blk in range(0, n, 2 * d):
+            for j in range(32):
+                if j & rd or (((j >> lr) << 6) & ~(2 * d - 1)) != blk:
+                    continue
+                for hl in range(2):
+                    w = [reg[j][hl], reg[j + rd][hl]]
+                    bfly(w, 0, 1, off + blk + d - 1, inv)
+                    reg[j][hl], reg[j + rd][hl] = w
+
+
+def derivative_t(R):
+    orig = [[list(x) for x in reg] for reg in R]
+    for c, reg in enumerate(R):
+        for j in range(32):
+            for hl in range(2):
+                acc = orig[c][j][hl]
+                for bit in (1, 2, 4, 8, 16):
+                    if not j & bit:
+                        acc ^= orig[c][j | bit][hl]
+                for wb in (1, 2, 4, 8):
+                    if not c & wb:
+                        acc ^= orig[c | wb][j][hl]
+                if hl == 0:
+                    acc ^= orig[c][j][1]
+                reg[j][hl] = acc
+
+
+def gather(R, f):
+    out = {}
+    for q, reg in enumerate(R):
+        for j in range(32):
+            for hl in range(2):
+                out[f(q, j, hl)] = reg[j][hl]
+    return [out[e] for e in range(len(out))]
+
+
+def test_layout_maps_are_bijections():
+    for nq, lr in ((16, 1), (8, 2)):
+        n = 64 * nq
+        for f in (e_s, e_b, lambda q, j, hl: e_t(q, j, hl, lr)):
+            es = {f(q, j, hl) for q in range(nq) for j in range(32) for hl in range(2)}
+            assert es == set(range(n))
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_halflane_decoder_equals_leopard_loops(seed):
+    rng = np.random.default_rng(seed)
+    n = 1024
+    x = [int(v) for v in rng.integers(0, 65536, n)]
+    ref = list(x)
+    ref_ifft(ref, 0)
+    ref_derivative(ref)
+    ref_fft(ref, 0)
+    # kernel order: load in S, IFFT bit 0 in S, swap to B, bits 1-5, transpose
+    # to T, bits 6-9, derivative, FFT 9-6, transpose, 5-1, swap, bit 0
+    R = [[[x[e_s(q, j, 0)], x[e_s(q, j, 1)]] for j in range(32)] for q in range(16)]
+    layer0_s(R, 0, True)
+    swap_sb(R)
+    assert gather(R, e_b) == gather(R, e_b)  # (layout B now)
+    for d in (2, 4, 8, 16, 32):
+        layer_b(R, d, 0, True)
+    R = xpose_bt(R, 1)
+    for d in (64, 128, 256, 512):
+        layer_t(R, d, 1, 0, True)
+    derivative_t(R)
+    for d in (512, 256, 128, 64):
+        layer_t(R, d, 1, 0, False)
+    R = xpose_bt(R, 1)
+    for d in (32, 16, 8, 4, 2):
+        layer_b(R, d, 0, False)
+    swap_sb(R)
+    layer0_s(R, 0, False)
+    assert gather(R, e_s) == ref
+
+
+@pytest.mark.parametrize("rev", [False, True])
+def test_halflane_encoder_equals_leopard_loops(rev):
+    rng = np.random.default_rng(7 + rev)
+    m = 512
+    io, fo = (0, m) if rev else (m, 0)
+    x = [int(v) for v in rng.integers(0, 65536, m)]
+    ref = list(x)
+    ref_ifft(ref, io)
+    ref_fft(ref, fo)
+    R = [[[x[e_s(q, j, 0)], x[e_s(q, j, 1)]] for j in range(32)] for q in range(8)]
+    layer0_s(R, io, True)
+    swap_sb(R)
+    for d in (2, 4, 8, 16, 32):
+        layer_b(R, d, io, True)
+    R = xpose_bt(R, 2)
+    for d in (64, 128):
+        layer_t(R, d, 2, io, True)
+    # merged dist-256 layers (registers j, j + 16 in T): y ^= x; x ^= y (A ^ B); y ^= x
+    a, b = int(SKEW[io + 255]), int(SKEW[fo + 255])
+    for reg in R:
+        for j in range(16):
+            for hl in range(2):
+                xx, yy = reg[j][hl], reg[j + 16][hl]
+                yy ^= xx
+                xx ^= (mul(yy, a) if a != MOD else 0) ^ (mul(yy, b) if b != MOD else 0)
+                yy ^= xx
+                reg[j][hl], reg[j + 16][hl] = xx, yy
+    for d in (128, 64):
+        layer_t(R, d, 2, fo, False)
+    R = xpose_bt(R, 2)
+    for d in (32, 16, 8, 4, 2):
+        layer_b(R, d, fo, False)
+    swap_sb(R)
+    layer0_s(R, fo, False)
+    assert gather(R, e_s) == ref
