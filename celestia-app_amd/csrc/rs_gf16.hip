@@ -2092,12 +2092,9 @@ static bool enc32_waves(int k) {
 
 // k = 512 encoder: the half-lane kernel (round 5); DAGPU_GF16_ENCH=0 selects
 // leo16_encode_reg32_kernel (A/B)
-static bool ench_on() {
-  static const bool v = [] {
-    const char* e = getenv("DAGPU_GF16_ENCH");
-    return !(e && e[0] == '0');
-  }();
-  return v;
+static bool ench_on() {  // read per launch: the tests switch it in-process
+  const char* e = getenv("DAGPU_GF16_ENCH");
+  return !(e && e[0] == '0');
 }
 
 hipError_t launch_leo16_encode(int k, const EncodeArgs& a, hipStream_t s) {
@@ -2182,12 +2179,9 @@ static hipError_t dec_lds_attr() {  // above the 64 KiB default: once per proces
 
 // k = 512 decoder: the half-lane unpacked kernel (round 5); DAGPU_DEC1K_PACKED=1
 // selects the packed one of rounds 2-4 (A/B)
-static bool dec1k_packed() {
-  static const bool v = [] {
-    const char* e = getenv("DAGPU_DEC1K_PACKED");
-    return e && e[0] == '1';
-  }();
-  return v;
+static bool dec1k_packed() {  // read per launch: the tests switch it in-process
+  const char* e = getenv("DAGPU_DEC1K_PACKED");
+  return e && e[0] == '1';
 }
 
 hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mark_present) {

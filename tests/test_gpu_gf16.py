@@ -22,7 +22,7 @@ def ctx():
 
 
 @pytest.mark.parametrize("k", [256, 512])
-@pytest.mark.parametrize("shard", [64, 512, 1536])
+@pytest.mark.parametrize("shard", [64, 320, 512, 1536])
 def test_gf16_encode_matches_oracle(ctx, k, shard):
     rng = np.random.default_rng(k + shard)
     data = rng.integers(0, 256, (2, k, shard), dtype=np.uint8)
@@ -137,3 +137,41 @@ def test_gf16_repair_max_erasure(ctx, k):
     bad[r, c, 100] ^= 1
     with pytest.raises(da.ErrByzantineData):
         da.repair(bad, present, rr, cr, ctx)
+
+
+@pytest.mark.parametrize("shard", [64, 256, 1536])
+def test_k512_encoders_agree(ctx, shard, monkeypatch):
+    """Round 5: the half-lane k = 512 encoder (two workgroups per CU, 256-B
+    pieces) byte-equal to the 16-wave register encoder (DAGPU_GF16_ENCH=0),
+    plain and as the reverse transform, and to the oracle."""
+    k = 512
+    rng = np.random.default_rng(3 * shard)
+    data = rng.integers(0, 256, (3, k, shard), dtype=np.uint8)
+    codec = da.LeoRSCodec(ctx)
+    half = codec.encode_batch(data)
+    monkeypatch.setenv("DAGPU_GF16_ENCH", "0")
+    reg = codec.encode_batch(data)
+    assert (half == reg).all()
+    assert (half[0] == oracle.encode(data[0])).all()
+
+
+@pytest.mark.parametrize("shard", [256, 512])
+def test_k512_decoders_agree(ctx, shard, monkeypatch):
+    """Round 5: the half-lane unpacked k = 512 decoder byte-equal to the packed
+    one of rounds 2-4 (DAGPU_DEC1K_PACKED=1) on random, data-half and
+    parity-half erasures."""
+    k = 512
+    rng = np.random.default_rng(11 + shard)
+    data = rng.integers(0, 256, (k, shard), dtype=np.uint8)
+    full = np.concatenate([data, oracle.encode(data)])
+    codec = da.LeoRSCodec(ctx)
+    pats = [set(rng.choice(2 * k, k, replace=False).tolist()), set(range(k)), set(range(k, 2 * k)),
+            set(rng.choice(2 * k, k + 77, replace=False).tolist())]
+    for keep in pats:
+        shards = [full[i].tobytes() if i in keep else None for i in range(2 * k)]
+        new = codec.decode(shards)
+        monkeypatch.setenv("DAGPU_DEC1K_PACKED", "1")
+        old = codec.decode(shards)
+        monkeypatch.delenv("DAGPU_DEC1K_PACKED")
+        assert new == old
+        assert b"".join(new) == full.tobytes()

@@ -10,7 +10,7 @@ if [ "$MODE" = full ]; then
   cat $OUT/valu_bench_$TAG.log
 fi
 export DAGPU_PIPE_SLICES=1  # one launch per kernel per step: clean per-launch counters
-BENCH="bench.py --steps 5 --warmup 1 --no-cpu --no-e2e --no-replay --no-configs --distinct 16"
+BENCH="bench.py --steps 5 --warmup 1 --no-cpu --no-e2e --no-replay --no-configs --no-check --distinct 16"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_$TAG -o run -- python3 $BENCH > $OUT/trace_$TAG.log 2>&1 || { echo "trace failed"; tail -20 $OUT/trace_$TAG.log; exit 1; }
 echo "trace ok"
 for P in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
