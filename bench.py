@@ -255,6 +255,21 @@ def load_stress_pmc(kernel: str):
         return None
 
 
+def gf16_kernel_names(k: int):
+    """(forward encoder, decoder) kernel names the library runs at width k
+    (csrc/rs_gf16.hip launch selection, its A/B switches included), as
+    rocprofv3 / tools/pmc_stress.py name them."""
+    if k == 512:
+        enc = ("leo16_encode_reg32_kernel<512, false>" if os.environ.get("DAGPU_GF16_ENCH") == "0"
+               else "leo16_encode_h_kernel<false>")
+        dec = ("leo16_decode_reg1k_kernel" if os.environ.get("DAGPU_DEC1K_PACKED") == "1"
+               else "leo16_decode_h1k_kernel")
+        return enc, dec
+    if k == 256:
+        return "leo16_encode_reg_kernel<256, false>", "leo16_decode_reg_kernel"
+    return f"leo16w encode k={k}", f"leo16w decode k={k}"
+
+
 def stress_roofline(kernel: str, alg_bytes: float, ms: float, launches: int, pmc_name: str, work: str):
     """Roofline entry of a stress line's dominant kernel: algorithmic bytes per
     launch over its average launch time (HIP events of the library's profiled
@@ -885,7 +900,7 @@ def bench_split(dist, rank, world, local, ctx, k, steps, warmup):
     L.dagpu_profile_read(ctx.handle, _abi.addr(tot), _abi.addr(cnt), 1)
     prof = {n: float(tot[i]) for i, n in enumerate(_abi.PROFILE_KERNELS) if cnt[i]}
     # this rank's column pass: 2k/P column vectors, each k shards read + k written
-    enc = {512: "leo16_encode_reg32_kernel<512, false>", 256: "leo16_encode_reg_kernel<256, false>"}.get(k)
+    enc = gf16_kernel_names(k)[0]
     roof = stress_roofline("rs_col (GF(2^16) column encode)", (2 * k // world) * 2 * k * SHARE,
                            prof.get("rs_col"), int(cnt[1]), enc or f"leo16 encode k={k}",
                            f"{2 * k // world} column vectors x (k read + k written) x 512 B") if cnt[1] else None
@@ -1121,8 +1136,7 @@ def run_repair(ctx, k, B, steps, warmup, distinct=None, pattern="subgrid", slice
     prof = {"decode_ms": float(tot[idec]), "decode_launches": int(cnt[idec]),
             "fill_ms": float(tot[ifil]), "fill_launches": int(cnt[ifil]), "schedule": sched}
     # a decoded vector reads its k given shards and writes its k missing ones
-    dec_name = {128: "leo8_decode128_sliced_kernel", 256: "leo16_decode_reg_kernel",
-                512: "leo16_decode_reg1k_kernel"}.get(k, f"decoder k={k}")
+    dec_name = "leo8_decode128_sliced_kernel" if k == 128 else gf16_kernel_names(k)[1]
     roof = stress_roofline(f"decode ({dec_name})", sched["decodes"] * 2 * k * SHARE, prof["decode_ms"],
                            prof["decode_launches"], dec_name,
                            f"{sched['decodes']} decoded vectors x (k read + k written) x 512 B") \
