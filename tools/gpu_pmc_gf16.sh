@@ -13,6 +13,8 @@ for wl in "$@"; do
     repair256) A="--mode repair --k 256 --batch 8 --steps 3 --warmup 1";;
     split512) A="--mode split --split-k 512 --steps 3 --warmup 1";;
     repair128) A="--mode repair --k 128 --batch 256 --steps 3 --warmup 1";;
+    split1024) A="--mode split --split-k 1024 --steps 3 --warmup 1";;
+    repair1024) A="--mode repair --k 1024 --batch 1 --steps 2 --warmup 1";;
     *) echo "unknown $wl"; exit 2;;
   esac
   B="$GRAFT_REPO_ROOT/bench.py $A"

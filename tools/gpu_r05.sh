@@ -26,5 +26,12 @@ case "$1" in
     bash tools/gpu_ab.sh --rounds 1 repair512q3 new= reg32=DAGPU_GF16_ENCH=0 prev=lib:celestia-app_amd/libdagpu_prev.so && \
     bash tools/gpu_pmc_gf16.sh repair512 split512
     ;;
-  *) echo "steps: base mul332 first"; exit 2;;
+  final-a)  # round end, part 1: the whole -m gpu suite, the default bench line and its rocprofv3 kernel trace
+    bash tools/gpu_final.sh
+    ;;
+  final-b)  # round end, part 2: headline counters (kernel stats + FETCH/WRITE/SQ/GRBM passes, --no-check) and the stress / wide counters
+    bash tools/gpu_profile.sh r05 counters && \
+    bash tools/gpu_pmc_gf16.sh repair512 repair512q3 split512 repair128 split1024 repair1024
+    ;;
+  *) echo "steps: base mul332 first final-a final-b"; exit 2;;
 esac

@@ -14,7 +14,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KEEP = ("leo16", "errloc", "decode128", "leo8_encode_sliced2", "repair_plan")
+KEEP = ("leo16", "errloc", "decode128", "leo8_encode_sliced2", "repair_plan", "leo16w")
 
 
 def kname(n: str) -> str:
