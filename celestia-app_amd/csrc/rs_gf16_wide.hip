@@ -44,7 +44,7 @@ constexpr int kPtabPos = 2 * kMaxK;  // skew positions used by any transform <= 
 struct WideTabs {
   const uint16_t* log;
   const uint16_t* exp;
-  const uint32_t* ptab;   // kPtabPos x 16 dwords
+  const uint32_t* ptab;   // kPtabPos x kTabW dwords
   const uint16_t* wfold;  // folded Walsh weights, n = 2048 .. 2 kMaxK, back to back
 };
 
@@ -53,27 +53,30 @@ __device__ __forceinline__ uint32_t xor3w(uint32_t a, uint32_t b, uint32_t c) {
 }
 
 // x ^= y * skew[pos] for 4 symbols (lo / hi byte dwords) with the position's
-// product table t[16] (rs_gf16.hip mul16_add, table from registers)
+// product table t[kTabW] in registers: the 3/3/2 bit split of rs_gf16.hip
+// mul16x_add_t (round 5; 12 v_perm per 4 symbols instead of 16).  Table:
+// [0,1] / [2,3] group 0 (y bits 0-2) -> product lo / hi byte, [4..7] group 1
+// (bits 3-5), [8] / [9] group 2 (bits 6-7), [10..13] group 3 (bits 8-10),
+// [14..17] group 4 (bits 11-13), [18] / [19] group 5 (bits 14-15).
+constexpr int kTabW = 20;
 __device__ __forceinline__ void pmul_add(uint32_t& xlo, uint32_t& xhi, uint32_t ylo, uint32_t yhi,
-                                         const uint32_t (&t)[16]) {
-  uint32_t pl[8], ph[8];
-#pragma unroll
-  for (int g = 0; g < 4; g++) {
-    const uint32_t sl = (ylo >> (2 * g)) & 0x03030303u;
-    const uint32_t sh = (yhi >> (2 * g)) & 0x03030303u;
-    pl[g] = __builtin_amdgcn_perm(t[g], t[g], sl);
-    ph[g] = __builtin_amdgcn_perm(t[8 + g], t[8 + g], sl);
-    pl[4 + g] = __builtin_amdgcn_perm(t[4 + g], t[4 + g], sh);
-    ph[4 + g] = __builtin_amdgcn_perm(t[12 + g], t[12 + g], sh);
-  }
-  xlo = xor3w(xor3w(xor3w(xlo, pl[0], pl[1]), xor3w(pl[2], pl[3], pl[4]), pl[5]), pl[6], pl[7]);
-  xhi = xor3w(xor3w(xor3w(xhi, ph[0], ph[1]), xor3w(ph[2], ph[3], ph[4]), ph[5]), ph[6], ph[7]);
+                                         const uint32_t (&t)[kTabW]) {
+  const uint32_t s0 = ylo & 0x07070707u, s1 = (ylo >> 3) & 0x07070707u, s2 = (ylo >> 6) & 0x03030303u;
+  const uint32_t s3 = yhi & 0x07070707u, s4 = (yhi >> 3) & 0x07070707u, s5 = (yhi >> 6) & 0x03030303u;
+  const uint32_t l0 = __builtin_amdgcn_perm(t[1], t[0], s0), h0 = __builtin_amdgcn_perm(t[3], t[2], s0);
+  const uint32_t l1 = __builtin_amdgcn_perm(t[5], t[4], s1), h1 = __builtin_amdgcn_perm(t[7], t[6], s1);
+  const uint32_t l2 = __builtin_amdgcn_perm(t[8], t[8], s2), h2 = __builtin_amdgcn_perm(t[9], t[9], s2);
+  const uint32_t l3 = __builtin_amdgcn_perm(t[11], t[10], s3), h3 = __builtin_amdgcn_perm(t[13], t[12], s3);
+  const uint32_t l4 = __builtin_amdgcn_perm(t[15], t[14], s4), h4 = __builtin_amdgcn_perm(t[17], t[16], s4);
+  const uint32_t l5 = __builtin_amdgcn_perm(t[18], t[18], s5), h5 = __builtin_amdgcn_perm(t[19], t[19], s5);
+  xlo = xor3w(xor3w(xor3w(xlo, l0, l1), l2, l3), l4, l5);
+  xhi = xor3w(xor3w(xor3w(xhi, h0, h1), h2, h3), h4, h5);
 }
 
-__device__ __forceinline__ void load_tab(const WideTabs& T, int pos, uint32_t (&t)[16]) {
-  const uint4* p = (const uint4*)(T.ptab + (long)pos * 16);
+__device__ __forceinline__ void load_tab(const WideTabs& T, int pos, uint32_t (&t)[kTabW]) {
+  const uint4* p = (const uint4*)(T.ptab + (long)pos * kTabW);
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
+  for (int i = 0; i < kTabW / 4; i++) {
     const uint4 v = p[i];
     t[4 * i] = v.x;
     t[4 * i + 1] = v.y;
@@ -137,7 +140,7 @@ struct Unit {
       }
   }
   // ifftDIT2: y ^= x; x ^= y * skew
-  __device__ __forceinline__ void ifft2(int i, int j, const uint32_t (&t)[16]) {
+  __device__ __forceinline__ void ifft2(int i, int j, const uint32_t (&t)[kTabW]) {
 #pragma unroll
     for (int g = 0; g < G; g++) {
       lo[j][g] ^= lo[i][g];
@@ -146,7 +149,7 @@ struct Unit {
     }
   }
   // fftDIT2: x ^= y * skew; y ^= x
-  __device__ __forceinline__ void fft2(int i, int j, const uint32_t (&t)[16]) {
+  __device__ __forceinline__ void fft2(int i, int j, const uint32_t (&t)[kTabW]) {
 #pragma unroll
     for (int g = 0; g < G; g++) {
       pmul_add(lo[i][g], hi[i][g], lo[j][g], hi[j][g], t);
@@ -162,7 +165,7 @@ template <int NG, int G>
 __device__ void wide_ifft(const Planes<NG>& P, const WideTabs& T, int n, int base) {
   constexpr int CH = NG / G;
   int dist = 1, dist4 = 4;
-  uint32_t t[16];
+  uint32_t t[kTabW];
   while (dist4 <= n) {
     const int units = (n / 4) * CH;
     for (int u = threadIdx.x; u < units; u += kWideThreads) {
@@ -204,7 +207,7 @@ template <int NG, int G>
 __device__ void wide_fft(const Planes<NG>& P, const WideTabs& T, int n, int fo) {
   constexpr int CH = NG / G;
   int dist4 = n, dist = n >> 2;
-  uint32_t t[16];
+  uint32_t t[kTabW];
   while (dist != 0) {
     const int units = (n / 4) * CH;
     for (int u = threadIdx.x; u < units; u += kWideThreads) {
@@ -516,22 +519,23 @@ hipError_t tables(WideTabs& out) {
     return hipSuccess;
   }
   static const gf16::Tables t = gf16::make_tables();
-  std::vector<uint32_t> pt((size_t)kPtabPos * 16, 0u);
+  std::vector<uint32_t> pt((size_t)kPtabPos * kTabW, 0u);
   for (int pos = 0; pos < kPtabPos; pos++) {
     const unsigned lm = t.skew[pos];
     if (lm == kMod) continue;  // leopard skips the multiply: zero table
-    for (int g = 0; g < 8; g++)
-      for (int e2 = 0; e2 < 4; e2++) {
-        const unsigned x = (unsigned)e2 << (2 * g);
-        unsigned prod = 0;
-        if (x) {
-          unsigned s = (unsigned)t.log[x] + lm;
-          s = (s + (s >> 16)) & 0xFFFFu;
-          prod = t.exp[s];
-        }
-        const int lo_idx = g, hi_idx = 8 + g;  // (g < 4: low-byte groups, g >= 4: high-byte groups)
-        pt[(size_t)pos * 16 + lo_idx] |= (prod & 0xFFu) << (8 * e2);
-        pt[(size_t)pos * 16 + hi_idx] |= ((prod >> 8) & 0xFFu) << (8 * e2);
+    static const int shift[6] = {0, 3, 6, 8, 11, 14}, width[6] = {3, 3, 2, 3, 3, 2};
+    static const int base[6] = {0, 4, 8, 10, 14, 18};
+    uint32_t* o = pt.data() + (size_t)pos * kTabW;
+    for (int g = 0; g < 6; g++)
+      for (int e2 = 1; e2 < (1 << width[g]); e2++) {
+        const unsigned x = (unsigned)e2 << shift[g];
+        unsigned s = (unsigned)t.log[x] + lm;
+        s = (s + (s >> 16)) & 0xFFFFu;
+        const unsigned prod = t.exp[s];
+        const int lo_dw = width[g] == 3 ? base[g] + (e2 >> 2) : base[g];
+        const int hi_dw = width[g] == 3 ? base[g] + 2 + (e2 >> 2) : base[g] + 1;
+        o[lo_dw] |= (prod & 0xFFu) << (8 * (e2 & 3));
+        o[hi_dw] |= ((prod >> 8) & 0xFFu) << (8 * (e2 & 3));
       }
   }
   std::vector<uint16_t> wf((size_t)wfold_offset(2 * 2 * kMaxK), 0);
