@@ -261,12 +261,16 @@ def gf16_kernel_names(k: int):
     rocprofv3 / tools/pmc_stress.py name them."""
     if k == 512:
         enc = ("leo16_encode_reg32_kernel<512, false>" if os.environ.get("DAGPU_GF16_ENCH") == "0"
-               else "leo16_encode_h_kernel<false>")
+               else "leo16_encode_h_kernel<512, false>")
         dec = ("leo16_decode_reg1k_kernel" if os.environ.get("DAGPU_DEC1K_PACKED") == "1"
-               else "leo16_decode_h1k_kernel")
+               else "leo16_decode_h_kernel<512>")
         return enc, dec
     if k == 256:
-        return "leo16_encode_reg_kernel<256, false>", "leo16_decode_reg_kernel"
+        enc = ("leo16_encode_reg_kernel<256, false>" if os.environ.get("DAGPU_GF16_ENCH") == "0"
+               else "leo16_encode_h_kernel<256, false>")
+        dec = ("leo16_decode_reg_kernel" if os.environ.get("DAGPU_DEC256_REG") == "1"
+               else "leo16_decode_h_kernel<256>")
+        return enc, dec
     return f"leo16w encode k={k}", f"leo16w decode k={k}"
 
 

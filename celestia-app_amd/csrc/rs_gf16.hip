@@ -1505,7 +1505,7 @@ __global__ __launch_bounds__(kDec1k) __attribute__((amdgpu_waves_per_eu(4, 4))) 
 }
 
 // ---------------------------------------------------------------------------
-// k = 512 decoder, round 5 (leo16_decode_h1k_kernel): unpacked symbols with
+// k = 512 / 256 decoder, round 5 (leo16_decode_h_kernel<K>): unpacked symbols with
 // the 3/3/2 multiply (mul16x_add_t, 28 ops per 4 symbols) instead of the
 // packed 2-bit one (22 ops per 2 symbols).  Unpacked, a lane holds 4 symbols of
 // an element in 2 VGPRs, so 1,024 elements x 64 lanes would need the CU's
@@ -1528,7 +1528,6 @@ __global__ __launch_bounds__(kDec1k) __attribute__((amdgpu_waves_per_eu(4, 4))) 
 // from SGPRs).  Pre/post multiplies: the decoders' 16-dword LDS tables
 // (mul16_table_to), read per lane.
 // ---------------------------------------------------------------------------
-constexpr int kDecH = 1024;
 using W32 = W16n<32>;
 
 // e of register j, lane half hl, in layout S (within the wave's 64 elements)
@@ -1672,9 +1671,10 @@ __device__ __forceinline__ void xpose_bt(W32& w, uint32_t* lds, int q, int lane)
 }
 
 // Formal derivative in layout T, D(x)_e = x_e ^ XOR_{s: bit s of e = 0} x_{e | 2^s}:
-// register bits (element bits 1, 6-9) in place in ascending register order,
-// wave bits (2-5) and the half bit (0, lanes 0-31 read lane + 32) from the
-// originals staged in LDS, 8 register pairs per round.
+// register bits (element bits 1..LR and 6..) in place in ascending register
+// order, wave bits (LR+1 .. 5) and the half bit (0, lanes 0-31 read lane + 32)
+// from the originals staged in LDS, 8 register pairs per round (NQ waves).
+template <int NQ>
 __device__ __forceinline__ void derivative_t(W32& w, uint32_t* lds, int c, int lane, uint32_t lowmask) {
   constexpr int B = 8;
 #pragma unroll
@@ -1696,7 +1696,7 @@ __device__ __forceinline__ void derivative_t(W32& w, uint32_t* lds, int c, int l
           ahi ^= w.hi[j | bit];
         }
 #pragma unroll
-      for (int wb = 1; wb < 16; wb <<= 1)
+      for (int wb = 1; wb < NQ; wb <<= 1)
         if ((c & wb) == 0) {
           alo ^= lds[(((c | wb) * B + u) * 2) * 64 + lane];
           ahi ^= lds[(((c | wb) * B + u) * 2 + 1) * 64 + lane];
@@ -1712,14 +1712,20 @@ __device__ __forceinline__ void derivative_t(W32& w, uint32_t* lds, int c, int l
   }
 }
 
-__global__ __launch_bounds__(kDecH) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_decode_h1k_kernel(
+// K = 512 (n = 1024, 16 waves, LR = 1) and, round 5, K = 256 (n = 512, 8 waves,
+// LR = 2: 512 threads at <= 128 VGPRs and 64 KiB of LDS, two workgroups per CU).
+template <int K>
+constexpr size_t dec_h_lds_bytes() { return (size_t)2 * (2 * K) * 16 * sizeof(uint32_t); }
+template <int K>
+__global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_decode_h_kernel(
     DecodeArgs a) {
-  constexpr int K = kDecH / 2;
-  // dynamic LDS (kDecHLds): [0, 64 KiB) premultiply tables, then transposes and
-  // derivative staging; [64, 128 KiB) the erased elements' tables
+  constexpr int NQ = K / 32, LR = K == 512 ? 1 : 2, RPR = K == 512 ? 1 : 2;
+  // dynamic LDS (dec_h_lds_bytes): [0, n x 64 B) premultiply tables, then the
+  // transposes and the derivative staging (each <= n x 64 B); [n x 64 B, 2 n x 64 B)
+  // the erased elements' tables
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn_lds[];
   uint32_t* lds = dyn_lds;
-  uint32_t* post_tab = dyn_lds + 16 * 16 * 64;
+  uint32_t* post_tab = dyn_lds + 2 * K * 16;
   const long blk = blockIdx.x;
   const int piece = (int)(blk % a.nchunk);  // nchunk = 256-B pieces of the shard
   const long v = blk / a.nchunk;
@@ -1773,18 +1779,18 @@ __global__ __launch_bounds__(kDecH) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   layer_b<true, 8>(w, q);
   layer_b<true, 16>(w, q);
   layer_b<true, 32>(w, q);
-  xpose_bt(w, lds, q, lane);
-  layer_t<true, 64>(w);
-  layer_t<true, 128>(w);
-  layer_t<true, 256>(w);
-  layer_t<true, 512>(w);
-  derivative_t(w, lds, q, lane, lowmask);
+  xpose_bt<LR, RPR>(w, lds, q, lane);
+  layer_t<true, 64, LR>(w);
+  layer_t<true, 128, LR>(w);
+  layer_t<true, 256, LR>(w);
+  if constexpr (K == 512) layer_t<true, 512, LR>(w);
+  derivative_t<NQ>(w, lds, q, lane, lowmask);
   // ---- FFT (fftDIT, skew index iend - 1) ----
-  layer_t<false, 512>(w);
-  layer_t<false, 256>(w);
-  layer_t<false, 128>(w);
-  layer_t<false, 64>(w);
-  xpose_bt(w, lds, q, lane);
+  if constexpr (K == 512) layer_t<false, 512, LR>(w);
+  layer_t<false, 256, LR>(w);
+  layer_t<false, 128, LR>(w);
+  layer_t<false, 64, LR>(w);
+  xpose_bt<LR, RPR>(w, lds, q, lane);
   layer_b<false, 32>(w, q);
   layer_b<false, 16>(w, q);
   layer_b<false, 8>(w, q);
@@ -1820,7 +1826,7 @@ __global__ __launch_bounds__(kDecH) __attribute__((amdgpu_waves_per_eu(4, 4))) v
 
 // ---------------------------------------------------------------------------
 // k = 512 encoder, round 5 (leo16_encode_h_kernel): the half-lane layouts of
-// leo16_decode_h1k_kernel over m = 512 elements -- 8 waves (512 threads) x 32
+// leo16_decode_h_kernel over m = 512 elements -- 8 waves (512 threads) x 32
 // register pairs x 2 halves, 64 data VGPRs within the 128 of 4 waves per SIMD
 // -- so TWO workgroups share a CU and one's loads and stores overlap the
 // other's transform (leo16_encode_reg32_kernel's 16 waves filled a CU alone
@@ -1830,11 +1836,13 @@ __global__ __launch_bounds__(kDecH) __attribute__((amdgpu_waves_per_eu(4, 4))) v
 // The last IFFT layer and the first FFT layer (both dist 256, registers j and
 // j + 16 in T) are merged as in the other encoders.
 // ---------------------------------------------------------------------------
-constexpr int kEncH = 512;
-template <bool REV>
-__global__ __launch_bounds__(kEncH) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_encode_h_kernel(
+// M = 256 (round 5 too): 4 waves (256 threads), T with three low register
+// bits, the merged dist-128 layer; four workgroups per CU.
+template <int M, bool REV>
+__global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_encode_h_kernel(
     EncodeArgs a) {
-  constexpr int M = 512, IO = REV ? 0 : M, FO = REV ? M : 0;
+  constexpr int IO = REV ? 0 : M, FO = REV ? M : 0;
+  constexpr int LR = M == 512 ? 2 : 3, RPR = M == 512 ? 2 : 8;
   __shared__ __attribute__((aligned(16))) uint32_t lds[8 * 8 * 2 * 64];  // 32 KiB per transpose round
   const long blk = blockIdx.x;
   const int piece = (int)(blk % a.nchunk);  // nchunk = 256-B pieces of the shard
@@ -1881,20 +1889,20 @@ __global__ __launch_bounds__(kEncH) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   layer_b<true, 8, IO>(w, q);
   layer_b<true, 16, IO>(w, q);
   layer_b<true, 32, IO>(w, q);
-  xpose_bt<2, 2>(w, lds, q, lane);
-  layer_t<true, 64, 2, IO>(w);
-  layer_t<true, 128, 2, IO>(w);
-  // last IFFT layer (dist 256, skew IO - 1 + 256) merged with the first FFT
-  // layer (dist 256, skew FO + 255): registers j, j + 16
+  xpose_bt<LR, RPR>(w, lds, q, lane);
+  layer_t<true, 64, LR, IO>(w);
+  if constexpr (M == 512) layer_t<true, 128, LR, IO>(w);
+  // last IFFT layer (dist M / 2, skew IO - 1 + M / 2) merged with the first FFT
+  // layer (dist M / 2, skew FO + M / 2 - 1): registers j, j + 16
 #pragma unroll
   for (int j = 0; j < 16; j++) {
-    ifft_fft2_16(w, j, j + 16, MERGED_TAB(1));
+    ifft_fft2_16(w, j, j + 16, MERGED_TAB(M == 512 ? 1 : 0));
     pin_pair(w, j, j + 16);
   }
   // ---- FFT (fftDIT, skew index FO + iend - 1) ----
-  layer_t<false, 128, 2, FO>(w);
-  layer_t<false, 64, 2, FO>(w);
-  xpose_bt<2, 2>(w, lds, q, lane);
+  if constexpr (M == 512) layer_t<false, 128, LR, FO>(w);
+  layer_t<false, 64, LR, FO>(w);
+  xpose_bt<LR, RPR>(w, lds, q, lane);
   layer_b<false, 32, FO>(w, q);
   layer_b<false, 16, FO>(w, q);
   layer_b<false, 8, FO>(w, q);
@@ -2090,8 +2098,8 @@ static bool enc32_waves(int k) {
   return k == 512;
 }
 
-// k = 512 encoder: the half-lane kernel (round 5); DAGPU_GF16_ENCH=0 selects
-// leo16_encode_reg32_kernel (A/B)
+// k = 256 / 512 encoders: the half-lane kernels (round 5); DAGPU_GF16_ENCH=0
+// selects the register kernels of round 4 (A/B)
 static bool ench_on() {  // read per launch: the tests switch it in-process
   const char* e = getenv("DAGPU_GF16_ENCH");
   return !(e && e[0] == '0');
@@ -2109,11 +2117,16 @@ hipError_t launch_leo16_encode(int k, const EncodeArgs& a, hipStream_t s) {
     b.nchunk = (a.shard_bytes + 511) / 512;
     const long blocks = b.nsq * b.nvec * b.nchunk;
     if (blocks <= 0) return hipSuccess;
-    if (k == 512 && ench_on()) {  // half-lane kernel, 256-B pieces
+    if (ench_on()) {  // half-lane kernels, 256-B pieces
       b.nchunk = (a.shard_bytes + 255) / 256;
       const long hb = b.nsq * b.nvec * b.nchunk;
-      if (a.reverse) hipLaunchKernelGGL((leo16_encode_h_kernel<true>), dim3((unsigned)hb), dim3(kEncH), 0, s, b);
-      else hipLaunchKernelGGL((leo16_encode_h_kernel<false>), dim3((unsigned)hb), dim3(kEncH), 0, s, b);
+      if (k == 512) {
+        if (a.reverse) hipLaunchKernelGGL((leo16_encode_h_kernel<512, true>), dim3((unsigned)hb), dim3(512), 0, s, b);
+        else hipLaunchKernelGGL((leo16_encode_h_kernel<512, false>), dim3((unsigned)hb), dim3(512), 0, s, b);
+      } else {
+        if (a.reverse) hipLaunchKernelGGL((leo16_encode_h_kernel<256, true>), dim3((unsigned)hb), dim3(256), 0, s, b);
+        else hipLaunchKernelGGL((leo16_encode_h_kernel<256, false>), dim3((unsigned)hb), dim3(256), 0, s, b);
+      }
     } else if (enc32_waves(k)) {
       if (k == 256) {
         constexpr int L = enc32_lds_bytes<256>();
@@ -2160,7 +2173,6 @@ hipError_t launch_leo16_errlocs(const DecodeArgs& a, hipStream_t s) {
 // dynamic LDS of the register-resident decoders: staging + erasure tables
 constexpr size_t kDecLds = (8 * 16 * 2 * 64 + kDecN * 16) * sizeof(uint32_t);    // 96 KiB
 constexpr size_t kDec1kLds = (16 * 16 * 64 + kDec1k * 16) * sizeof(uint32_t);     // 128 KiB
-constexpr size_t kDecHLds = (16 * 16 * 64 + kDecH * 16) * sizeof(uint32_t);       // 128 KiB
 static hipError_t dec_lds_attr() {  // above the 64 KiB default: once per process
   static std::once_flag once;
   static hipError_t err = hipSuccess;
@@ -2171,12 +2183,21 @@ static hipError_t dec_lds_attr() {  // above the 64 KiB default: once per proces
       err = hipFuncSetAttribute((const void*)leo16_decode_reg1k_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDec1kLds);
     if (err == hipSuccess)
-      err = hipFuncSetAttribute((const void*)leo16_decode_h1k_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDecHLds);
+      err = hipFuncSetAttribute((const void*)leo16_decode_h_kernel<512>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)dec_h_lds_bytes<512>());
+    if (err == hipSuccess)
+      err = hipFuncSetAttribute((const void*)leo16_decode_h_kernel<256>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)dec_h_lds_bytes<256>());
   });
   return err;
 }
 
+// k = 256 decoder: the half-lane kernel (round 5); DAGPU_DEC256_REG=1 selects
+// leo16_decode_reg_kernel (A/B)
+static bool dec256_reg() {
+  const char* e = getenv("DAGPU_DEC256_REG");
+  return e && e[0] == '1';
+}
 // k = 512 decoder: the half-lane unpacked kernel (round 5); DAGPU_DEC1K_PACKED=1
 // selects the packed one of rounds 2-4 (A/B)
 static bool dec1k_packed() {  // read per launch: the tests switch it in-process
@@ -2192,7 +2213,13 @@ hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mar
   const long nv = a.nsq * a.nvec;
   if (nv <= 0) return hipSuccess;
 #ifndef DAGPU_GF16_LDS_DECODE
-  if (a.k == kDecN / 2) {  // register-resident decoder; nchunk = 512-B chunks of the shard
+  if (a.k == 256 && a.shard_bytes % 256 == 0 && !dec256_reg()) {  // half-lane decoder, 256-B pieces
+    DecodeArgs b = a;
+    b.nchunk = a.shard_bytes / 256;
+    if ((e = dec_lds_attr()) != hipSuccess) return e;
+    hipLaunchKernelGGL(leo16_decode_h_kernel<256>, dim3((unsigned)(nv * b.nchunk)), dim3(512),
+                       dec_h_lds_bytes<256>(), s, b);
+  } else if (a.k == kDecN / 2) {  // register-resident decoder; nchunk = 512-B chunks of the shard
     DecodeArgs b = a;
     b.nchunk = (a.shard_bytes + 511) / 512;
     if ((e = dec_lds_attr()) != hipSuccess) return e;
@@ -2204,7 +2231,8 @@ hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mar
     if (dec1k_packed())
       hipLaunchKernelGGL(leo16_decode_reg1k_kernel, dim3((unsigned)(nv * b.nchunk)), dim3(kDec1k), kDec1kLds, s, b);
     else
-      hipLaunchKernelGGL(leo16_decode_h1k_kernel, dim3((unsigned)(nv * b.nchunk)), dim3(kDecH), kDecHLds, s, b);
+      hipLaunchKernelGGL(leo16_decode_h_kernel<512>, dim3((unsigned)(nv * b.nchunk)), dim3(1024),
+                         dec_h_lds_bytes<512>(), s, b);
   } else
 #endif
   {

@@ -139,13 +139,13 @@ def test_gf16_repair_max_erasure(ctx, k):
         da.repair(bad, present, rr, cr, ctx)
 
 
+@pytest.mark.parametrize("k", [256, 512])
 @pytest.mark.parametrize("shard", [64, 256, 1536])
-def test_k512_encoders_agree(ctx, shard, monkeypatch):
-    """Round 5: the half-lane k = 512 encoder (two workgroups per CU, 256-B
-    pieces) byte-equal to the 16-wave register encoder (DAGPU_GF16_ENCH=0),
-    plain and as the reverse transform, and to the oracle."""
-    k = 512
-    rng = np.random.default_rng(3 * shard)
+def test_halflane_encoders_agree(ctx, k, shard, monkeypatch):
+    """Round 5: the half-lane encoders (k = 512: two workgroups per CU, k = 256:
+    four; 256-B pieces) byte-equal to the round-4 register encoders
+    (DAGPU_GF16_ENCH=0) and to the oracle."""
+    rng = np.random.default_rng(3 * shard + k)
     data = rng.integers(0, 256, (3, k, shard), dtype=np.uint8)
     codec = da.LeoRSCodec(ctx)
     half = codec.encode_batch(data)
@@ -155,13 +155,13 @@ def test_k512_encoders_agree(ctx, shard, monkeypatch):
     assert (half[0] == oracle.encode(data[0])).all()
 
 
+@pytest.mark.parametrize("k,env", [(512, "DAGPU_DEC1K_PACKED"), (256, "DAGPU_DEC256_REG")])
 @pytest.mark.parametrize("shard", [256, 512])
-def test_k512_decoders_agree(ctx, shard, monkeypatch):
-    """Round 5: the half-lane unpacked k = 512 decoder byte-equal to the packed
-    one of rounds 2-4 (DAGPU_DEC1K_PACKED=1) on random, data-half and
-    parity-half erasures."""
-    k = 512
-    rng = np.random.default_rng(11 + shard)
+def test_halflane_decoders_agree(ctx, k, env, shard, monkeypatch):
+    """Round 5: the half-lane unpacked decoders byte-equal to the register
+    decoders they replace (k = 512: the packed one of rounds 2-4; k = 256: the
+    8-wave one) on random, data-half and parity-half erasures."""
+    rng = np.random.default_rng(11 + shard + k)
     data = rng.integers(0, 256, (k, shard), dtype=np.uint8)
     full = np.concatenate([data, oracle.encode(data)])
     codec = da.LeoRSCodec(ctx)
@@ -170,8 +170,8 @@ def test_k512_decoders_agree(ctx, shard, monkeypatch):
     for keep in pats:
         shards = [full[i].tobytes() if i in keep else None for i in range(2 * k)]
         new = codec.decode(shards)
-        monkeypatch.setenv("DAGPU_DEC1K_PACKED", "1")
+        monkeypatch.setenv(env, "1")
         old = codec.decode(shards)
-        monkeypatch.delenv("DAGPU_DEC1K_PACKED")
+        monkeypatch.delenv(env)
         assert new == old
         assert b"".join(new) == full.tobytes()

@@ -4,7 +4,8 @@ elements, and leo16_encode_h_kernel, k = 512 encode over m = 512): the same
 layouts S / B / T (two elements per register, one per half wave), the
 permlane32 swap S <-> B, the LDS transpose B <-> T, the skew position of
 every butterfly, the closed-form formal derivative with its half-bit term and
-the merged last-IFFT / first-FFT encoder layer -- on one symbol column, against
+the merged last-IFFT / first-FFT encoder layer (k = 256 too: n = 512 decode, m = 256
+encode) -- on one symbol column, against
 the plain Leopard loops (klauspost/reedsolomon v1.11.8 leopard.go
 ifftDITDecoder / ifftDITEncoder, formalDerivative, fftDIT; SURVEY.md Appendix
 A.5-A.6).  The field arithmetic is the same on every symbol column, so one
@@ -180,8 +181,9 @@ def layer_t(R, d, lr, off, inv):
                     reg[j][hl], reg[j + rd][hl] = w
 
 
-def derivative_t(R):
+def derivative_t(R, lr):
     orig = [[list(x) for x in reg] for reg in R]
+    nq = len(R)
     for c, reg in enumerate(R):
         for j in range(32):
             for hl in range(2):
@@ -190,7 +192,7 @@ def derivative_t(R):
                     if not j & bit:
                         acc ^= orig[c][j | bit][hl]
                 for wb in (1, 2, 4, 8):
-                    if not c & wb:
+                    if wb < nq and not c & wb:
                         acc ^= orig[c | wb][j][hl]
                 if hl == 0:
                     acc ^= orig[c][j][1]
@@ -207,37 +209,38 @@ def gather(R, f):
 
 
 def test_layout_maps_are_bijections():
-    for nq, lr in ((16, 1), (8, 2)):
+    for nq, lr in ((16, 1), (8, 2), (4, 3)):
         n = 64 * nq
         for f in (e_s, e_b, lambda q, j, hl: e_t(q, j, hl, lr)):
             es = {f(q, j, hl) for q in range(nq) for j in range(32) for hl in range(2)}
             assert es == set(range(n))
 
 
-@pytest.mark.parametrize("seed", [1, 2])
-def test_halflane_decoder_equals_leopard_loops(seed):
+@pytest.mark.parametrize("k,seed", [(512, 1), (512, 2), (256, 3)])
+def test_halflane_decoder_equals_leopard_loops(k, seed):
     rng = np.random.default_rng(seed)
-    n = 1024
+    n = 2 * k
+    nq, lr = n // 64, (1 if n == 1024 else 2)
     x = [int(v) for v in rng.integers(0, 65536, n)]
     ref = list(x)
     ref_ifft(ref, 0)
     ref_derivative(ref)
     ref_fft(ref, 0)
     # kernel order: load in S, IFFT bit 0 in S, swap to B, bits 1-5, transpose
-    # to T, bits 6-9, derivative, FFT 9-6, transpose, 5-1, swap, bit 0
-    R = [[[x[e_s(q, j, 0)], x[e_s(q, j, 1)]] for j in range(32)] for q in range(16)]
+    # to T, bits 6.., derivative, FFT .. 6, transpose, 5-1, swap, bit 0
+    R = [[[x[e_s(q, j, 0)], x[e_s(q, j, 1)]] for j in range(32)] for q in range(nq)]
     layer0_s(R, 0, True)
     swap_sb(R)
-    assert gather(R, e_b) == gather(R, e_b)  # (layout B now)
     for d in (2, 4, 8, 16, 32):
         layer_b(R, d, 0, True)
-    R = xpose_bt(R, 1)
-    for d in (64, 128, 256, 512):
-        layer_t(R, d, 1, 0, True)
-    derivative_t(R)
-    for d in (512, 256, 128, 64):
-        layer_t(R, d, 1, 0, False)
-    R = xpose_bt(R, 1)
+    R = xpose_bt(R, lr)
+    tds = [d for d in (64, 128, 256, 512) if d < n]
+    for d in tds:
+        layer_t(R, d, lr, 0, True)
+    derivative_t(R, lr)
+    for d in reversed(tds):
+        layer_t(R, d, lr, 0, False)
+    R = xpose_bt(R, lr)
     for d in (32, 16, 8, 4, 2):
         layer_b(R, d, 0, False)
     swap_sb(R)
@@ -245,25 +248,27 @@ def test_halflane_decoder_equals_leopard_loops(seed):
     assert gather(R, e_s) == ref
 
 
-@pytest.mark.parametrize("rev", [False, True])
-def test_halflane_encoder_equals_leopard_loops(rev):
-    rng = np.random.default_rng(7 + rev)
-    m = 512
+@pytest.mark.parametrize("m,rev", [(512, False), (512, True), (256, False), (256, True)])
+def test_halflane_encoder_equals_leopard_loops(m, rev):
+    rng = np.random.default_rng(7 + rev + m)
+    nq, lr = m // 64, (2 if m == 512 else 3)
     io, fo = (0, m) if rev else (m, 0)
     x = [int(v) for v in rng.integers(0, 65536, m)]
     ref = list(x)
     ref_ifft(ref, io)
     ref_fft(ref, fo)
-    R = [[[x[e_s(q, j, 0)], x[e_s(q, j, 1)]] for j in range(32)] for q in range(8)]
+    R = [[[x[e_s(q, j, 0)], x[e_s(q, j, 1)]] for j in range(32)] for q in range(nq)]
     layer0_s(R, io, True)
     swap_sb(R)
     for d in (2, 4, 8, 16, 32):
         layer_b(R, d, io, True)
-    R = xpose_bt(R, 2)
-    for d in (64, 128):
-        layer_t(R, d, 2, io, True)
-    # merged dist-256 layers (registers j, j + 16 in T): y ^= x; x ^= y (A ^ B); y ^= x
-    a, b = int(SKEW[io + 255]), int(SKEW[fo + 255])
+    R = xpose_bt(R, lr)
+    tds = [d for d in (64, 128) if d < m // 2]
+    for d in tds:
+        layer_t(R, d, lr, io, True)
+    # merged dist-m/2 layers (registers j, j + 16 in T): y ^= x; x ^= y (A ^ B); y ^= x
+    h = m // 2
+    a, b = int(SKEW[io + h - 1]), int(SKEW[fo + h - 1])
     for reg in R:
         for j in range(16):
             for hl in range(2):
@@ -272,9 +277,9 @@ def test_halflane_encoder_equals_leopard_loops(rev):
                 xx ^= (mul(yy, a) if a != MOD else 0) ^ (mul(yy, b) if b != MOD else 0)
                 yy ^= xx
                 reg[j][hl], reg[j + 16][hl] = xx, yy
-    for d in (128, 64):
-        layer_t(R, d, 2, fo, False)
-    R = xpose_bt(R, 2)
+    for d in reversed(tds):
+        layer_t(R, d, lr, fo, False)
+    R = xpose_bt(R, lr)
     for d in (32, 16, 8, 4, 2):
         layer_b(R, d, fo, False)
     swap_sb(R)
