@@ -26,6 +26,17 @@ case "$1" in
     bash tools/gpu_ab.sh --rounds 1 repair512q3 new= reg32=DAGPU_GF16_ENCH=0 prev=lib:celestia-app_amd/libdagpu_prev.so && \
     bash tools/gpu_pmc_gf16.sh repair512 split512
     ;;
+  pf)  # round 5: k = 256 half-lane kernels and the SGPR table prefetch (issued one group ahead): tests, A/B vs the build without prefetch (nopf) and round 4 (prev)
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_gf16.py tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py tests/test_gpu_split.py > gpurun_out/r05_pf_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r05_pf_tests.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 2 repair512 new= nopf=lib:celestia-app_amd/libdagpu_nopf.so && \
+    bash tools/gpu_ab.sh --rounds 2 split512 new= nopf=lib:celestia-app_amd/libdagpu_nopf.so prev=lib:celestia-app_amd/libdagpu_prev.so && \
+    bash tools/gpu_ab.sh --rounds 1 repair512q3 new= nopf=lib:celestia-app_amd/libdagpu_nopf.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 256 --batch 8 --steps 5 --warmup 1" new= nopf=lib:celestia-app_amd/libdagpu_nopf.so prev=lib:celestia-app_amd/libdagpu_prev.so && \
+    bash tools/gpu_ab.sh --rounds 1 "bench:--mode repair --k 256 --batch 8 --steps 5 --warmup 1 --pattern q3" new= nopf=lib:celestia-app_amd/libdagpu_nopf.so prev=lib:celestia-app_amd/libdagpu_prev.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode split --split-k 256 --steps 10 --warmup 2" new= nopf=lib:celestia-app_amd/libdagpu_nopf.so prev=lib:celestia-app_amd/libdagpu_prev.so && \
+    bash tools/gpu_pmc_gf16.sh repair512 split512
+    ;;
   final-a)  # round end, part 1: the whole -m gpu suite, the default bench line and its rocprofv3 kernel trace
     bash tools/gpu_final.sh
     ;;
