@@ -505,9 +505,8 @@ constexpr int kTab16x = 20;
 __constant__ uint32_t g_ptab16x[kTabPos * kTab16x];
 __constant__ uint32_t g_ptab16x_merged[2 * kTab16x];
 
-template <class TT>
 __device__ __forceinline__ void mul16x_add_t(uint32_t& xlo, uint32_t& xhi, uint32_t ylo, uint32_t yhi,
-                                             const TT& t) {
+                                             const uint32_t* t) {
   const uint32_t s0 = ylo & 0x07070707u, s1 = (ylo >> 3) & 0x07070707u, s2 = (ylo >> 6) & 0x03030303u;
   const uint32_t s3 = yhi & 0x07070707u, s4 = (yhi >> 3) & 0x07070707u, s5 = (yhi >> 6) & 0x03030303u;
   using B = uint32_t;
@@ -1602,142 +1601,6 @@ __device__ __forceinline__ void pin_pair(W32& w, int i, int j) {
   asm volatile("" : "+v"(w.lo[i]), "+v"(w.hi[i]), "+v"(w.lo[j]), "+v"(w.hi[j]));
 }
 
-// Skew tables of the B and T layers, double-buffered in SGPRs (round 5): each
-// group's table load is issued once the previous group's table has arrived
-// (its position passes through an asm reading that table, opaque_after), so it
-// is in flight while that group computes.  Scalar loads return out of order, so
-// the compiler waits for every outstanding one before a table's first use; with
-// each load issued one group ahead, that wait finds it done.  (Loaded just
-// before their use, every table load's latency was exposed: profiles r05.)
-typedef unsigned int u32x16_t __attribute__((ext_vector_type(16)));
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-struct Tab20 {
-  u32x16_t a;  // dwords 0-15
-  u32x4_t b;   // dwords 16-19
-  __device__ __forceinline__ uint32_t operator[](int i) const { return i < 16 ? a[i] : b[i - 16]; }
-};
-// Issue the two scalar loads of position pos's table without waiting: the
-// compiler's waitcnt pass does not see inline-asm loads, so wait_tab (an
-// s_waitcnt that passes the registers through) must come before their use.
-__device__ __forceinline__ Tab20 issue_tab(int pos) {
-  const uint64_t p = (uint64_t)(g_ptab16x + pos * kTab16x);
-  Tab20 t;
-  asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx4 %1, %2, 0x40" : "=&s"(t.a), "=&s"(t.b) : "s"(p));
-  return t;
-}
-__device__ __forceinline__ void wait_tab(Tab20& t) {
-  asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(t.a), "+s"(t.b));
-}
-template <bool INV>
-__device__ __forceinline__ void bfly_t(W32& w, int i, int j, const Tab20& t) {
-  if constexpr (INV) {  // ifftDIT2: y ^= x; x ^= y * skew
-    w.lo[j] ^= w.lo[i];
-    w.hi[j] ^= w.hi[i];
-    mul16x_add_t(w.lo[i], w.hi[i], w.lo[j], w.hi[j], t);
-  } else {  // fftDIT2: x ^= y * skew; y ^= x
-    mul16x_add_t(w.lo[i], w.hi[i], w.lo[j], w.hi[j], t);
-    w.lo[j] ^= w.lo[i];
-    w.hi[j] ^= w.hi[i];
-  }
-  pin_pair(w, i, j);
-}
-
-// B phase: the layers on element bits 1-5 (D = 2 .. 32; IFFT ascending, FFT
-// descending) as one sequence of groups (one skew position each: a block of
-// 2 D elements of the wave), g = 0 .. 30
-constexpr int bgD(bool inv, int g) {
-  for (int li = 0; li < 5; li++) {
-    const int D = 2 << (inv ? li : 4 - li), n = 64 / (2 * D);
-    if (g < n) return D;
-    g -= n;
-  }
-  return 0;
-}
-constexpr int bgR(bool inv, int g) {
-  for (int li = 0; li < 5; li++) {
-    const int D = 2 << (inv ? li : 4 - li), n = 64 / (2 * D);
-    if (g < n) return g * 2 * D;
-    g -= n;
-  }
-  return 0;
-}
-template <bool INV, int OFF, int G>
-__device__ __forceinline__ void bphase(W32& w, int qb, Tab20 cur) {
-  constexpr int D = bgD(INV, G), r = bgR(INV, G);
-  wait_tab(cur);
-  if constexpr (G + 1 < 31) {
-    constexpr int P1 = OFF + bgR(INV, G + 1) + bgD(INV, G + 1) - 1;  // (constant-evaluated)
-    const Tab20 nxt = issue_tab(qb + P1);  // in flight while this group computes
-#pragma unroll
-    for (int e = r; e < r + D; e += 2) bfly_t<INV>(w, e / 2, e / 2 + D / 2, cur);
-    bphase<INV, OFF, G + 1>(w, qb, nxt);
-  } else {
-#pragma unroll
-    for (int e = r; e < r + D; e += 2) bfly_t<INV>(w, e / 2, e / 2 + D / 2, cur);
-  }
-}
-template <bool INV, int OFF>
-__device__ __forceinline__ void bphase_run(W32& w, int q) {
-  const int qb = 64 * q;
-  constexpr int P0 = OFF + bgR(INV, 0) + bgD(INV, 0) - 1;
-  bphase<INV, OFF, 0>(w, qb, issue_tab(qb + P0));
-}
-
-// T phase: the layers on element bits 6 .. log2(DMAX) of an N-element
-// transform in layout T (LR low register bits), groups = (layer, block).
-constexpr int tgCount(int N, int DMAX) {
-  int c = 0;
-  for (int D = 64; D <= DMAX; D *= 2) c += N / (2 * D);
-  return c;
-}
-constexpr int tgD(bool inv, int g, int N, int DMAX) {
-  int nl = 0;
-  for (int D = 64; D <= DMAX; D *= 2) nl++;
-  for (int li = 0; li < nl; li++) {
-    const int D = 64 << (inv ? li : nl - 1 - li), n = N / (2 * D);
-    if (g < n) return D;
-    g -= n;
-  }
-  return 0;
-}
-constexpr int tgB(bool inv, int g, int N, int DMAX) {
-  int nl = 0;
-  for (int D = 64; D <= DMAX; D *= 2) nl++;
-  for (int li = 0; li < nl; li++) {
-    const int D = 64 << (inv ? li : nl - 1 - li), n = N / (2 * D);
-    if (g < n) return g * 2 * D;
-    g -= n;
-  }
-  return 0;
-}
-template <bool INV, int LR, int OFF, int N, int DMAX, int G>
-__device__ __forceinline__ void tphase(W32& w, Tab20 cur) {
-  constexpr int D = tgD(INV, G, N, DMAX), blk = tgB(INV, G, N, DMAX), RD = (D / 64) << LR;
-  constexpr int NG = tgCount(N, DMAX);
-  auto run = [&]() {
-#pragma unroll
-    for (int j = 0; j < 32; j++) {
-      if (j & RD) continue;
-      if ((((j >> LR) << 6) & ~(2 * D - 1)) != blk) continue;
-      bfly_t<INV>(w, j, j + RD, cur);
-    }
-  };
-  wait_tab(cur);
-  if constexpr (G + 1 < NG) {
-    constexpr int P1 = OFF + tgB(INV, G + 1, N, DMAX) + tgD(INV, G + 1, N, DMAX) - 1;
-    const Tab20 nxt = issue_tab(P1);  // in flight while this group computes
-    run();
-    tphase<INV, LR, OFF, N, DMAX, G + 1>(w, nxt);
-  } else {
-    run();
-  }
-}
-template <bool INV, int LR, int OFF, int N, int DMAX>
-__device__ __forceinline__ void tphase_run(W32& w) {
-  constexpr int P0 = OFF + tgB(INV, 0, N, DMAX) + tgD(INV, 0, N, DMAX) - 1;
-  tphase<INV, LR, OFF, N, DMAX, 0>(w, issue_tab(P0));
-}
-
 // One layer on element bit b >= 1 in layout B (dist D = 1 << b, registers j
 // and j + D / 2): butterflies grouped by skew position (block of 2 D elements,
 // position = block start + D - 1), one table per group.
@@ -1911,14 +1774,28 @@ __global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   // ---- IFFT (ifftDITDecoder, skew index iend - 1) ----
   layer0_s<true>(w, q, hl);
   swap_sb(w);
-  bphase_run<true, 0>(w, q);  // bits 1-5
+  layer_b<true, 2>(w, q);
+  layer_b<true, 4>(w, q);
+  layer_b<true, 8>(w, q);
+  layer_b<true, 16>(w, q);
+  layer_b<true, 32>(w, q);
   xpose_bt<LR, RPR>(w, lds, q, lane);
-  tphase_run<true, LR, 0, 2 * K, K>(w);  // bits 6 ..
+  layer_t<true, 64, LR>(w);
+  layer_t<true, 128, LR>(w);
+  layer_t<true, 256, LR>(w);
+  if constexpr (K == 512) layer_t<true, 512, LR>(w);
   derivative_t<NQ>(w, lds, q, lane, lowmask);
   // ---- FFT (fftDIT, skew index iend - 1) ----
-  tphase_run<false, LR, 0, 2 * K, K>(w);
+  if constexpr (K == 512) layer_t<false, 512, LR>(w);
+  layer_t<false, 256, LR>(w);
+  layer_t<false, 128, LR>(w);
+  layer_t<false, 64, LR>(w);
   xpose_bt<LR, RPR>(w, lds, q, lane);
-  bphase_run<false, 0>(w, q);
+  layer_b<false, 32>(w, q);
+  layer_b<false, 16>(w, q);
+  layer_b<false, 8>(w, q);
+  layer_b<false, 4>(w, q);
+  layer_b<false, 2>(w, q);
   swap_sb(w);
   layer0_s<false>(w, q, hl);
   // erased shards = work * (65535 - errLocs), per lane; a register whose two
@@ -2007,9 +1884,14 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
   // ---- IFFT (ifftDITEncoder, skew index IO - 1 + iend) ----
   layer0_s<true, IO>(w, q, hl);
   swap_sb(w);
-  bphase_run<true, IO>(w, q);
+  layer_b<true, 2, IO>(w, q);
+  layer_b<true, 4, IO>(w, q);
+  layer_b<true, 8, IO>(w, q);
+  layer_b<true, 16, IO>(w, q);
+  layer_b<true, 32, IO>(w, q);
   xpose_bt<LR, RPR>(w, lds, q, lane);
-  tphase_run<true, LR, IO, M, M / 4>(w);
+  layer_t<true, 64, LR, IO>(w);
+  if constexpr (M == 512) layer_t<true, 128, LR, IO>(w);
   // last IFFT layer (dist M / 2, skew IO - 1 + M / 2) merged with the first FFT
   // layer (dist M / 2, skew FO + M / 2 - 1): registers j, j + 16
 #pragma unroll
@@ -2018,9 +1900,14 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
     pin_pair(w, j, j + 16);
   }
   // ---- FFT (fftDIT, skew index FO + iend - 1) ----
-  tphase_run<false, LR, FO, M, M / 4>(w);
+  if constexpr (M == 512) layer_t<false, 128, LR, FO>(w);
+  layer_t<false, 64, LR, FO>(w);
   xpose_bt<LR, RPR>(w, lds, q, lane);
-  bphase_run<false, FO>(w, q);
+  layer_b<false, 32, FO>(w, q);
+  layer_b<false, 16, FO>(w, q);
+  layer_b<false, 8, FO>(w, q);
+  layer_b<false, 4, FO>(w, q);
+  layer_b<false, 2, FO>(w, q);
   swap_sb(w);
   layer0_s<false, FO>(w, q, hl);
   if (!active) return;
