@@ -1376,8 +1376,15 @@ __device__ __forceinline__ void derivativep(W1k& w, uint32_t* lds, int c, int la
 // library): lane 0 of waves 0 and 15 stamp s_memtime at the decoder's phase
 // boundaries, [block][wave 0 / 15][phase].
 #ifdef DAGPU_PHASE_PROBE
-constexpr int kProbePhases = 12;
+constexpr int kProbePhases = 14;
 __device__ uint64_t g_probe[8192 * 2 * kProbePhases];
+__device__ uint64_t g_probe_e[8192 * 2 * kProbePhases];  // the half-lane encoders'
+// half-lane kernels: waves 0 and QL (the last) of the first 8192 workgroups
+#define H_PROBE(buf, i, QL)                                                                      \
+  do {                                                                                          \
+    if ((threadIdx.x & 63) == 0 && (q == 0 || q == (QL)) && blockIdx.x < 8192)                  \
+      buf[(blockIdx.x * 2 + (q == (QL))) * kProbePhases + (i)] = __builtin_amdgcn_s_memtime();  \
+  } while (0)
 #define DEC_PROBE(i)                                                                            \
   do {                                                                                          \
     if ((threadIdx.x & 63) == 0 && (q == 0 || q == 15) && blk < 8192)                           \
@@ -1385,6 +1392,7 @@ __device__ uint64_t g_probe[8192 * 2 * kProbePhases];
   } while (0)
 #else
 #define DEC_PROBE(i) ((void)0)
+#define H_PROBE(buf, i, QL) ((void)0)
 #endif
 
 __global__ __launch_bounds__(kDec1k) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_decode_reg1k_kernel(
@@ -1735,6 +1743,7 @@ __global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   const int hl = lane >> 5;
   const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t lowmask = hl ? 0u : 0xFFFFFFFFu;
+  H_PROBE(g_probe, 0, NQ - 1);
   // lane (hl, c): 64-B block c >> 3 of this 256-B piece, symbols 4 (c & 7) .. +3
   const uint32_t col = (uint32_t)piece * 256u + (uint32_t)((lane & 31) >> 3) * 64u + (uint32_t)(lane & 7) * 4u;
   const uint32_t voff = col + (uint32_t)hl * 32u * (uint32_t)a.shard_stride;  // upper half: shard + 32
@@ -1759,6 +1768,7 @@ __global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     w.hi[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff + 32u, so, 0);
   }
   __syncthreads();
+  H_PROBE(g_probe, 1, NQ - 1);
   const int q_pm = opaque_s(q);
 #pragma unroll
   for (int j = 0; j < 32; j++) {
@@ -1771,33 +1781,43 @@ __global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     w.hi[j] = xh;
   }
   __syncthreads();  // the transposes reuse the premultiply tables' LDS
+  H_PROBE(g_probe, 2, NQ - 1);
   // ---- IFFT (ifftDITDecoder, skew index iend - 1) ----
   layer0_s<true>(w, q, hl);
   swap_sb(w);
+  H_PROBE(g_probe, 3, NQ - 1);
   layer_b<true, 2>(w, q);
   layer_b<true, 4>(w, q);
   layer_b<true, 8>(w, q);
   layer_b<true, 16>(w, q);
   layer_b<true, 32>(w, q);
+  H_PROBE(g_probe, 4, NQ - 1);
   xpose_bt<LR, RPR>(w, lds, q, lane);
+  H_PROBE(g_probe, 5, NQ - 1);
   layer_t<true, 64, LR>(w);
   layer_t<true, 128, LR>(w);
   layer_t<true, 256, LR>(w);
   if constexpr (K == 512) layer_t<true, 512, LR>(w);
+  H_PROBE(g_probe, 6, NQ - 1);
   derivative_t<NQ>(w, lds, q, lane, lowmask);
+  H_PROBE(g_probe, 7, NQ - 1);
   // ---- FFT (fftDIT, skew index iend - 1) ----
   if constexpr (K == 512) layer_t<false, 512, LR>(w);
   layer_t<false, 256, LR>(w);
   layer_t<false, 128, LR>(w);
   layer_t<false, 64, LR>(w);
+  H_PROBE(g_probe, 8, NQ - 1);
   xpose_bt<LR, RPR>(w, lds, q, lane);
+  H_PROBE(g_probe, 9, NQ - 1);
   layer_b<false, 32>(w, q);
   layer_b<false, 16>(w, q);
   layer_b<false, 8>(w, q);
   layer_b<false, 4>(w, q);
   layer_b<false, 2>(w, q);
+  H_PROBE(g_probe, 10, NQ - 1);
   swap_sb(w);
   layer0_s<false>(w, q, hl);
+  H_PROBE(g_probe, 11, NQ - 1);
   // erased shards = work * (65535 - errLocs), per lane; a register whose two
   // elements are both given is skipped (wave-uniform)
   uint64_t pm_e = pm;
@@ -1822,6 +1842,7 @@ __global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     }
     __builtin_amdgcn_sched_barrier(0);
   }
+  H_PROBE(g_probe, 12, NQ - 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -1855,6 +1876,7 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
   const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t col = (uint32_t)piece * 256u + (uint32_t)((lane & 31) >> 3) * 64u + (uint32_t)(lane & 7) * 4u;
   const bool active = col < (uint32_t)a.shard_bytes;
+  H_PROBE(g_probe_e, 0, M / 64 - 1);
   const uint32_t cl = active ? col : 0u;  // inactive lanes read valid memory, store nothing
   W32 w;
   {
@@ -1881,15 +1903,19 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
   // Repair fill: which out-half shards are given (element 64 q + lane), read
   // before the transform so that the store loop does not wait on presence loads
   const uint64_t given = a.out_present ? __builtin_amdgcn_ballot_w64(fill_given(a, sq, vec, 64 * q + lane)) : 0ull;
+  H_PROBE(g_probe_e, 1, M / 64 - 1);
   // ---- IFFT (ifftDITEncoder, skew index IO - 1 + iend) ----
   layer0_s<true, IO>(w, q, hl);
   swap_sb(w);
+  H_PROBE(g_probe_e, 2, M / 64 - 1);
   layer_b<true, 2, IO>(w, q);
   layer_b<true, 4, IO>(w, q);
   layer_b<true, 8, IO>(w, q);
   layer_b<true, 16, IO>(w, q);
   layer_b<true, 32, IO>(w, q);
+  H_PROBE(g_probe_e, 3, M / 64 - 1);
   xpose_bt<LR, RPR>(w, lds, q, lane);
+  H_PROBE(g_probe_e, 4, M / 64 - 1);
   layer_t<true, 64, LR, IO>(w);
   if constexpr (M == 512) layer_t<true, 128, LR, IO>(w);
   // last IFFT layer (dist M / 2, skew IO - 1 + M / 2) merged with the first FFT
@@ -1902,14 +1928,18 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
   // ---- FFT (fftDIT, skew index FO + iend - 1) ----
   if constexpr (M == 512) layer_t<false, 128, LR, FO>(w);
   layer_t<false, 64, LR, FO>(w);
+  H_PROBE(g_probe_e, 5, M / 64 - 1);
   xpose_bt<LR, RPR>(w, lds, q, lane);
+  H_PROBE(g_probe_e, 6, M / 64 - 1);
   layer_b<false, 32, FO>(w, q);
   layer_b<false, 16, FO>(w, q);
   layer_b<false, 8, FO>(w, q);
   layer_b<false, 4, FO>(w, q);
   layer_b<false, 2, FO>(w, q);
+  H_PROBE(g_probe_e, 7, M / 64 - 1);
   swap_sb(w);
   layer0_s<false, FO>(w, q, hl);
+  H_PROBE(g_probe_e, 8, M / 64 - 1);
   if (!active) return;
   // ---- store: compare (prerepairSanityCheck), Repair fill, or plain ----
   const auto out_rsrc = make_rsrc(a.out + sq * a.out_sq_stride + vec * a.out_vec_stride);
@@ -1955,6 +1985,7 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
     __builtin_amdgcn_raw_buffer_store_b32(w.lo[j], out_rsrc, vout, so, 0);
     __builtin_amdgcn_raw_buffer_store_b32(w.hi[j], out_rsrc, vout + 32u, so, 0);
   }
+  H_PROBE(g_probe_e, 9, M / 64 - 1);
 }
 
 // Tables are module globals: upload once per device.
@@ -2424,12 +2455,16 @@ hipError_t launch_rs_decode(const DecodeArgs& a, hipStream_t s, bool mark_presen
 
 #ifdef DAGPU_PHASE_PROBE
 // probe builds only: op 0 clears the stamps, op 1 copies n of them to out
+// op 0: zero both buffers; 1: read the decoders' stamps; 2: the half-lane encoders'
 extern "C" int dagpu_debug_probe(int op, uint64_t* out, size_t n) {
   if (op == 0) {
     static uint64_t zero[8192 * 2 * dagpu::kProbePhases];
-    return (int)hipMemcpyToSymbol(HIP_SYMBOL(dagpu::g_probe), zero, sizeof zero);
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(dagpu::g_probe), zero, sizeof zero);
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dagpu::g_probe_e), zero, sizeof zero);
+    return (int)e;
   }
   if (n > 8192 * 2 * (size_t)dagpu::kProbePhases) n = 8192 * 2 * (size_t)dagpu::kProbePhases;
+  if (op == 2) return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(dagpu::g_probe_e), n * sizeof(uint64_t));
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(dagpu::g_probe), n * sizeof(uint64_t));
 }
 #endif

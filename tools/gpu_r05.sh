@@ -37,6 +37,13 @@ case "$1" in
     bash tools/gpu_ab.sh --rounds 2 "bench:--mode split --split-k 256 --steps 10 --warmup 2" new= nopf=lib:celestia-app_amd/libdagpu_nopf.so prev=lib:celestia-app_amd/libdagpu_prev.so && \
     bash tools/gpu_pmc_gf16.sh repair512 split512
     ;;
+  probe)  # round 5: phase probes of the half-lane kernels (libdagpu_probe.so, a -DDAGPU_PHASE_PROBE build), then the whole suite + default bench
+    for w in dec512h dec256h enc512h; do
+      timeout -k 10 300 python -u tools/phase_probe.py $w > gpurun_out/phase_probe_${w}_r05.log 2>&1 || { echo "probe $w failed"; tail -5 gpurun_out/phase_probe_${w}_r05.log; exit 1; }
+      cat gpurun_out/phase_probe_${w}_r05.log
+    done
+    bash tools/gpu_final.sh
+    ;;
   final-a)  # round end, part 1: the whole -m gpu suite, the default bench line and its rocprofv3 kernel trace
     bash tools/gpu_final.sh
     ;;

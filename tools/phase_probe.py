@@ -2,7 +2,8 @@
 library: lane 0 of two waves of every workgroup stamps s_memtime (shader
 clocks) at the phase boundaries; this prints the mean clocks per phase over the
 workgroups of one Repair.
-  dec512: leo16_decode_reg1k_kernel (k = 512, waves 0 and 15)
+  dec512: leo16_decode_reg1k_kernel (k = 512, waves 0 and 15; DAGPU_DEC1K_PACKED=1)
+  dec512h / dec256h / enc512h: the round-5 half-lane kernels
   dec128: leo8_decode128_sliced_kernel (k = 128, waves 0 and 3)
     (build: make -C <copy of celestia-app_amd> libdagpu.so HIPFLAGS="... -DDAGPU_PHASE_PROBE",
      copy it to celestia-app_amd/libdagpu_probe.so)
@@ -28,6 +29,19 @@ KERNELS = {
                    names=["tables built", "premultiply", "IFFT block (bits 0-5)", "transpose 1", "IFFT bits 6-9",
                           "derivative", "FFT bits 9-6", "transpose 2", "FFT block (bits 5-0)",
                           "postmultiply + stores"]),
+    # round 5: the half-lane GF(2^16) kernels (rs_gf16.hip H_PROBE; op 1 = decoder stamps, op 2 = encoder)
+    "dec512h": dict(fn="dagpu_debug_probe", op=1, P=14, k=512, n=2, waves=("wave 0", "wave 15"),
+                    names=["tables, loads", "premultiply", "IFFT bit 0 (S) + swap", "IFFT bits 1-5 (B)",
+                           "transpose 1", "IFFT bits 6-9 (T)", "derivative", "FFT bits 9-6 (T)", "transpose 2",
+                           "FFT bits 5-1 (B)", "swap + FFT bit 0 (S)", "postmultiply + stores"]),
+    "dec256h": dict(fn="dagpu_debug_probe", op=1, P=14, k=256, n=8, waves=("wave 0", "wave 7"),
+                    names=["tables, loads", "premultiply", "IFFT bit 0 (S) + swap", "IFFT bits 1-5 (B)",
+                           "transpose 1", "IFFT bits 6-8 (T)", "derivative", "FFT bits 8-6 (T)", "transpose 2",
+                           "FFT bits 5-1 (B)", "swap + FFT bit 0 (S)", "postmultiply + stores"]),
+    "enc512h": dict(fn="dagpu_debug_probe", op=2, P=14, split=512, waves=("wave 0", "wave 7"),
+                    names=["loads (+ copy, given)", "IFFT bit 0 (S) + swap", "IFFT bits 1-5 (B)", "transpose 1",
+                           "IFFT 6-7, merged 8, FFT 7-6 (T)", "transpose 2", "FFT bits 5-1 (B)",
+                           "swap + FFT bit 0 (S)", "stores"]),
     "dec128": dict(fn="dagpu_debug_probe8", P=14, k=128, n=256, waves=("wave 0", "wave 3"),
                    names=["tables, loads, premultiply, transpose8", "IFFT layers 0-1 (A)", "transpose A->A*",
                           "IFFT layers 2-3 (A*)", "exchange A*->B", "IFFT layers 4-7 (B)", "derivative",
@@ -45,14 +59,20 @@ def main():
     L = _abi.lib()
     fn = getattr(L, kern["fn"])
     fn.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]
-    bench.run_repair(ctx, kern["k"], kern["n"], 1, 1)  # warm
-    torch.cuda.synchronize()
-    fn(0, None, 0)
-    bench.run_repair(ctx, kern["k"], kern["n"], 1, 0)
+    if "split" in kern:  # the split square at P = 1 (its row and column encodes)
+        bench.bench_split(None, 0, 1, 0, ctx, kern["split"], 1, 1)
+        torch.cuda.synchronize()
+        fn(0, None, 0)
+        bench.bench_split(None, 0, 1, 0, ctx, kern["split"], 1, 0)
+    else:
+        bench.run_repair(ctx, kern["k"], kern["n"], 1, 1)  # warm
+        torch.cuda.synchronize()
+        fn(0, None, 0)
+        bench.run_repair(ctx, kern["k"], kern["n"], 1, 0)
     torch.cuda.synchronize()
     n = 8192 * 2 * P
     buf = np.zeros(n, np.uint64)
-    fn(1, buf.ctypes.data, n)
+    fn(kern.get("op", 1), buf.ctypes.data, n)
     st = buf.reshape(8192, 2, P).astype(np.int64)
     for wv, label in enumerate(kern["waves"]):
         s = st[:, wv, :]
