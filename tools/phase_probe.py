@@ -5,8 +5,9 @@ workgroups of one Repair.
   dec512: leo16_decode_reg1k_kernel (k = 512, waves 0 and 15; DAGPU_DEC1K_PACKED=1)
   dec512h / dec256h / enc512h: the round-5 half-lane kernels
   dec128: leo8_decode128_sliced_kernel (k = 128, waves 0 and 3)
-    (build: make -C <copy of celestia-app_amd> libdagpu.so HIPFLAGS="... -DDAGPU_PHASE_PROBE",
-     copy it to celestia-app_amd/libdagpu_probe.so)
+    (build: copy celestia-app_amd AND include/ side by side (the Makefile reads
+     ../include/dagpu.h), make -C <copy>/celestia-app_amd libdagpu.so HIPFLAGS="... -DDAGPU_PHASE_PROBE",
+     check `nm -D` shows dagpu_debug_probe, copy it to celestia-app_amd/libdagpu_probe.so)
     python tools/phase_probe.py [dec512|dec128]
 """
 import ctypes
