@@ -1724,7 +1724,10 @@ __device__ __forceinline__ void derivative_t(W32& w, uint32_t* lds, int c, int l
 // LR = 2: 512 threads at <= 128 VGPRs and 64 KiB of LDS, two workgroups per CU).
 template <int K>
 constexpr size_t dec_h_lds_bytes() { return (size_t)2 * (2 * K) * 16 * sizeof(uint32_t); }
-template <int K>
+// SKIP: a missing shard's load gets an out-of-range voffset (the buffer
+// returns 0 without touching memory), halving a maximal-erasure vector's
+// load traffic; its premultiply table is zero either way.
+template <int K, bool SKIP = true>
 __global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_decode_h_kernel(
     DecodeArgs a) {
   constexpr int NQ = K / 32, LR = K == 512 ? 1 : 2, RPR = K == 512 ? 1 : 2;
@@ -1759,13 +1762,16 @@ __global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   mul16_table_to(post_tab + threadIdx.x * 16, kMod16 - my_err, (pm >> lane) & 1);
   W32 w;
   const int q_ld = opaque_s(q);
+  const uint32_t pmh_ld = hl ? (uint32_t)(pm >> 32) : (uint32_t)pm;
 #pragma unroll
   for (int j = 0; j < 32; j++) {
     const int i = 64 * q_ld + s_local(j, 0);
     const int shard = i < K ? K + i : i - K;
     const uint32_t so = (uint32_t)shard * (uint32_t)a.shard_stride;
-    w.lo[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, so, 0);
-    w.hi[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff + 32u, so, 0);
+    // missing: voffset >= 2^31 > num_records (soffset < 2^30 here), so out of range
+    const uint32_t vj = (!SKIP || ((pmh_ld >> s_local(j, 0)) & 1)) ? voff : (voff | 0x80000000u);
+    w.lo[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, vj, so, 0);
+    w.hi[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, vj + 32u, so, 0);
   }
   __syncthreads();
   H_PROBE(g_probe, 1, NQ - 1);
@@ -2213,16 +2219,23 @@ static hipError_t dec_lds_attr() {  // above the 64 KiB default: once per proces
     if (err == hipSuccess)
       err = hipFuncSetAttribute((const void*)leo16_decode_reg1k_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDec1kLds);
-    if (err == hipSuccess)
-      err = hipFuncSetAttribute((const void*)leo16_decode_h_kernel<512>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)dec_h_lds_bytes<512>());
-    if (err == hipSuccess)
-      err = hipFuncSetAttribute((const void*)leo16_decode_h_kernel<256>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)dec_h_lds_bytes<256>());
+    const void* h512[2] = {(const void*)leo16_decode_h_kernel<512, false>, (const void*)leo16_decode_h_kernel<512, true>};
+    const void* h256[2] = {(const void*)leo16_decode_h_kernel<256, false>, (const void*)leo16_decode_h_kernel<256, true>};
+    for (int i = 0; i < 2 && err == hipSuccess; i++) {
+      err = hipFuncSetAttribute(h512[i], hipFuncAttributeMaxDynamicSharedMemorySize, (int)dec_h_lds_bytes<512>());
+      if (err == hipSuccess)
+        err = hipFuncSetAttribute(h256[i], hipFuncAttributeMaxDynamicSharedMemorySize, (int)dec_h_lds_bytes<256>());
+    }
   });
   return err;
 }
 
+// half-lane decoders: DAGPU_DEC_LOADALL=1 loads missing shards too (A/B of the
+// out-of-range skip)
+static bool dec_load_all() {
+  const char* e = getenv("DAGPU_DEC_LOADALL");
+  return e && e[0] == '1';
+}
 // k = 256 decoder: the half-lane kernel (round 5); DAGPU_DEC256_REG=1 selects
 // leo16_decode_reg_kernel (A/B)
 static bool dec256_reg() {
@@ -2248,8 +2261,12 @@ hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mar
     DecodeArgs b = a;
     b.nchunk = a.shard_bytes / 256;
     if ((e = dec_lds_attr()) != hipSuccess) return e;
-    hipLaunchKernelGGL(leo16_decode_h_kernel<256>, dim3((unsigned)(nv * b.nchunk)), dim3(512),
-                       dec_h_lds_bytes<256>(), s, b);
+    if (dec_load_all())
+      hipLaunchKernelGGL((leo16_decode_h_kernel<256, false>), dim3((unsigned)(nv * b.nchunk)), dim3(512),
+                         dec_h_lds_bytes<256>(), s, b);
+    else
+      hipLaunchKernelGGL((leo16_decode_h_kernel<256, true>), dim3((unsigned)(nv * b.nchunk)), dim3(512),
+                         dec_h_lds_bytes<256>(), s, b);
   } else if (a.k == kDecN / 2) {  // register-resident decoder; nchunk = 512-B chunks of the shard
     DecodeArgs b = a;
     b.nchunk = (a.shard_bytes + 511) / 512;
@@ -2262,8 +2279,12 @@ hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mar
     if (dec1k_packed())
       hipLaunchKernelGGL(leo16_decode_reg1k_kernel, dim3((unsigned)(nv * b.nchunk)), dim3(kDec1k), kDec1kLds, s, b);
     else
-      hipLaunchKernelGGL(leo16_decode_h_kernel<512>, dim3((unsigned)(nv * b.nchunk)), dim3(1024),
-                         dec_h_lds_bytes<512>(), s, b);
+      if (dec_load_all())
+        hipLaunchKernelGGL((leo16_decode_h_kernel<512, false>), dim3((unsigned)(nv * b.nchunk)), dim3(1024),
+                           dec_h_lds_bytes<512>(), s, b);
+      else
+        hipLaunchKernelGGL((leo16_decode_h_kernel<512, true>), dim3((unsigned)(nv * b.nchunk)), dim3(1024),
+                           dec_h_lds_bytes<512>(), s, b);
   } else
 #endif
   {

@@ -44,6 +44,12 @@ case "$1" in
     done
     bash tools/gpu_final.sh
     ;;
+  skip)  # round 5: half-lane decoders skip the loads of missing shards (out-of-range voffset): tests, A/B vs DAGPU_DEC_LOADALL=1
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_gf16.py tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py tests/test_gpu_repair_async.py > gpurun_out/r05_skip_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r05_skip_tests.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 3 repair512 skip= all=DAGPU_DEC_LOADALL=1 && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 256 --batch 8 --steps 5 --warmup 1" skip= all=DAGPU_DEC_LOADALL=1
+    ;;
   final-a)  # round end, part 1: the whole -m gpu suite, the default bench line and its rocprofv3 kernel trace
     bash tools/gpu_final.sh
     ;;
