@@ -526,8 +526,9 @@ def main():
             "repair_k512_gf16_q3": run_repair(ctx, 512, 2, 2, 1, pattern="q3"),
             # configs[4] stress square through the split path at P = 1 (the N > 1 line
             # carries the same square split over every rank as split_stress)
-            "configs[4]_split_k256": bench_split(None, 0, 1, local, ctx, 256, 5, 1),
-            "configs[4]_split_k512": bench_split(None, 0, 1, local, ctx, 512, 5, 1),
+            # 20 steps: at 5 the first step's launch latency was ~7 % of a 1.4-ms square
+            "configs[4]_split_k256": bench_split(None, 0, 1, local, ctx, 256, 20, 3),
+            "configs[4]_split_k512": bench_split(None, 0, 1, local, ctx, 512, 20, 3),
         }
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.cpu_threads or host_threads())

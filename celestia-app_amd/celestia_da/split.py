@@ -169,7 +169,8 @@ def extend_split_distributed(dist, part: SplitPart, ods_rows: torch.Tensor, grou
     col_all = torch.empty(part.parts * part.col_roots.numel(), dtype=torch.uint8, device=part.slab.device)
     all_gather_flat(dist, row_sub_all, part.row_sub, group)
     all_gather_flat(dist, col_all, part.col_roots, group)
-    status = max_status(dist, part.status, group)
     rr, dah = part.step_finish(row_sub_all, col_all, stream)
+    # the status read-back is this step's one host wait, after all of it is queued
+    status = max_status(dist, part.status, group)
     _check_status(status)
     return rr, col_all, dah

@@ -550,7 +550,7 @@ int dagpu_roots_device(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_ed
                        (hipStream_t)stream);
 }
 
-namespace {
+extern "C++" {  // external C++ helpers (runtime.hpp): split.cpp forks onto the side streams too
 
 hipEvent_t ev_take(dagpu_ctx* c) {
   std::lock_guard<std::mutex> g(c->ev_mu);
@@ -590,7 +590,7 @@ size_t pipe_slices(dagpu_ctx* ctx, uint32_t k, size_t n) {
 
 // The side streams paired with caller stream `s` (created on first use).
 // which: 0 = RS, 1 = RS at the device's greatest stream priority, 2 = NMT.
-hipStream_t side_stream(dagpu_ctx* ctx, hipStream_t s, int which = 0) {
+hipStream_t side_stream(dagpu_ctx* ctx, hipStream_t s, int which) {
   std::lock_guard<std::mutex> g(ctx->side_mu);
   dagpu_ctx::Side* sd = nullptr;
   for (auto& p : ctx->side)
@@ -625,7 +625,7 @@ hipStream_t side_stream(dagpu_ctx* ctx, hipStream_t s, int which = 0) {
   return *slot;
 }
 
-}  // namespace
+}  // extern "C++"
 
 int dagpu_extend_batch_device(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_ods,
                               uint8_t* d_eds, uint8_t* d_row_roots, uint8_t* d_col_roots,

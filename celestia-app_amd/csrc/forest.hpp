@@ -104,8 +104,9 @@ struct ForestPlan {
 // Enqueue every inner level and the roots of plan `p` on stream s.
 //   d_leaves  level-0 records (rec = 96 B NMT / 32 B RFC-6962)
 //   d_inner   p.inner_records records
-//   d_meta    p.meta.size() int64 (uploaded here; keep `p` alive until the
-//             stream has passed this point)
+//   d_meta    p.meta.size() int64 (ragged plans: uploaded here, keep `p` alive
+//             until the stream has passed this point; uniform plans upload
+//             nothing and need neither)
 //   d_status  per-tree status (check_order), may be null otherwise
 //   d_roots   ntrees roots (90 B packed / 96 B records / 32 B digests)
 hipError_t forest_enqueue(const ForestPlan& p, const uint8_t* d_leaves, uint8_t* d_inner, int64_t* d_meta,

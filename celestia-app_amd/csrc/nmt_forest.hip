@@ -254,10 +254,25 @@ __device__ __forceinline__ void forest_level_node(const ForestLevelArgs& a, long
     if (bad) atomicOr(&a.status[t], kForestPushOrder);
   }
   uint32_t st[8];
-  auto get = [&](int P, int i) -> uint32_t {
-    return P == 0 ? lmn[i] : P == 1 ? lmx[i] : P == 2 ? ld[i] : P == 3 ? rmn[i] : P == 4 ? rmx[i] : rd[i];
-  };
-  sha_node_msg(get, st);
+  // A min namespace equal to the parity namespace (the largest) makes the max
+  // the parity namespace too.  Waves whose children all carry it (the parity
+  // quadrants of a wrapper square / split slab) hash with constant namespace
+  // words, as nmt_level_kernel does.
+  const bool lpar = ns_is_parity(lmn), rpar = ns_is_parity(rmn);
+  if (__all(lpar && rpar)) {
+    auto get = [&](int P, int i) -> uint32_t { return P == 2 ? ld[i] : P == 5 ? rd[i] : 0xFFFFFFFFu; };
+    sha_node_msg<true, true, true>(get, st);
+  } else if (__all(lpar)) {
+    auto get = [&](int P, int i) -> uint32_t {
+      return P <= 1 ? 0xFFFFFFFFu : P == 2 ? ld[i] : P == 3 ? rmn[i] : P == 4 ? rmx[i] : rd[i];
+    };
+    sha_node_msg<true>(get, st);
+  } else {
+    auto get = [&](int P, int i) -> uint32_t {
+      return P == 0 ? lmn[i] : P == 1 ? lmx[i] : P == 2 ? ld[i] : P == 3 ? rmn[i] : P == 4 ? rmx[i] : rd[i];
+    };
+    sha_node_msg(get, st);
+  }
   uint32_t dg[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) dg[i] = bswap32(st[i]);
@@ -284,10 +299,13 @@ __global__ __launch_bounds__(256) void forest_level2_kernel(ForestLevelArgs a, F
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void forest_roots_kernel(const uint8_t* leaves, const uint8_t* inner,
                                                            const int64_t* root_idx, long ntrees, int rfc,
-                                                           int records, uint8_t* out, long stride) {
+                                                           int records, uint8_t* out, long stride,
+                                                           int64_t ubase, long utstride) {
   const long t = (long)blockIdx.x * 256 + threadIdx.x;
   if (t >= ntrees) return;
-  const int64_t ix = root_idx[t];
+  // uniform plan (root_idx null): ubase >= 0 -> inner record ubase + t;
+  // -2 -> leaf t * utstride (single-leaf trees); -1 -> empty trees
+  const int64_t ix = root_idx ? root_idx[t] : ubase >= 0 ? ubase + t : ubase == -2 ? -(t * utstride) - 2 : -1;
   const int rec = rfc ? kRecRfc : kRecNmt;
   uint32_t mn[8], mx[8], dg[8];
   if (ix == -1) {  // empty tree: SHA256("")
@@ -331,7 +349,20 @@ hipError_t launch_forest_roots(const uint8_t* leaves, const uint8_t* inner, cons
   if (ntrees <= 0) return hipSuccess;
   if (out_stride == 0) out_stride = rfc ? kRecRfc : records ? kRecNmt : kNodeSize;
   hipLaunchKernelGGL(forest_roots_kernel, dim3((unsigned)((ntrees + 255) / 256)), dim3(256), 0, s, leaves,
-                     inner, root_idx, ntrees, rfc, records, out, out_stride);
+                     inner, root_idx, ntrees, rfc, records, out, out_stride, (int64_t)-1, 0L);
+  return hipGetLastError();
+}
+
+// Roots of a uniform plan from its shape alone: nothing to upload, so the
+// caller's host plan need not outlive the enqueue.
+static hipError_t launch_forest_roots_uniform(const ForestPlan& p, const uint8_t* leaves, const uint8_t* inner,
+                                              int rfc, int records, uint8_t* out, long out_stride,
+                                              hipStream_t s) {
+  if (p.ntrees <= 0) return hipSuccess;
+  if (out_stride == 0) out_stride = rfc ? kRecRfc : records ? kRecNmt : kNodeSize;
+  const int64_t ubase = p.per0 == 0 ? -1 : p.nlevels == 0 ? -2 : (int64_t)p.base[p.nlevels];
+  hipLaunchKernelGGL(forest_roots_kernel, dim3((unsigned)((p.ntrees + 255) / 256)), dim3(256), 0, s, leaves,
+                     inner, (const int64_t*)nullptr, p.ntrees, rfc, records, out, out_stride, ubase, p.tstride0);
   return hipGetLastError();
 }
 
@@ -507,13 +538,16 @@ hipError_t forest_enqueue(const ForestPlan& p, const uint8_t* d_leaves, uint8_t*
                           int ignore_max, int check_order, int rfc, int32_t* d_status, uint8_t* d_roots,
                           int records, long roots_stride, hipStream_t s) {
   if (p.ntrees == 0) return hipSuccess;
-  hipError_t e = hipMemcpyAsync(d_meta, p.meta.data(), p.meta.size() * sizeof(int64_t),
-                                hipMemcpyHostToDevice, s);
-  if (e != hipSuccess) return e;
+  hipError_t e = hipSuccess;
+  if (!p.uniform) {  // uniform plans address their levels and roots by shape
+    e = hipMemcpyAsync(d_meta, p.meta.data(), p.meta.size() * sizeof(int64_t), hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return e;
+  }
   for (int L = 1; L <= p.nlevels; L++) {
     e = launch_forest_level(level_args(p, L, d_leaves, d_inner, d_meta, ignore_max, check_order, rfc, d_status), s);
     if (e != hipSuccess) return e;
   }
+  if (p.uniform) return launch_forest_roots_uniform(p, d_leaves, d_inner, rfc, records, d_roots, roots_stride, s);
   return launch_forest_roots(d_leaves, d_inner, d_meta + p.meta_root, p.ntrees, rfc, records, d_roots,
                              roots_stride, s);
 }
@@ -521,7 +555,7 @@ hipError_t forest_enqueue(const ForestPlan& p, const uint8_t* d_leaves, uint8_t*
 hipError_t forest_enqueue_pair(const ForestJob& x, const ForestJob& y, hipStream_t s) {
   const ForestJob* j[2] = {&x, &y};
   for (int f = 0; f < 2; f++) {
-    if (j[f]->p->ntrees == 0) continue;
+    if (j[f]->p->ntrees == 0 || j[f]->p->uniform) continue;
     hipError_t e = hipMemcpyAsync(j[f]->d_meta, j[f]->p->meta.data(), j[f]->p->meta.size() * sizeof(int64_t),
                                   hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return e;
@@ -547,6 +581,12 @@ hipError_t forest_enqueue_pair(const ForestJob& x, const ForestJob& y, hipStream
   for (int f = 0; f < 2; f++) {
     const ForestJob& q = *j[f];
     if (q.p->ntrees == 0) continue;
+    if (q.p->uniform) {
+      hipError_t e = launch_forest_roots_uniform(*q.p, q.d_leaves, q.d_inner, q.rfc, q.records, q.d_roots,
+                                                 q.roots_stride, s);
+      if (e != hipSuccess) return e;
+      continue;
+    }
     hipError_t e = launch_forest_roots(q.d_leaves, q.d_inner, q.d_meta + q.p->meta_root, q.p->ntrees, q.rfc,
                                        q.records, q.d_roots, q.roots_stride, s);
     if (e != hipSuccess) return e;

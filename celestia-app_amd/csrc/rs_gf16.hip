@@ -1720,10 +1720,69 @@ __device__ __forceinline__ void derivative_t(W32& w, uint32_t* lds, int c, int l
   }
 }
 
+// ONE product table per element, in the 3/3/2 format of mul16x_add_t (round 5):
+// exp(errLoc) for a present element (premultiply), exp(-errLoc) for a missing
+// one (postmultiply).  A missing element's loaded bytes are zero (or zeroed)
+// and a present one is never stored, so neither needs the other table.  From
+// the 16 products pb[b] = (1 << b) * exp(lm): a 3-bit group's entries 0..3 are
+// (0, p0, p1, p0 ^ p1) and entries 4..7 those XOR p2 (GF(2)-linear multiply).
+__device__ __forceinline__ void mul16x_table_to(uint32_t* out, uint32_t lm) {
+  uint32_t pb[16];
+#pragma unroll
+  for (int b = 0; b < 16; b++) {
+    uint32_t sidx = (uint32_t)g_logbit16[b] + lm;
+    sidx = (sidx + (sidx >> 16)) & 0xFFFFu;
+    pb[b] = g_exp16[sidx];
+  }
+  uint32_t t[kTab16x];
+  // entries 0..3 of a group over basis products p0, p1: low bytes, high bytes
+  auto quad = [&](uint32_t p0, uint32_t p1, uint32_t& lo, uint32_t& hi) {
+    const uint32_t q = p0 ^ p1;
+    lo = __builtin_amdgcn_perm(q, __builtin_amdgcn_perm(p1, p0, 0x0C04000Cu), 0x04020100u);
+    hi = __builtin_amdgcn_perm(q, __builtin_amdgcn_perm(p1, p0, 0x0C05010Cu), 0x05020100u);
+  };
+  auto grp3 = [&](int b0, int base) {
+    uint32_t lo, hi;
+    quad(pb[b0], pb[b0 + 1], lo, hi);
+    t[base] = lo;
+    t[base + 1] = lo ^ __builtin_amdgcn_perm(pb[b0 + 2], pb[b0 + 2], 0x00000000u);
+    t[base + 2] = hi;
+    t[base + 3] = hi ^ __builtin_amdgcn_perm(pb[b0 + 2], pb[b0 + 2], 0x01010101u);
+  };
+  auto grp2 = [&](int b0, int base) { quad(pb[b0], pb[b0 + 1], t[base], t[base + 1]); };
+  grp3(0, 0);
+  grp3(3, 4);
+  grp2(6, 8);
+  grp3(8, 10);
+  grp3(11, 14);
+  grp2(14, 18);
+  uint4* o = (uint4*)out;
+#pragma unroll
+  for (int i = 0; i < kTab16x / 4; i++) o[i] = make_uint4(t[4 * i], t[4 * i + 1], t[4 * i + 2], t[4 * i + 3]);
+}
+__device__ __forceinline__ void mul16x_table_from(const uint32_t* tab, int e, uint32_t (&t)[kTab16x]) {
+  const uint4* q = (const uint4*)(tab + e * kTab16x);
+#pragma unroll
+  for (int h = 0; h < kTab16x / 4; h++) {
+    const uint4 v = q[h];
+    t[4 * h] = v.x;
+    t[4 * h + 1] = v.y;
+    t[4 * h + 2] = v.z;
+    t[4 * h + 3] = v.w;
+  }
+}
+// (xl, xh) *= the table's multiplier
+__device__ __forceinline__ void mul16x_by(uint32_t& xl, uint32_t& xh, const uint32_t (&t)[kTab16x]) {
+  uint32_t zl = 0u, zh = 0u;
+  mul16x_add_t(zl, zh, xl, xh, t);
+  xl = zl;
+  xh = zh;
+}
+
 // K = 512 (n = 1024, 16 waves, LR = 1) and, round 5, K = 256 (n = 512, 8 waves,
 // LR = 2: 512 threads at <= 128 VGPRs and 64 KiB of LDS, two workgroups per CU).
 template <int K>
-constexpr size_t dec_h_lds_bytes() { return (size_t)2 * (2 * K) * 16 * sizeof(uint32_t); }
+constexpr size_t dec_h_lds_bytes() { return (size_t)(2 * K) * (16 + kTab16x) * sizeof(uint32_t); }
 // SKIP: a missing shard's load gets an out-of-range voffset (the buffer
 // returns 0 without touching memory), halving a maximal-erasure vector's
 // load traffic; its premultiply table is zero either way.
@@ -1731,12 +1790,13 @@ template <int K, bool SKIP = true>
 __global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_decode_h_kernel(
     DecodeArgs a) {
   constexpr int NQ = K / 32, LR = K == 512 ? 1 : 2, RPR = K == 512 ? 1 : 2;
-  // dynamic LDS (dec_h_lds_bytes): [0, n x 64 B) premultiply tables, then the
-  // transposes and the derivative staging (each <= n x 64 B); [n x 64 B, 2 n x 64 B)
-  // the erased elements' tables
+  // dynamic LDS (dec_h_lds_bytes): [0, n x 64 B) the transposes and the
+  // derivative staging (each <= n x 64 B); then n x 80 B of per-element tables
+  // (mul16x_table_to: the premultiply's for present, the postmultiply's for
+  // missing elements)
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn_lds[];
   uint32_t* lds = dyn_lds;
-  uint32_t* post_tab = dyn_lds + 2 * K * 16;
+  uint32_t* tab = dyn_lds + 2 * K * 16;
   const long blk = blockIdx.x;
   const int piece = (int)(blk % a.nchunk);  // nchunk = 256-B pieces of the shard
   const long v = blk / a.nchunk;
@@ -1753,13 +1813,13 @@ __global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   const auto rsrc = make_rsrc(a.data + sq * a.sq_stride + vec * a.vec_stride);
   const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
   const uint16_t* err = (const uint16_t*)(a.err + err_vec(a, v) * rs_err_bytes(K));
-  // thread t builds element t's tables (pre: zero if missing; post: read for missing only)
+  // thread t builds element t's table
   const int my_i = 64 * q + lane;
   const int my_shard = my_i < K ? K + my_i : my_i - K;
-  const uint64_t pm = __builtin_amdgcn_ballot_w64(pres[(long)my_shard * a.p_shard_stride] != 0);
+  const bool my_present = pres[(long)my_shard * a.p_shard_stride] != 0;
+  const uint64_t pm = __builtin_amdgcn_ballot_w64(my_present);
   const uint32_t my_err = err[my_i];
-  mul16_table_to(lds + threadIdx.x * 16, my_err, !((pm >> lane) & 1));
-  mul16_table_to(post_tab + threadIdx.x * 16, kMod16 - my_err, (pm >> lane) & 1);
+  mul16x_table_to(tab + threadIdx.x * kTab16x, my_present ? my_err : kMod16 - my_err);
   W32 w;
   const int q_ld = opaque_s(q);
   const uint32_t pmh_ld = hl ? (uint32_t)(pm >> 32) : (uint32_t)pm;
@@ -1778,15 +1838,19 @@ __global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   const int q_pm = opaque_s(q);
 #pragma unroll
   for (int j = 0; j < 32; j++) {
-    uint32_t t[16];
-    mul16_table_from(lds, 64 * q_pm + s_local(j, 0) + 32 * hl, t);
+    uint32_t t[kTab16x];
+    mul16x_table_from(tab, 64 * q_pm + s_local(j, 0) + 32 * hl, t);
     uint32_t xl = w.lo[j], xh = w.hi[j];
-    mul16_by(xl, xh, t);
+    if constexpr (!SKIP) {  // a missing element's loaded bytes are not zero here
+      const bool p = (pmh_ld >> s_local(j, 0)) & 1;
+      xl = p ? xl : 0u;
+      xh = p ? xh : 0u;
+    }
+    mul16x_by(xl, xh, t);
     asm volatile("" : "+v"(xl), "+v"(xh));  // one element's table live at a time
     w.lo[j] = xl;
     w.hi[j] = xh;
   }
-  __syncthreads();  // the transposes reuse the premultiply tables' LDS
   H_PROBE(g_probe, 2, NQ - 1);
   // ---- IFFT (ifftDITDecoder, skew index iend - 1) ----
   layer0_s<true>(w, q, hl);
@@ -1834,10 +1898,10 @@ __global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   for (int j = 0; j < 32; j++) {
     const int l0 = s_local(j, 0);
     if (((pm_e >> l0) & 1) && ((pm_e >> (l0 + 32)) & 1)) continue;  // uniform
-    uint32_t t[16];
-    mul16_table_from(post_tab, 64 * q_e + l0 + 32 * hl, t);
+    uint32_t t[kTab16x];
+    mul16x_table_from(tab, 64 * q_e + l0 + 32 * hl, t);
     uint32_t xl = w.lo[j], xh = w.hi[j];
-    mul16_by(xl, xh, t);
+    mul16x_by(xl, xh, t);
     asm volatile("" : "+v"(xl), "+v"(xh));
     const int i = 64 * q_e + l0;
     const int shard = i < K ? K + i : i - K;

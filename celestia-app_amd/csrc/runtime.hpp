@@ -210,6 +210,14 @@ inline bool& on_repair_worker() {
   return w;
 }
 
+// dagpu.cpp: timing-disabled events recycled per call, and the side streams
+// paired with a caller stream (which: 0 RS, 1 RS at the greatest priority, 2 NMT).
+hipEvent_t ev_take(dagpu_ctx* c);
+void ev_give(dagpu_ctx* c, hipEvent_t e);
+hipStream_t side_stream(dagpu_ctx* ctx, hipStream_t s, int which = 0);
+long env_long(const char* name);
+size_t pipe_slices(dagpu_ctx* ctx, uint32_t k, size_t n);
+
 inline hipEvent_t pool_get(dagpu_ctx* c) {
   if (!c->pool.empty()) {
     hipEvent_t e = c->pool.back();

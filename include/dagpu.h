@@ -353,7 +353,8 @@ int dagpu_blob_commitments(dagpu_ctx* ctx, size_t nblobs, const uint8_t* namespa
  *   4 all-gather row-subtree records (P x 2k x 96 B, rank order) and column
  *     roots (2k x 90 B, column order); max-reduce the status words
  *   5 dagpu_split_finish_device row roots (2k x 90 B) and the DAH (32 B)
- * Steps 3 and 5 synchronise `stream` before returning.  With P = 1 the one
+ * Every step only enqueues on `stream` (nothing is read from host memory):
+ * synchronise it before reading the results.  With P = 1 the one
  * send block is rows 0..k-1 of the slab: pass the slab itself as d_send and
  * skip step 2 (the encoder then writes [Q0 | Q1] in place).
  * d_workspace: dagpu_split_workspace_size(k, P) bytes (0 = invalid k / P). */

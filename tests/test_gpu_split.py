@@ -47,6 +47,20 @@ def test_split_local_matches_oracle(ctx, k, parts):
     assert got_dah == dah
 
 
+@pytest.mark.parametrize("mode", ["0", "1", "2"])
+@pytest.mark.parametrize("k,parts", [(2, 2), (64, 1), (512, 1), (512, 4)])
+def test_split_overlap_modes(ctx, monkeypatch, k, parts, mode):
+    """DAGPU_SPLIT_OVERLAP (column encode on a side stream beside the leaves of
+    rows 0..k-1; 0 = one stream) gives the oracle's roots and DAH; (2, 2) has
+    single-leaf top trees (uniform roots addressed by shape, nothing uploaded)."""
+    monkeypatch.setenv("DAGPU_SPLIT_OVERLAP", mode)
+    ods, rr, cr, dah = _want(k, 7100 + k)
+    d = torch.from_numpy(np.ascontiguousarray(ods).reshape(-1)).cuda()
+    for _ in range(2):  # the second run reuses the side stream and pooled events
+        got_rr, got_cr, got_dah = split.extend_split_local(d, k, parts, ctx)
+        assert (got_rr, got_cr, got_dah) == (rr, cr, dah)
+
+
 def test_split_push_order(ctx):
     k = 16
     ods = np.ascontiguousarray(synth.random_blob_square(k, 5)).reshape(k, k, 512).copy()

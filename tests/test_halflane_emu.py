@@ -285,3 +285,90 @@ def test_halflane_encoder_equals_leopard_loops(m, rev):
     swap_sb(R)
     layer0_s(R, fo, False)
     assert gather(R, e_s) == ref
+
+
+# ---- the decoders' per-element 3/3/2 product table (mul16x_table_to) --------
+
+def perm(hi: int, lo: int, sel: int) -> int:
+    """v_perm_b32 (__builtin_amdgcn_perm(hi, lo, sel)): selector byte 0-3 picks
+    a byte of lo, 4-7 of hi, 0x0C gives 0x00 (the only other value used)."""
+    src = lo | (hi << 32)
+    out = 0
+    for i in range(4):
+        s = (sel >> (8 * i)) & 0xFF
+        b = 0 if s == 0x0C else (src >> (8 * s)) & 0xFF
+        assert s <= 7 or s == 0x0C
+        out |= b << (8 * i)
+    return out
+
+
+def table332_device(lm: int):
+    """mul16x_table_to: the 16 products (1 << b) * exp(lm), then each group's
+    entries by XOR and v_perm byte packing."""
+    pb = [mul(1 << b, lm) for b in range(16)]
+    t = [0] * 20
+
+    def quad(p0, p1):
+        q = p0 ^ p1
+        lo = perm(q, perm(p1, p0, 0x0C04000C), 0x04020100)
+        hi = perm(q, perm(p1, p0, 0x0C05010C), 0x05020100)
+        return lo, hi
+
+    def grp3(b0, base):
+        lo, hi = quad(pb[b0], pb[b0 + 1])
+        t[base] = lo
+        t[base + 1] = lo ^ perm(pb[b0 + 2], pb[b0 + 2], 0x00000000)
+        t[base + 2] = hi
+        t[base + 3] = hi ^ perm(pb[b0 + 2], pb[b0 + 2], 0x01010101)
+
+    def grp2(b0, base):
+        t[base], t[base + 1] = quad(pb[b0], pb[b0 + 1])
+
+    grp3(0, 0)
+    grp3(3, 4)
+    grp2(6, 8)
+    grp3(8, 10)
+    grp3(11, 14)
+    grp2(14, 18)
+    return t
+
+
+def table332_host(lm: int):
+    """The host builder's definition (ensure_tables tab332): entry e2 of group g
+    = (e2 << shift) * c, low byte in the lo pool, high byte in the hi pool."""
+    t = [0] * 20
+    shift, width, base = [0, 3, 6, 8, 11, 14], [3, 3, 2, 3, 3, 2], [0, 4, 8, 10, 14, 18]
+    for g in range(6):
+        for e2 in range(1, 1 << width[g]):
+            prod = mul(e2 << shift[g], lm)
+            lo_dw = base[g] + (e2 >> 2) if width[g] == 3 else base[g]
+            hi_dw = base[g] + 2 + (e2 >> 2) if width[g] == 3 else base[g] + 1
+            t[lo_dw] |= (prod & 0xFF) << (8 * (e2 & 3))
+            t[hi_dw] |= ((prod >> 8) & 0xFF) << (8 * (e2 & 3))
+    return t
+
+
+def mul16x(ylo: int, yhi: int, t):
+    """mul16x_add_t with zero accumulators (mul16x_by) on 4 symbols: symbol i =
+    byte i of ylo (low) | byte i of yhi (high)."""
+    s = [ylo & 0x07070707, (ylo >> 3) & 0x07070707, (ylo >> 6) & 0x03030303,
+         yhi & 0x07070707, (yhi >> 3) & 0x07070707, (yhi >> 6) & 0x03030303]
+    lo = (perm(t[1], t[0], s[0]) ^ perm(t[5], t[4], s[1]) ^ perm(t[8], t[8], s[2]) ^
+          perm(t[11], t[10], s[3]) ^ perm(t[15], t[14], s[4]) ^ perm(t[18], t[18], s[5]))
+    hi = (perm(t[3], t[2], s[0]) ^ perm(t[7], t[6], s[1]) ^ perm(t[9], t[9], s[2]) ^
+          perm(t[13], t[12], s[3]) ^ perm(t[17], t[16], s[4]) ^ perm(t[19], t[19], s[5]))
+    return lo, hi
+
+
+@pytest.mark.parametrize("lm", [0, 1, 2, 255, 256, 4097, 40000, 65534])
+def test_device_table332_equals_host_definition(lm):
+    rng = np.random.default_rng(lm)
+    t = table332_device(lm)
+    assert t == table332_host(lm)
+    for _ in range(64):
+        syms = [int(x) for x in rng.integers(0, 65536, 4)]
+        ylo = sum((v & 0xFF) << (8 * i) for i, v in enumerate(syms))
+        yhi = sum((v >> 8) << (8 * i) for i, v in enumerate(syms))
+        lo, hi = mul16x(ylo, yhi, t)
+        got = [((lo >> (8 * i)) & 0xFF) | (((hi >> (8 * i)) & 0xFF) << 8) for i in range(4)]
+        assert got == [mul(v, lm) for v in syms]

@@ -50,6 +50,19 @@ case "$1" in
     bash tools/gpu_ab.sh --rounds 3 repair512 skip= all=DAGPU_DEC_LOADALL=1 && \
     bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 256 --batch 8 --steps 5 --warmup 1" skip= all=DAGPU_DEC_LOADALL=1
     ;;
+  splitov)  # round 5: forest levels fold all-parity waves, uniform forests upload nothing (no host syncs in the split
+            # steps), split column encode on a side stream beside the leaves of rows 0..k-1: tests, then A/B
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_split.py tests/test_gpu_trees.py tests/test_gpu_inclusion.py tests/test_gpu_proof.py > gpurun_out/r05_splitov_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r05_splitov_tests.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 3 "bench:--mode split --split-k 512 --steps 50 --warmup 5" ov1= ov0=DAGPU_SPLIT_OVERLAP=0 ov2=DAGPU_SPLIT_OVERLAP=2 head=lib:celestia-app_amd/libdagpu_head.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode split --split-k 1024 --steps 20 --warmup 3" ov1= ov0=DAGPU_SPLIT_OVERLAP=0 head=lib:celestia-app_amd/libdagpu_head.so
+    ;;
+  dectab)  # round 5: half-lane decoders build ONE 3/3/2 table per element (pre for present, post for missing): tests, A/B
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_gf16.py tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py > gpurun_out/r05_dectab_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r05_dectab_tests.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 3 repair512 tab= head=lib:celestia-app_amd/libdagpu_head.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 256 --batch 8 --steps 5 --warmup 1" tab= head=lib:celestia-app_amd/libdagpu_head.so
+    ;;
   final-a)  # round end, part 1: the whole -m gpu suite, the default bench line and its rocprofv3 kernel trace
     bash tools/gpu_final.sh
     ;;
