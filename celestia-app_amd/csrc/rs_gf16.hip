@@ -1630,21 +1630,32 @@ __device__ __forceinline__ void layer_b(W32& w, int q) {
 // One layer on element bit b >= 6 in layout T (LR low register bits stay
 // element bits 1..LR, the wave holds the next 5 - LR, register bits LR.. are
 // element bits 6..; decoder n = 1024: LR = 1, encoder m = 512: LR = 2):
-// positions are compile-time (bits above b are register bits).
+// positions are compile-time (bits above b are register bits).  The block at
+// OFF + blk = 0 has position D - 1, whose skew is log 0 (the only zero skews are
+// at 2^m - 1): Leopard skips its multiply, and so does this (y ^= x alone, in
+// the IFFT and the FFT butterfly) -- half of the layer at 2 D = n / 2, all of
+// the top layer.
 template <bool INV, int D, int LR = 1, int OFF = 0>
 __device__ __forceinline__ void layer_t(W32& w) {
   constexpr int RD = (D / 64) << LR;
   constexpr int N = 64 << (5 - LR);  // elements of the transform
 #pragma unroll
   for (int blk = 0; blk < N; blk += 2 * D) {  // element block start (bits > b)
+    const bool zero = OFF + blk == 0;  // compile-time once unrolled
     const int jf = (blk >> 6) << LR;  // first register of the block
-    const int pos = opaque_tok(OFF + blk + D - 1, w.lo[jf]);  // loaded here, not hoisted / merged
+    const int pos = zero ? 0 : opaque_tok(OFF + blk + D - 1, w.lo[jf]);  // loaded here, not hoisted / merged
 #pragma unroll
     for (int j = 0; j < 32; j++) {
       if (j & RD) continue;
       if ((((j >> LR) << 6) & ~(2 * D - 1)) != blk) continue;
-      if constexpr (INV) ifft2_16(w, j, j + RD, pos);
-      else fft2_16(w, j, j + RD, pos);
+      if (zero) {
+        w.lo[j + RD] ^= w.lo[j];
+        w.hi[j + RD] ^= w.hi[j];
+      } else if constexpr (INV) {
+        ifft2_16(w, j, j + RD, pos);
+      } else {
+        fft2_16(w, j, j + RD, pos);
+      }
       pin_pair(w, j, j + RD);
     }
   }

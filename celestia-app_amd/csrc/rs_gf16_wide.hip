@@ -73,6 +73,9 @@ __device__ __forceinline__ void pmul_add(uint32_t& xlo, uint32_t& xhi, uint32_t 
   xhi = xor3w(xor3w(xor3w(xhi, h0, h1), h2, h3), h4, h5);
 }
 
+// The only zero skews (log 0) sit at positions 2^m - 1 (Leopard skips their
+// multiply): the block at offset 0 of every layer, all of the top layer.
+__device__ __forceinline__ bool zero_skew(int pos) { return ((pos + 1) & pos) == 0; }
 __device__ __forceinline__ void load_tab(const WideTabs& T, int pos, uint32_t (&t)[kTabW]) {
   const uint4* p = (const uint4*)(T.ptab + (long)pos * kTabW);
 #pragma unroll
@@ -139,20 +142,26 @@ struct Unit {
         P.hi[P.at(e[r], g0 + g)] = hi[r][g];
       }
   }
-  // ifftDIT2: y ^= x; x ^= y * skew
-  __device__ __forceinline__ void ifft2(int i, int j, const uint32_t (&t)[kTabW]) {
+  // ifftDIT2: y ^= x; x ^= y * skew (zero: the skew is log 0, no multiply)
+  __device__ __forceinline__ void ifft2(int i, int j, const uint32_t (&t)[kTabW], bool zero) {
 #pragma unroll
     for (int g = 0; g < G; g++) {
       lo[j][g] ^= lo[i][g];
       hi[j][g] ^= hi[i][g];
-      pmul_add(lo[i][g], hi[i][g], lo[j][g], hi[j][g], t);
+    }
+    if (!zero) {
+#pragma unroll
+      for (int g = 0; g < G; g++) pmul_add(lo[i][g], hi[i][g], lo[j][g], hi[j][g], t);
     }
   }
   // fftDIT2: x ^= y * skew; y ^= x
-  __device__ __forceinline__ void fft2(int i, int j, const uint32_t (&t)[kTabW]) {
+  __device__ __forceinline__ void fft2(int i, int j, const uint32_t (&t)[kTabW], bool zero) {
+    if (!zero) {
+#pragma unroll
+      for (int g = 0; g < G; g++) pmul_add(lo[i][g], hi[i][g], lo[j][g], hi[j][g], t);
+    }
 #pragma unroll
     for (int g = 0; g < G; g++) {
-      pmul_add(lo[i][g], hi[i][g], lo[j][g], hi[j][g], t);
       lo[j][g] ^= lo[i][g];
       hi[j][g] ^= hi[i][g];
     }
@@ -174,13 +183,16 @@ __device__ void wide_ifft(const Planes<NG>& P, const WideTabs& T, int n, int bas
       const int e[4] = {i, i + dist, i + 2 * dist, i + 3 * dist};
       Unit<NG, G, 4> x;
       x.load(P, e, g0);
-      load_tab(T, base + iend, t);
-      x.ifft2(0, 1, t);
-      load_tab(T, base + iend + 2 * dist, t);
-      x.ifft2(2, 3, t);
-      load_tab(T, base + iend + dist, t);
-      x.ifft2(0, 2, t);
-      x.ifft2(1, 3, t);
+      bool z = zero_skew(base + iend);
+      if (!z) load_tab(T, base + iend, t);
+      x.ifft2(0, 1, t, z);
+      z = zero_skew(base + iend + 2 * dist);
+      if (!z) load_tab(T, base + iend + 2 * dist, t);
+      x.ifft2(2, 3, t, z);
+      z = zero_skew(base + iend + dist);
+      if (!z) load_tab(T, base + iend + dist, t);
+      x.ifft2(0, 2, t, z);
+      x.ifft2(1, 3, t, z);
       x.store(P, e, g0);
     }
     __syncthreads();
@@ -189,13 +201,14 @@ __device__ void wide_ifft(const Planes<NG>& P, const WideTabs& T, int n, int bas
   }
   if (dist < n) {  // one radix-2 layer left (log2 n odd)
     const int units = (n / 2) * CH;
-    load_tab(T, base + dist, t);
+    const bool z = zero_skew(base + dist);
+    if (!z) load_tab(T, base + dist, t);
     for (int u = threadIdx.x; u < units; u += kWideThreads) {
       const int p = u / CH, g0 = (u - p * CH) * G;
       const int e[2] = {p, p + dist};
       Unit<NG, G, 2> x;
       x.load(P, e, g0);
-      x.ifft2(0, 1, t);
+      x.ifft2(0, 1, t, z);
       x.store(P, e, g0);
     }
     __syncthreads();
@@ -216,13 +229,16 @@ __device__ void wide_fft(const Planes<NG>& P, const WideTabs& T, int n, int fo) 
       const int e[4] = {i, i + dist, i + 2 * dist, i + 3 * dist};
       Unit<NG, G, 4> x;
       x.load(P, e, g0);
-      load_tab(T, fo + iend + dist - 1, t);
-      x.fft2(0, 2, t);
-      x.fft2(1, 3, t);
-      load_tab(T, fo + iend - 1, t);
-      x.fft2(0, 1, t);
-      load_tab(T, fo + iend + 2 * dist - 1, t);
-      x.fft2(2, 3, t);
+      bool z = zero_skew(fo + iend + dist - 1);
+      if (!z) load_tab(T, fo + iend + dist - 1, t);
+      x.fft2(0, 2, t, z);
+      x.fft2(1, 3, t, z);
+      z = zero_skew(fo + iend - 1);
+      if (!z) load_tab(T, fo + iend - 1, t);
+      x.fft2(0, 1, t, z);
+      z = zero_skew(fo + iend + 2 * dist - 1);
+      if (!z) load_tab(T, fo + iend + 2 * dist - 1, t);
+      x.fft2(2, 3, t, z);
       x.store(P, e, g0);
     }
     __syncthreads();
@@ -234,10 +250,11 @@ __device__ void wide_fft(const Planes<NG>& P, const WideTabs& T, int n, int fo) 
     for (int u = threadIdx.x; u < units; u += kWideThreads) {
       const int p = u / CH, g0 = (u - p * CH) * G;
       const int e[2] = {2 * p, 2 * p + 1};
-      load_tab(T, fo + 2 * p, t);
+      const bool z = zero_skew(fo + 2 * p);
+      if (!z) load_tab(T, fo + 2 * p, t);
       Unit<NG, G, 2> x;
       x.load(P, e, g0);
-      x.fft2(0, 1, t);
+      x.fft2(0, 1, t, z);
       x.store(P, e, g0);
     }
     __syncthreads();

@@ -63,6 +63,18 @@ case "$1" in
     bash tools/gpu_ab.sh --rounds 3 repair512 tab= head=lib:celestia-app_amd/libdagpu_head.so && \
     bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 256 --batch 8 --steps 5 --warmup 1" tab= head=lib:celestia-app_amd/libdagpu_head.so
     ;;
+  zskip)  # round 5: butterflies at zero skews (positions 2^m - 1) skip their multiply (half-lane T layers, wide kernels)
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_gf16.py tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py tests/test_gpu_split.py > gpurun_out/r05_zskip_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r05_zskip_tests.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 600 --timeout-method thread tests/test_gpu_wide.py -k "not k8192 and not k4096" > gpurun_out/r05_zskip_wide.log 2>&1
+    rc=$?; echo "wide tests rc=$rc"; tail -3 gpurun_out/r05_zskip_wide.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 3 repair512 zs= tab=lib:celestia-app_amd/libdagpu_tab.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 256 --batch 8 --steps 5 --warmup 1" zs= tab=lib:celestia-app_amd/libdagpu_tab.so && \
+    bash tools/gpu_ab.sh --rounds 2 repair512q3 zs= tab=lib:celestia-app_amd/libdagpu_tab.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode split --split-k 512 --steps 50 --warmup 5" zs= tab=lib:celestia-app_amd/libdagpu_tab.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 1024 --batch 1 --steps 2 --warmup 1" zs= tab=lib:celestia-app_amd/libdagpu_tab.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode split --split-k 1024 --steps 10 --warmup 2" zs= tab=lib:celestia-app_amd/libdagpu_tab.so
+    ;;
   final-a)  # round end, part 1: the whole -m gpu suite, the default bench line and its rocprofv3 kernel trace
     bash tools/gpu_final.sh
     ;;
