@@ -259,17 +259,18 @@ def gf16_kernel_names(k: int):
     """(forward encoder, decoder) kernel names the library runs at width k
     (csrc/rs_gf16.hip launch selection, its A/B switches included), as
     rocprofv3 / tools/pmc_stress.py name them."""
+    ld = 0 if os.environ.get("DAGPU_DEC_LOADALL") == "1" else 1
     if k == 512:
         enc = ("leo16_encode_reg32_kernel<512, false>" if os.environ.get("DAGPU_GF16_ENCH") == "0"
                else "leo16_encode_h_kernel<512, false>")
         dec = ("leo16_decode_reg1k_kernel" if os.environ.get("DAGPU_DEC1K_PACKED") == "1"
-               else "leo16_decode_h_kernel<512>")
+               else f"leo16_decode_h_kernel<512, {ld}>")
         return enc, dec
     if k == 256:
         enc = ("leo16_encode_reg_kernel<256, false>" if os.environ.get("DAGPU_GF16_ENCH") == "0"
                else "leo16_encode_h_kernel<256, false>")
         dec = ("leo16_decode_reg_kernel" if os.environ.get("DAGPU_DEC256_REG") == "1"
-               else "leo16_decode_h_kernel<256>")
+               else f"leo16_decode_h_kernel<256, {ld}>")
         return enc, dec
     return f"leo16w encode k={k}", f"leo16w decode k={k}"
 

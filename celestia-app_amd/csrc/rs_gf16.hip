@@ -1794,12 +1794,15 @@ __device__ __forceinline__ void mul16x_by(uint32_t& xl, uint32_t& xh, const uint
 // LR = 2: 512 threads at <= 128 VGPRs and 64 KiB of LDS, two workgroups per CU).
 template <int K>
 constexpr size_t dec_h_lds_bytes() { return (size_t)(2 * K) * (16 + kTab16x) * sizeof(uint32_t); }
-// SKIP: a missing shard's load gets an out-of-range voffset (the buffer
-// returns 0 without touching memory), halving a maximal-erasure vector's
-// load traffic; its premultiply table is zero either way.
-template <int K, bool SKIP = true>
+// LD (load mode): 0 = every shard loaded; 1 (default) = a missing shard's load
+// gets an out-of-range voffset (the buffer returns 0 without touching memory),
+// halving a maximal-erasure vector's load traffic.  (8-byte lane-pair loads with
+// a DPP swap, half the vector-memory instructions, measured no faster:
+// profiles/gf16_load64_ab_r05.log.)
+template <int K, int LD = 1>
 __global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_decode_h_kernel(
     DecodeArgs a) {
+  constexpr bool SKIP = LD >= 1;
   constexpr int NQ = K / 32, LR = K == 512 ? 1 : 2, RPR = K == 512 ? 1 : 2;
   // dynamic LDS (dec_h_lds_bytes): [0, n x 64 B) the transposes and the
   // derivative staging (each <= n x 64 B); then n x 80 B of per-element tables
@@ -2294,8 +2297,8 @@ static hipError_t dec_lds_attr() {  // above the 64 KiB default: once per proces
     if (err == hipSuccess)
       err = hipFuncSetAttribute((const void*)leo16_decode_reg1k_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDec1kLds);
-    const void* h512[2] = {(const void*)leo16_decode_h_kernel<512, false>, (const void*)leo16_decode_h_kernel<512, true>};
-    const void* h256[2] = {(const void*)leo16_decode_h_kernel<256, false>, (const void*)leo16_decode_h_kernel<256, true>};
+    const void* h512[2] = {(const void*)leo16_decode_h_kernel<512, 0>, (const void*)leo16_decode_h_kernel<512, 1>};
+    const void* h256[2] = {(const void*)leo16_decode_h_kernel<256, 0>, (const void*)leo16_decode_h_kernel<256, 1>};
     for (int i = 0; i < 2 && err == hipSuccess; i++) {
       err = hipFuncSetAttribute(h512[i], hipFuncAttributeMaxDynamicSharedMemorySize, (int)dec_h_lds_bytes<512>());
       if (err == hipSuccess)
@@ -2305,11 +2308,15 @@ static hipError_t dec_lds_attr() {  // above the 64 KiB default: once per proces
   return err;
 }
 
-// half-lane decoders: DAGPU_DEC_LOADALL=1 loads missing shards too (A/B of the
-// out-of-range skip)
-static bool dec_load_all() {
+// half-lane decoders: DAGPU_DEC_LOADALL=1 loads missing shards too (LD = 0, A/B
+// of the out-of-range skip); read per launch
+template <int K>
+static void launch_dec_h(const DecodeArgs& b, long grid, hipStream_t s) {
   const char* e = getenv("DAGPU_DEC_LOADALL");
-  return e && e[0] == '1';
+  if (e && e[0] == '1')
+    hipLaunchKernelGGL((leo16_decode_h_kernel<K, 0>), dim3((unsigned)grid), dim3(2 * K), dec_h_lds_bytes<K>(), s, b);
+  else
+    hipLaunchKernelGGL((leo16_decode_h_kernel<K, 1>), dim3((unsigned)grid), dim3(2 * K), dec_h_lds_bytes<K>(), s, b);
 }
 // k = 256 decoder: the half-lane kernel (round 5); DAGPU_DEC256_REG=1 selects
 // leo16_decode_reg_kernel (A/B)
@@ -2336,12 +2343,7 @@ hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mar
     DecodeArgs b = a;
     b.nchunk = a.shard_bytes / 256;
     if ((e = dec_lds_attr()) != hipSuccess) return e;
-    if (dec_load_all())
-      hipLaunchKernelGGL((leo16_decode_h_kernel<256, false>), dim3((unsigned)(nv * b.nchunk)), dim3(512),
-                         dec_h_lds_bytes<256>(), s, b);
-    else
-      hipLaunchKernelGGL((leo16_decode_h_kernel<256, true>), dim3((unsigned)(nv * b.nchunk)), dim3(512),
-                         dec_h_lds_bytes<256>(), s, b);
+    launch_dec_h<256>(b, nv * b.nchunk, s);
   } else if (a.k == kDecN / 2) {  // register-resident decoder; nchunk = 512-B chunks of the shard
     DecodeArgs b = a;
     b.nchunk = (a.shard_bytes + 511) / 512;
@@ -2354,12 +2356,7 @@ hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mar
     if (dec1k_packed())
       hipLaunchKernelGGL(leo16_decode_reg1k_kernel, dim3((unsigned)(nv * b.nchunk)), dim3(kDec1k), kDec1kLds, s, b);
     else
-      if (dec_load_all())
-        hipLaunchKernelGGL((leo16_decode_h_kernel<512, false>), dim3((unsigned)(nv * b.nchunk)), dim3(1024),
-                           dec_h_lds_bytes<512>(), s, b);
-      else
-        hipLaunchKernelGGL((leo16_decode_h_kernel<512, true>), dim3((unsigned)(nv * b.nchunk)), dim3(1024),
-                           dec_h_lds_bytes<512>(), s, b);
+      launch_dec_h<512>(b, nv * b.nchunk, s);
   } else
 #endif
   {

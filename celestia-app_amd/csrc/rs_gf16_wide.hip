@@ -22,7 +22,8 @@
 // 16-dword product table of that skew position (the products of every 2-bit
 // group of a symbol, low and high bytes, for v_perm; 1 MiB for all positions
 // < 2 kMaxK), loaded once per unit and applied to its G groups.  The decoder's
-// per-element errLocs multiplies use log/exp gathers (L2-resident tables).
+// per-element errLocs multiplies use one product table per element (exp gathers;
+// log/exp gathers per symbol at 4 symbols per element).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -88,6 +89,42 @@ __device__ __forceinline__ void load_tab(const WideTabs& T, int pos, uint32_t (&
   }
 }
 
+// The product table (pmul_add format) of exp(lm), for the decoder's per-element
+// errLocs multiplies (round 5): the 16 products (1 << b) * exp(lm) (logs of the
+// basis from uniform loads, 16 independent exp gathers), then each 3-bit
+// group's entries 0..3 = (0, p0, p1, p0 ^ p1) and 4..7 = those ^ p2, packed by
+// v_perm (rs_gf16.hip mul16x_table_to, checked in tests/test_halflane_emu.py).
+// It replaces a log and an exp gather per symbol (8 dependent gathers per 4
+// symbols) with 2 per 4 symbols, all independent.
+__device__ __forceinline__ void elem_tab(const WideTabs& T, uint32_t lm, uint32_t (&t)[kTabW]) {
+  uint32_t pb[16];
+#pragma unroll
+  for (int b = 0; b < 16; b++) {
+    uint32_t sidx = (uint32_t)T.log[1u << b] + lm;
+    sidx = (sidx + (sidx >> 16)) & 0xFFFFu;
+    pb[b] = T.exp[sidx];
+  }
+  auto quad = [&](uint32_t p0, uint32_t p1, uint32_t& lo, uint32_t& hi) {
+    const uint32_t q = p0 ^ p1;
+    lo = __builtin_amdgcn_perm(q, __builtin_amdgcn_perm(p1, p0, 0x0C04000Cu), 0x04020100u);
+    hi = __builtin_amdgcn_perm(q, __builtin_amdgcn_perm(p1, p0, 0x0C05010Cu), 0x05020100u);
+  };
+  auto grp3 = [&](int b0, int base) {
+    uint32_t lo, hi;
+    quad(pb[b0], pb[b0 + 1], lo, hi);
+    t[base] = lo;
+    t[base + 1] = lo ^ __builtin_amdgcn_perm(pb[b0 + 2], pb[b0 + 2], 0x00000000u);
+    t[base + 2] = hi;
+    t[base + 3] = hi ^ __builtin_amdgcn_perm(pb[b0 + 2], pb[b0 + 2], 0x01010101u);
+  };
+  grp3(0, 0);
+  grp3(3, 4);
+  quad(pb[6], pb[7], t[8], t[9]);
+  grp3(8, 10);
+  grp3(11, 14);
+  quad(pb[14], pb[15], t[18], t[19]);
+}
+
 // mulLog on one 16-bit symbol (leopard.go mulLog): a * exp(lm), 0 stays 0
 __device__ __forceinline__ uint32_t mul_log(const WideTabs& T, uint32_t a, uint32_t lm) {
   if (a == 0) return 0;
@@ -96,18 +133,37 @@ __device__ __forceinline__ uint32_t mul_log(const WideTabs& T, uint32_t a, uint3
   return T.exp[s];
 }
 
-// 4 symbols of a (lo, hi) dword pair times exp(lm)
-__device__ __forceinline__ void mul4(const WideTabs& T, uint32_t& lo, uint32_t& hi, uint32_t lm) {
-  uint32_t rl = 0, rh = 0;
+// (lo, hi) *= exp(lm) for one element's NG dword pairs: NG >= 2 through the
+// element's product table (16 gathers, k = 1024 Repair 45.9 -> 75.2 squares/s,
+// profiles/gf16_widedec_ab_r05.log); NG = 1 (n >= 8192: 4 symbols per element)
+// by log/exp gathers per symbol (8, fewer than the table's 16).
+template <int NG>
+__device__ __forceinline__ void mul_elem(const WideTabs& T, uint32_t (&lo)[NG], uint32_t (&hi)[NG], uint32_t lm) {
+  if constexpr (NG >= 2) {
+    uint32_t t[kTabW];
+    elem_tab(T, lm, t);
 #pragma unroll
-  for (int b = 0; b < 4; b++) {
-    const uint32_t s = ((lo >> (8 * b)) & 0xFFu) | (((hi >> (8 * b)) & 0xFFu) << 8);
-    const uint32_t p = mul_log(T, s, lm);
-    rl |= (p & 0xFFu) << (8 * b);
-    rh |= (p >> 8) << (8 * b);
+    for (int g = 0; g < NG; g++) {
+      uint32_t rl = 0, rh = 0;
+      pmul_add(rl, rh, lo[g], hi[g], t);
+      lo[g] = rl;
+      hi[g] = rh;
+    }
+  } else {
+#pragma unroll
+    for (int g = 0; g < NG; g++) {
+      uint32_t rl = 0, rh = 0;
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const uint32_t sym = ((lo[g] >> (8 * b)) & 0xFFu) | (((hi[g] >> (8 * b)) & 0xFFu) << 8);
+        const uint32_t p = mul_log(T, sym, lm);
+        rl |= (p & 0xFFu) << (8 * b);
+        rh |= (p >> 8) << (8 * b);
+      }
+      lo[g] = rl;
+      hi[g] = rh;
+    }
   }
-  lo = rl;
-  hi = rh;
 }
 
 // LDS planes: lo[e * NGP + g], hi[...] (NG = S / 4 dword groups, NGP = NG + 1
@@ -442,18 +498,30 @@ __global__ __launch_bounds__(kWideThreads) void leo16w_decode_kernel(DecodeArgs 
   uint8_t* base = a.data + sq * a.sq_stride + vec * a.vec_stride + col;
   const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
   const uint16_t* err = (const uint16_t*)(a.err + err_vec(a, v) * (long)rs_err_bytes(k));
-  for (int t = threadIdx.x; t < n * NG; t += kWideThreads) {
-    const int i = t / NG, g = t - i * NG;
+  // one thread per element: its table once, then its NG dword pairs
+  for (int i = threadIdx.x; i < n; i += kWideThreads) {
     const long shard = i < k ? k + i : i - k;
-    uint32_t lo = 0, hi = 0;
     if (pres[shard * a.p_shard_stride]) {
-      const uint32_t* src = (const uint32_t*)(base + shard * a.shard_stride) + g;
-      lo = src[0];
-      hi = src[8];
-      mul4(T, lo, hi, err[i]);
+      const uint32_t* src = (const uint32_t*)(base + shard * a.shard_stride);
+      uint32_t lo[NG], hi[NG];
+#pragma unroll
+      for (int g = 0; g < NG; g++) {
+        lo[g] = src[g];
+        hi[g] = src[8 + g];
+      }
+      mul_elem<NG>(T, lo, hi, err[i]);
+#pragma unroll
+      for (int g = 0; g < NG; g++) {
+        P.lo[P.at(i, g)] = lo[g];
+        P.hi[P.at(i, g)] = hi[g];
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < NG; g++) {
+        P.lo[P.at(i, g)] = 0u;
+        P.hi[P.at(i, g)] = 0u;
+      }
     }
-    P.lo[P.at(i, g)] = lo;
-    P.hi[P.at(i, g)] = hi;
   }
   __syncthreads();
   wide_ifft<NG, G>(P, T, n, -1);
@@ -491,15 +559,22 @@ __global__ __launch_bounds__(kWideThreads) void leo16w_decode_kernel(DecodeArgs 
     }
   }
   wide_fft<NG, G>(P, T, n, 0);
-  for (int t = threadIdx.x; t < n * NG; t += kWideThreads) {
-    const int i = t / NG, g = t - i * NG;
+  for (int i = threadIdx.x; i < n; i += kWideThreads) {
     const long shard = i < k ? k + i : i - k;
     if (pres[shard * a.p_shard_stride]) continue;
-    uint32_t lo = P.lo[P.at(i, g)], hi = P.hi[P.at(i, g)];
-    mul4(T, lo, hi, kMod - err[i]);
-    uint32_t* dst = (uint32_t*)(base + shard * a.shard_stride) + g;
-    dst[0] = lo;
-    dst[8] = hi;
+    uint32_t lo[NG], hi[NG];
+#pragma unroll
+    for (int g = 0; g < NG; g++) {
+      lo[g] = P.lo[P.at(i, g)];
+      hi[g] = P.hi[P.at(i, g)];
+    }
+    mul_elem<NG>(T, lo, hi, kMod - err[i]);
+    uint32_t* dst = (uint32_t*)(base + shard * a.shard_stride);
+#pragma unroll
+    for (int g = 0; g < NG; g++) {
+      dst[g] = lo[g];
+      dst[8 + g] = hi[g];
+    }
   }
 }
 

@@ -175,3 +175,25 @@ def test_halflane_decoders_agree(ctx, k, env, shard, monkeypatch):
         monkeypatch.delenv(env)
         assert new == old
         assert b"".join(new) == full.tobytes()
+
+
+@pytest.mark.parametrize("k", [512, 256])
+@pytest.mark.parametrize("mode", ["DAGPU_DEC_LOADALL"])
+def test_halflane_decoder_load_modes_agree(ctx, k, mode, monkeypatch):
+    """Round 5: the half-lane decoders' load modes -- missing shards skipped
+    (default) or loaded and zeroed -- give the same bytes, on shards of one and
+    several 256-B pieces and on erasure patterns of every shape."""
+    rng = np.random.default_rng(29 + k)
+    for shard in (256, 768):
+        data = rng.integers(0, 256, (k, shard), dtype=np.uint8)
+        full = np.concatenate([data, oracle.encode(data)])
+        codec = da.LeoRSCodec(ctx)
+        for keep in (set(rng.choice(2 * k, k, replace=False).tolist()), set(range(0, 2 * k, 2)),
+                     set(range(k // 2, k + k // 2))):
+            shards = [full[i].tobytes() if i in keep else None for i in range(2 * k)]
+            new = codec.decode(shards)
+            monkeypatch.setenv(mode, "1")
+            old = codec.decode(shards)
+            monkeypatch.delenv(mode)
+            assert new == old
+            assert b"".join(new) == full.tobytes()

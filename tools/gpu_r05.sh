@@ -75,6 +75,31 @@ case "$1" in
     bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 1024 --batch 1 --steps 2 --warmup 1" zs= tab=lib:celestia-app_amd/libdagpu_tab.so && \
     bash tools/gpu_ab.sh --rounds 2 "bench:--mode split --split-k 1024 --steps 10 --warmup 2" zs= tab=lib:celestia-app_amd/libdagpu_tab.so
     ;;
+  probe2)  # round 5: phase probes of the half-lane kernels after the one-table / zero-skew changes (libdagpu_probe.so rebuilt)
+    for w in dec512h dec256h enc512h; do
+      timeout -k 10 300 python -u tools/phase_probe.py $w > gpurun_out/phase_probe_${w}_r05b.log 2>&1 || { echo "probe $w failed"; tail -5 gpurun_out/phase_probe_${w}_r05b.log; exit 1; }
+      cat gpurun_out/phase_probe_${w}_r05b.log
+    done
+    ;;
+  load64)  # round 5: half-lane decoders load lane pairs with 8-byte loads + a DPP swap (half the VMEM instructions)
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_gf16.py tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py > gpurun_out/r05_load64_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r05_load64_tests.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 3 repair512 l64= l32=DAGPU_DEC_LOAD32=1 && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 256 --batch 8 --steps 5 --warmup 1" l64= l32=DAGPU_DEC_LOAD32=1 && \
+    bash tools/gpu_pmc_gf16.sh repair512 split512 split1024 repair1024
+    ;;
+  enc64)  # round 5: half-lane encoders' loads, Q0 copy and plain / fill stores as 8-byte lane-pair accesses (env A/B);
+          # wide decoder: one product table per element instead of log/exp gathers per symbol (A/B vs libdagpu_zs.so)
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_gf16.py tests/test_gpu_repair_fill.py tests/test_gpu_split.py tests/test_gpu_parity.py > gpurun_out/r05_enc64_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r05_enc64_tests.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 600 --timeout-method thread tests/test_gpu_wide.py -k "not k8192" > gpurun_out/r05_enc64_wide.log 2>&1
+    rc=$?; echo "wide tests rc=$rc"; tail -3 gpurun_out/r05_enc64_wide.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 1024 --batch 1 --steps 2 --warmup 1" wd= zs=lib:celestia-app_amd/libdagpu_zs.so && \
+    bash tools/gpu_ab.sh --rounds 1 "bench:--mode repair --k 2048 --batch 1 --steps 1 --warmup 1" wd= zs=lib:celestia-app_amd/libdagpu_zs.so && \
+    bash tools/gpu_ab.sh --rounds 3 "bench:--mode split --split-k 512 --steps 50 --warmup 5" e64= e32=DAGPU_ENC_LOAD32=1 && \
+    bash tools/gpu_ab.sh --rounds 2 repair512q3 e64= e32=DAGPU_ENC_LOAD32=1 && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode split --split-k 256 --steps 50 --warmup 5" e64= e32=DAGPU_ENC_LOAD32=1
+    ;;
   final-a)  # round end, part 1: the whole -m gpu suite, the default bench line and its rocprofv3 kernel trace
     bash tools/gpu_final.sh
     ;;
