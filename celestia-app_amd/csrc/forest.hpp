@@ -51,6 +51,7 @@ struct ForestLevelArgs {
   long ntrees, total_out;
   int ignore_max, check_order, rfc;
   int32_t* status;  // per tree, OR kForestPushOrder (check_order only)
+  int status_shared;  // 1: every tree ORs into status[0] (one flag for the batch)
 };
 
 hipError_t launch_forest_leaves(const ForestLeafArgs& a, hipStream_t s);
@@ -125,6 +126,7 @@ struct ForestJob {
   uint8_t* d_roots;
   int records;
   long roots_stride;
+  int status_shared = 0;  // ForestLevelArgs::status_shared
 };
 hipError_t forest_enqueue_pair(const ForestJob& x, const ForestJob& y, hipStream_t s);
 

@@ -251,7 +251,7 @@ __device__ __forceinline__ void forest_level_node(const ForestLevelArgs& a, long
       load8(a.in + (ibase + (j1 + 1) * a.in_lstride) * rec, n2);
       bad |= ns_less(n2, rmn);
     }
-    if (bad) atomicOr(&a.status[t], kForestPushOrder);
+    if (bad) atomicOr(&a.status[a.status_shared ? 0 : t], kForestPushOrder);
   }
   uint32_t st[8];
   // A min namespace equal to the parity namespace (the largest) makes the max
@@ -508,7 +508,8 @@ void ForestPlan::finalize() {
 
 // level L (>= 1) of plan p as kernel arguments
 static ForestLevelArgs level_args(const ForestPlan& p, int L, const uint8_t* d_leaves, uint8_t* d_inner,
-                                  int64_t* d_meta, int ignore_max, int check_order, int rfc, int32_t* d_status) {
+                                  int64_t* d_meta, int ignore_max, int check_order, int rfc, int32_t* d_status,
+                                  int status_shared = 0) {
   const int rec = rfc ? kRecRfc : kRecNmt;
   ForestLevelArgs a{};
   a.in = L == 1 ? d_leaves : d_inner + (long)p.base[L - 1] * rec;
@@ -531,6 +532,7 @@ static ForestLevelArgs level_args(const ForestPlan& p, int L, const uint8_t* d_l
   a.check_order = check_order && L == 1;
   a.rfc = rfc;
   a.status = d_status;
+  a.status_shared = status_shared;
   return a;
 }
 
@@ -567,7 +569,7 @@ hipError_t forest_enqueue_pair(const ForestJob& x, const ForestJob& y, hipStream
     for (int f = 0; f < 2; f++)
       if (j[f]->p->ntrees > 0 && L <= j[f]->p->nlevels && j[f]->p->total[L] > 0)
         a[n++] = level_args(*j[f]->p, L, j[f]->d_leaves, j[f]->d_inner, j[f]->d_meta, j[f]->ignore_max,
-                            j[f]->check_order, j[f]->rfc, j[f]->d_status);
+                            j[f]->check_order, j[f]->rfc, j[f]->d_status, j[f]->status_shared);
     hipError_t e = hipSuccess;
     if (n == 1) {
       e = launch_forest_level(a[0], s);

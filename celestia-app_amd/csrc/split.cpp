@@ -218,7 +218,8 @@ int dagpu_split_cols_device(dagpu_ctx* ctx, uint32_t k, uint32_t parts, uint32_t
     // full column trees (push order of Q0 columns checked at level 1) and the
     // row subtrees over this slab (row order was checked on the row owners),
     // each level of both in one launch
-    const dagpu::ForestJob cols{&pl.cols, ws.leaves, ws.col_inner, ws.meta, 1, 1, 0, d_status, d_col_roots, 0, 0};
+    // push order of the Q0 column parts, into the step's one status word
+    const dagpu::ForestJob cols{&pl.cols, ws.leaves, ws.col_inner, ws.meta, 1, 1, 0, d_status, d_col_roots, 0, 0, 1};
     const dagpu::ForestJob rows{&pl.rows, ws.leaves, ws.row_inner, ws.meta + pl.cols.meta.size(), 1, 0, 0,
                                 nullptr, d_row_sub, 1, 0};
     HIP_TRY(ctx, dagpu::forest_enqueue_pair(cols, rows, s));

@@ -74,6 +74,28 @@ def test_split_push_order(ctx):
         split.extend_split_local(d, k, 4, ctx)
 
 
+@pytest.mark.parametrize("parts", [1, 2, 4])
+def test_split_column_push_order(ctx, parts):
+    """Every row sorted on its own but two rows swapped: only COLUMN trees see
+    the violation.  The split must raise like the single-GPU DAH and the oracle
+    (the column forest's push-order flag goes to the step's one status word;
+    before round 5 it went to a per-tree slot past it and was lost)."""
+    k = 16
+    ods = np.ascontiguousarray(synth.random_blob_square(k, 12)).reshape(k, k, 512).copy()
+    ods[[2, 9]] = ods[[9, 2]]
+    ns = ods[:, :, :29]
+    assert all(ns[r, c].tobytes() <= ns[r, c + 1].tobytes() for r in range(k) for c in range(k - 1))
+    assert any(ns[2, c].tobytes() > ns[3, c].tobytes() for c in range(k))
+    with pytest.raises(oracle.OracleError):
+        oracle.extend_and_dah(ods.reshape(-1), k)
+    eds = da.extend_shares(ods.reshape(k * k, 512), ctx)
+    with pytest.raises(da.ErrInvalidPushOrder):
+        da.new_data_availability_header(eds)
+    d = torch.from_numpy(ods.reshape(-1)).cuda()
+    with pytest.raises(da.ErrInvalidPushOrder):
+        split.extend_split_local(d, k, parts, ctx)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

@@ -100,6 +100,10 @@ case "$1" in
     bash tools/gpu_ab.sh --rounds 2 repair512q3 e64= e32=DAGPU_ENC_LOAD32=1 && \
     bash tools/gpu_ab.sh --rounds 2 "bench:--mode split --split-k 256 --steps 50 --warmup 5" e64= e32=DAGPU_ENC_LOAD32=1
     ;;
+  colorder)  # round 5: the split's column push-order flag into its one status word (was a per-tree slot past it)
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_split.py tests/test_gpu_trees.py tests/test_gpu_inclusion.py tests/test_gpu_proof.py tests/test_gpu_parity.py > gpurun_out/r05_colorder_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r05_colorder_tests.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error" gpurun_out/r05_colorder_tests.log | head; exit $rc; }
+    ;;
   final-a)  # round end, part 1: the whole -m gpu suite, the default bench line and its rocprofv3 kernel trace
     bash tools/gpu_final.sh
     ;;
