@@ -104,6 +104,17 @@ case "$1" in
     timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_split.py tests/test_gpu_trees.py tests/test_gpu_inclusion.py tests/test_gpu_proof.py tests/test_gpu_parity.py > gpurun_out/r05_colorder_tests.log 2>&1
     rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r05_colorder_tests.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error" gpurun_out/r05_colorder_tests.log | head; exit $rc; }
     ;;
+  order)  # round 5: half-lane decoders issue their table gathers, then the data loads, then pack the table
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_gf16.py tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py > gpurun_out/r05_order_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r05_order_tests.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 3 repair512 ord= ord0=lib:celestia-app_amd/libdagpu_ord0.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 256 --batch 8 --steps 5 --warmup 1" ord= ord0=lib:celestia-app_amd/libdagpu_ord0.so
+    ;;
+  order8)  # round 5: the k = 128 sliced decoder issues its table loads, presence bytes and shard data before the table barrier
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py tests/test_gpu_parity.py tests/test_gpu_repair_async.py > gpurun_out/r05_order8_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r05_order8_tests.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 3 repair128 ord= ord0=lib:celestia-app_amd/libdagpu_ord0.so
+    ;;
   final-a)  # round end, part 1: the whole -m gpu suite, the default bench line and its rocprofv3 kernel trace
     bash tools/gpu_final.sh
     ;;
