@@ -115,6 +115,12 @@ case "$1" in
     rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r05_order8_tests.log; [ $rc -eq 0 ] || exit $rc
     bash tools/gpu_ab.sh --rounds 3 repair128 ord= ord0=lib:celestia-app_amd/libdagpu_ord0.so
     ;;
+  der64)  # round 5: the half-lane decoders' derivative stages lo and hi side by side (8-byte LDS accesses)
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_gf16.py tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py > gpurun_out/r05_der64_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r05_der64_tests.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 3 repair512 d64= d0=lib:celestia-app_amd/libdagpu_der0.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 256 --batch 8 --steps 5 --warmup 1" d64= d0=lib:celestia-app_amd/libdagpu_der0.so
+    ;;
   final-a)  # round end, part 1: the whole -m gpu suite, the default bench line and its rocprofv3 kernel trace
     bash tools/gpu_final.sh
     ;;
