@@ -15,6 +15,8 @@ for wl in "$@"; do
     repair128) A="--mode repair --k 128 --batch 256 --steps 3 --warmup 1";;
     split1024) A="--mode split --split-k 1024 --steps 3 --warmup 1";;
     repair1024) A="--mode repair --k 1024 --batch 1 --steps 2 --warmup 1";;
+    split2048) A="--mode split --split-k 2048 --steps 2 --warmup 1";;
+    repair2048) A="--mode repair --k 2048 --batch 1 --steps 1 --warmup 1";;
     *) echo "unknown $wl"; exit 2;;
   esac
   B="$GRAFT_REPO_ROOT/bench.py $A"

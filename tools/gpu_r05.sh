@@ -121,6 +121,9 @@ case "$1" in
     bash tools/gpu_ab.sh --rounds 3 repair512 d64= d0=lib:celestia-app_amd/libdagpu_der0.so && \
     bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 256 --batch 8 --steps 5 --warmup 1" d64= d0=lib:celestia-app_amd/libdagpu_der0.so
     ;;
+  wide2048)  # round 5: kernel stats + SQ/GRBM counters of the k = 2048 split square and Repair (wide kernels)
+    bash tools/gpu_pmc_gf16.sh split2048 repair2048
+    ;;
   final-a)  # round end, part 1: the whole -m gpu suite, the default bench line and its rocprofv3 kernel trace
     bash tools/gpu_final.sh
     ;;
