@@ -224,41 +224,67 @@ struct Unit {
   }
 };
 
+// A skew table from a wave-uniform position: scalar loads (constant address
+// space), so the table sits in SGPRs instead of five 16-B vector loads per lane.
+typedef const __attribute__((address_space(4))) uint32_t* ConstTab;
+template <int N>
+__device__ __forceinline__ void load_tab_u(const WideTabs& T, int pos, uint32_t (&t)[N]) {
+  const ConstTab p = (ConstTab)(T.ptab + (long)__builtin_amdgcn_readfirstlane(pos) * kTabW);
+#pragma unroll
+  for (int i = 0; i < kTabW; i++) t[i] = p[i];
+}
+
+// One radix-4 IFFT step (dist, dist4 = 4 dist) over all units.  UNI: the 64
+// units of a wave lie in one block of 4 dist elements (dist * CH >= 64), so
+// their three skew positions are wave-uniform and the tables come by scalar loads.
+template <int NG, int G, bool UNI>
+__device__ __forceinline__ void ifft_step(const Planes<NG>& P, const WideTabs& T, int n, int base, int dist) {
+  constexpr int CH = NG / G;
+  const int dist4 = dist << 2;
+  const int units = (n / 4) * CH;
+  uint32_t t[kTabW];
+  for (int u = threadIdx.x; u < units; u += kWideThreads) {
+    const int quad = u / CH, g0 = (u - quad * CH) * G;
+    const int r = (quad / dist) * dist4, i = r + (quad % dist), iend = r + dist;
+    const int e[4] = {i, i + dist, i + 2 * dist, i + 3 * dist};
+    Unit<NG, G, 4> x;
+    x.load(P, e, g0);
+    auto tab = [&](int pos) {
+      if constexpr (UNI) load_tab_u(T, pos, t);
+      else load_tab(T, pos, t);
+    };
+    bool z = zero_skew(base + iend);
+    if (!z) tab(base + iend);
+    x.ifft2(0, 1, t, z);
+    z = zero_skew(base + iend + 2 * dist);
+    if (!z) tab(base + iend + 2 * dist);
+    x.ifft2(2, 3, t, z);
+    z = zero_skew(base + iend + dist);
+    if (!z) tab(base + iend + dist);
+    x.ifft2(0, 2, t, z);
+    x.ifft2(1, 3, t, z);
+    x.store(P, e, g0);
+  }
+  __syncthreads();
+}
+
 // ifftDITEncoder / ifftDITDecoder over n elements (mtrunc = n), skew index
 // base + iend (encoder: base = IO - 1; decoder: -1)
 template <int NG, int G>
 __device__ void wide_ifft(const Planes<NG>& P, const WideTabs& T, int n, int base) {
   constexpr int CH = NG / G;
   int dist = 1, dist4 = 4;
-  uint32_t t[kTabW];
   while (dist4 <= n) {
-    const int units = (n / 4) * CH;
-    for (int u = threadIdx.x; u < units; u += kWideThreads) {
-      const int quad = u / CH, g0 = (u - quad * CH) * G;
-      const int r = (quad / dist) * dist4, i = r + (quad % dist), iend = r + dist;
-      const int e[4] = {i, i + dist, i + 2 * dist, i + 3 * dist};
-      Unit<NG, G, 4> x;
-      x.load(P, e, g0);
-      bool z = zero_skew(base + iend);
-      if (!z) load_tab(T, base + iend, t);
-      x.ifft2(0, 1, t, z);
-      z = zero_skew(base + iend + 2 * dist);
-      if (!z) load_tab(T, base + iend + 2 * dist, t);
-      x.ifft2(2, 3, t, z);
-      z = zero_skew(base + iend + dist);
-      if (!z) load_tab(T, base + iend + dist, t);
-      x.ifft2(0, 2, t, z);
-      x.ifft2(1, 3, t, z);
-      x.store(P, e, g0);
-    }
-    __syncthreads();
+    if (dist * CH >= 64) ifft_step<NG, G, true>(P, T, n, base, dist);
+    else ifft_step<NG, G, false>(P, T, n, base, dist);
     dist = dist4;
     dist4 <<= 2;
   }
-  if (dist < n) {  // one radix-2 layer left (log2 n odd)
+  if (dist < n) {  // one radix-2 layer left (log2 n odd): one position for all
     const int units = (n / 2) * CH;
+    uint32_t t[kTabW];
     const bool z = zero_skew(base + dist);
-    if (!z) load_tab(T, base + dist, t);
+    if (!z) load_tab_u(T, base + dist, t);
     for (int u = threadIdx.x; u < units; u += kWideThreads) {
       const int p = u / CH, g0 = (u - p * CH) * G;
       const int e[2] = {p, p + dist};
@@ -271,38 +297,52 @@ __device__ void wide_ifft(const Planes<NG>& P, const WideTabs& T, int n, int bas
   }
 }
 
+// One radix-4 FFT step (fftDIT, skew index fo + iend - 1); UNI as ifft_step.
+template <int NG, int G, bool UNI>
+__device__ __forceinline__ void fft_step(const Planes<NG>& P, const WideTabs& T, int n, int fo, int dist) {
+  constexpr int CH = NG / G;
+  const int dist4 = dist << 2;
+  const int units = (n / 4) * CH;
+  uint32_t t[kTabW];
+  for (int u = threadIdx.x; u < units; u += kWideThreads) {
+    const int quad = u / CH, g0 = (u - quad * CH) * G;
+    const int r = (quad / dist) * dist4, i = r + (quad % dist), iend = r + dist;
+    const int e[4] = {i, i + dist, i + 2 * dist, i + 3 * dist};
+    Unit<NG, G, 4> x;
+    x.load(P, e, g0);
+    auto tab = [&](int pos) {
+      if constexpr (UNI) load_tab_u(T, pos, t);
+      else load_tab(T, pos, t);
+    };
+    bool z = zero_skew(fo + iend + dist - 1);
+    if (!z) tab(fo + iend + dist - 1);
+    x.fft2(0, 2, t, z);
+    x.fft2(1, 3, t, z);
+    z = zero_skew(fo + iend - 1);
+    if (!z) tab(fo + iend - 1);
+    x.fft2(0, 1, t, z);
+    z = zero_skew(fo + iend + 2 * dist - 1);
+    if (!z) tab(fo + iend + 2 * dist - 1);
+    x.fft2(2, 3, t, z);
+    x.store(P, e, g0);
+  }
+  __syncthreads();
+}
+
 // fftDIT over n elements (mtrunc = n), skew index fo + iend - 1
 template <int NG, int G>
 __device__ void wide_fft(const Planes<NG>& P, const WideTabs& T, int n, int fo) {
   constexpr int CH = NG / G;
   int dist4 = n, dist = n >> 2;
-  uint32_t t[kTabW];
   while (dist != 0) {
-    const int units = (n / 4) * CH;
-    for (int u = threadIdx.x; u < units; u += kWideThreads) {
-      const int quad = u / CH, g0 = (u - quad * CH) * G;
-      const int r = (quad / dist) * dist4, i = r + (quad % dist), iend = r + dist;
-      const int e[4] = {i, i + dist, i + 2 * dist, i + 3 * dist};
-      Unit<NG, G, 4> x;
-      x.load(P, e, g0);
-      bool z = zero_skew(fo + iend + dist - 1);
-      if (!z) load_tab(T, fo + iend + dist - 1, t);
-      x.fft2(0, 2, t, z);
-      x.fft2(1, 3, t, z);
-      z = zero_skew(fo + iend - 1);
-      if (!z) load_tab(T, fo + iend - 1, t);
-      x.fft2(0, 1, t, z);
-      z = zero_skew(fo + iend + 2 * dist - 1);
-      if (!z) load_tab(T, fo + iend + 2 * dist - 1, t);
-      x.fft2(2, 3, t, z);
-      x.store(P, e, g0);
-    }
-    __syncthreads();
+    if (dist * CH >= 64) fft_step<NG, G, true>(P, T, n, fo, dist);
+    else fft_step<NG, G, false>(P, T, n, fo, dist);
     dist4 = dist;
     dist >>= 2;
   }
   if (dist4 == 2) {
     const int units = (n / 2) * CH;
+    uint32_t t[kTabW];
     for (int u = threadIdx.x; u < units; u += kWideThreads) {
       const int p = u / CH, g0 = (u - p * CH) * G;
       const int e[2] = {2 * p, 2 * p + 1};

@@ -124,6 +124,14 @@ case "$1" in
   wide2048)  # round 5: kernel stats + SQ/GRBM counters of the k = 2048 split square and Repair (wide kernels)
     bash tools/gpu_pmc_gf16.sh split2048 repair2048
     ;;
+  wtab)  # round 5: wide kernels load wave-uniform skew tables with scalar loads (radix-4 steps with dist * CH >= 64)
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 600 --timeout-method thread tests/test_gpu_wide.py -k "not k8192" > gpurun_out/r05_wtab_wide.log 2>&1
+    rc=$?; echo "wide tests rc=$rc"; tail -3 gpurun_out/r05_wtab_wide.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode split --split-k 1024 --steps 10 --warmup 2" ws= w0=lib:celestia-app_amd/libdagpu_w0.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 1024 --batch 1 --steps 2 --warmup 1" ws= w0=lib:celestia-app_amd/libdagpu_w0.so && \
+    bash tools/gpu_ab.sh --rounds 1 "bench:--mode repair --k 2048 --batch 1 --steps 1 --warmup 1" ws= w0=lib:celestia-app_amd/libdagpu_w0.so && \
+    bash tools/gpu_ab.sh --rounds 1 "bench:--mode split --split-k 2048 --steps 2 --warmup 1" ws= w0=lib:celestia-app_amd/libdagpu_w0.so
+    ;;
   final-a)  # round end, part 1: the whole -m gpu suite, the default bench line and its rocprofv3 kernel trace
     bash tools/gpu_final.sh
     ;;
