@@ -190,7 +190,7 @@ int dagpu_split_cols_device(dagpu_ctx* ctx, uint32_t k, uint32_t parts, uint32_t
   hipEvent_t fork = es ? ev_take(ctx) : nullptr, joined = es ? ev_take(ctx) : nullptr;
   if (es && fork && joined && hipEventRecord(fork, s) == hipSuccess && hipStreamWaitEvent(es, fork, 0) == hipSuccess) {
     hipError_t e = launch_rs_encode((int)k, ea, es);
-    if (e == hipSuccess) e = hipEventRecord(joined, es);
+    const bool encoding = e == hipSuccess && (e = hipEventRecord(joined, es)) == hipSuccess;
     dagpu::ForestLeafArgs top = la, bottom = la;
     top.nleaves = (long)k * W;
     bottom.data = d_slab + (size_t)k * W * kSS;
@@ -198,7 +198,12 @@ int dagpu_split_cols_device(dagpu_ctx* ctx, uint32_t k, uint32_t parts, uint32_t
     bottom.grid_r0 = k;
     bottom.out = ws.leaves + (size_t)k * W * dagpu::kRecNmt;
     if (e == hipSuccess) e = dagpu::launch_forest_leaves(top, s);
-    if (e == hipSuccess) e = hipStreamWaitEvent(s, joined, 0);
+    // the caller's stream waits for the side stream's encode whatever failed
+    // after it, so nothing of this call writes the slab out of stream order
+    if (encoding) {
+      const hipError_t we = hipStreamWaitEvent(s, joined, 0);
+      if (e == hipSuccess) e = we;
+    }
     if (e == hipSuccess) e = dagpu::launch_forest_leaves(bottom, s);
     ev_give(ctx, fork);
     ev_give(ctx, joined);
@@ -215,10 +220,9 @@ int dagpu_split_cols_device(dagpu_ctx* ctx, uint32_t k, uint32_t parts, uint32_t
   }
   {
     ProfScope p(ctx, 3, s);
-    // full column trees (push order of Q0 columns checked at level 1) and the
-    // row subtrees over this slab (row order was checked on the row owners),
-    // each level of both in one launch
-    // push order of the Q0 column parts, into the step's one status word
+    // full column trees (push order of the Q0 column parts checked at level 1,
+    // into the step's one status word) and the row subtrees over this slab (row
+    // order was checked on the row owners), each level of both in one launch
     const dagpu::ForestJob cols{&pl.cols, ws.leaves, ws.col_inner, ws.meta, 1, 1, 0, d_status, d_col_roots, 0, 0, 1};
     const dagpu::ForestJob rows{&pl.rows, ws.leaves, ws.row_inner, ws.meta + pl.cols.meta.size(), 1, 0, 0,
                                 nullptr, d_row_sub, 1, 0};
