@@ -46,6 +46,9 @@ class DeviceSquares:
         self.status = torch.zeros((n,), dtype=torch.int32, device=dev)
         ws = self.ctx._L.dagpu_workspace_size(self.k, self.n)
         self.workspace = torch.empty((ws,), dtype=torch.uint8, device=dev)
+        # tensors of started repairs, held until their join (dagpu_repair_start:
+        # the buffers must stay valid until the joined stream has passed the repair)
+        self._held = {}
 
     def q0(self) -> torch.Tensor:
         """(n, k, k*512) view of Q0 inside the EDS buffer."""
@@ -130,11 +133,18 @@ class DeviceSquares:
             present.data_ptr() + first * w * w, self.row_roots.data_ptr() + first * w * ROOT,
             self.col_roots.data_ptr() + first * w * ROOT, status.data_ptr() + 4 * first, workspace.data_ptr(),
             _stream_handle(stream), ctypes.byref(h)))
+        # the repair runs on the library's stream: keep its tensors (a temporary
+        # workspace included) out of the caching allocator until the join
+        self._held[h.value] = (present, status, workspace)
         return h.value
 
     def repair_join(self, handle: int, stream: Optional[torch.cuda.Stream] = None) -> None:
-        """dagpu_repair_join: `stream` waits for the started repair."""
-        self._ck(self.ctx._L.dagpu_repair_join(self.ctx.handle, handle, _stream_handle(stream)))
+        """dagpu_repair_join: `stream` waits for the started repair (whose
+        tensors are released afterwards: free them only in `stream`'s order)."""
+        try:
+            self._ck(self.ctx._L.dagpu_repair_join(self.ctx.handle, handle, _stream_handle(stream)))
+        finally:
+            self._held.pop(handle, None)
 
     def repair_workspace(self, count: Optional[int] = None) -> torch.Tensor:
         ws = self.ctx._L.dagpu_repair_workspace_size(self.k, self.n if count is None else count)

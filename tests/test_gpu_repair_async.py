@@ -177,3 +177,22 @@ def test_close_with_repairs_started():
     c.close()  # joins the worker and drains its stream
     torch.cuda.synchronize()
     assert torch.equal(ds.eds, ref) and (status.cpu().numpy() == 0).all()
+
+
+def test_started_repair_holds_its_tensors(ctx):
+    """A started repair's tensors stay allocated until its join, even when the
+    caller passes temporaries (the workspace below): the DeviceSquares wrapper
+    holds them.  Before round 5 the temporary went back to the caching
+    allocator at once, and a same-size allocation right after the start (here
+    filled with junk while the repair runs) could be handed the repair's own
+    workspace."""
+    k, n = 128, 8
+    ds, pres_t, ref, damaged = _setup(ctx, k, n, 616)
+    present, status = _inputs(ds, pres_t, damaged)
+    h = ds.repair_start(present, status, ds.repair_workspace())
+    junk = torch.empty((ctx._L.dagpu_repair_workspace_size(k, n),), dtype=torch.uint8, device="cuda")
+    junk.fill_(0xA5)
+    ds.repair_join(h)
+    torch.cuda.synchronize()
+    assert torch.equal(ds.eds, ref) and (status.cpu().numpy() == 0).all()
+    assert h not in ds._held

@@ -139,5 +139,5 @@ case "$1" in
     bash tools/gpu_profile.sh r05 counters && \
     bash tools/gpu_pmc_gf16.sh repair512 repair512q3 split512 repair128 split1024 repair1024
     ;;
-  *) echo "steps: base mul332 first final-a final-b"; exit 2;;
+  *) echo "steps: base mul332 first pf probe skip splitov dectab zskip probe2 load64 enc64 colorder order order8 der64 wide2048 wtab final-a final-b"; exit 2;;
 esac
