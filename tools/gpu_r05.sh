@@ -132,6 +132,12 @@ case "$1" in
     bash tools/gpu_ab.sh --rounds 1 "bench:--mode repair --k 2048 --batch 1 --steps 1 --warmup 1" ws= w0=lib:celestia-app_amd/libdagpu_w0.so && \
     bash tools/gpu_ab.sh --rounds 1 "bench:--mode split --split-k 2048 --steps 2 --warmup 1" ws= w0=lib:celestia-app_amd/libdagpu_w0.so
     ;;
+  vtab)  # round 5: the decoders' dist-2 B layers read their skew tables with vector loads (no VGPR copies of SGPR pools)
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_gf16.py tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py > gpurun_out/r05_vtab_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r05_vtab_tests.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 3 repair512 vt= lb0=lib:celestia-app_amd/libdagpu_lb0.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 256 --batch 8 --steps 5 --warmup 1" vt= lb0=lib:celestia-app_amd/libdagpu_lb0.so
+    ;;
   final-a)  # round end, part 1: the whole -m gpu suite, the default bench line and its rocprofv3 kernel trace
     bash tools/gpu_final.sh
     ;;
