@@ -165,11 +165,17 @@ def extend_split_distributed(dist, part: SplitPart, ods_rows: torch.Tensor, grou
     part.step_rows(ods_rows, stream)
     all_to_all_blocks(dist, part.slab_top, part.send, group)
     part.step_cols(stream)
-    row_sub_all = torch.empty(part.parts * part.row_sub.numel(), dtype=torch.uint8, device=part.slab.device)
-    col_all = torch.empty(part.parts * part.col_roots.numel(), dtype=torch.uint8, device=part.slab.device)
-    all_gather_flat(dist, row_sub_all, part.row_sub, group)
-    all_gather_flat(dist, col_all, part.col_roots, group)
+    own = dist is None
+    if own:  # one part: its own records and roots are the gathered arrays
+        row_sub_all, col_all = part.row_sub, part.col_roots
+    else:
+        row_sub_all = torch.empty(part.parts * part.row_sub.numel(), dtype=torch.uint8, device=part.slab.device)
+        col_all = torch.empty(part.parts * part.col_roots.numel(), dtype=torch.uint8, device=part.slab.device)
+        all_gather_flat(dist, row_sub_all, part.row_sub, group)
+        all_gather_flat(dist, col_all, part.col_roots, group)
     rr, dah = part.step_finish(row_sub_all, col_all, stream)
+    if own:  # the caller's copy (the part's buffer is rewritten by its next square)
+        col_all = col_all.clone()
     # the status read-back is this step's one host wait, after all of it is queued
     status = max_status(dist, part.status, group)
     _check_status(status)

@@ -61,6 +61,25 @@ def test_split_overlap_modes(ctx, monkeypatch, k, parts, mode):
         assert (got_rr, got_cr, got_dah) == (rr, cr, dah)
 
 
+@pytest.mark.parametrize("k", [8, 512])
+def test_split_distributed_one_part(ctx, k):
+    """extend_split_distributed without a process group (bench.py's configs[4]
+    line at one GPU): no gathers, the part's own records feed the finish, and
+    the returned column roots are the caller's copy (the next square rewrites
+    the part's buffers)."""
+    ods, rr, cr, dah = _want(k, 7100 + k)
+    d = torch.from_numpy(np.ascontiguousarray(ods).reshape(-1)).cuda()
+    part = split.SplitPart(k, 1, 0, ctx, d.device)
+    got = split.extend_split_distributed(None, part, d)
+    torch.cuda.synchronize()
+    first = tuple(t.cpu().numpy().tobytes() for t in got)
+    assert first == (rr, cr, dah)
+    other = torch.from_numpy(np.ascontiguousarray(_want(k, 8100 + k)[0]).reshape(-1)).cuda()
+    split.extend_split_distributed(None, part, other)
+    torch.cuda.synchronize()
+    assert tuple(t.cpu().numpy().tobytes() for t in got) == first
+
+
 def test_split_push_order(ctx):
     k = 16
     ods = np.ascontiguousarray(synth.random_blob_square(k, 5)).reshape(k, k, 512).copy()
