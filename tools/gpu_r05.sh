@@ -138,7 +138,7 @@ case "$1" in
     bash tools/gpu_ab.sh --rounds 3 repair512 vt= lb0=lib:celestia-app_amd/libdagpu_lb0.so && \
     bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 256 --batch 8 --steps 5 --warmup 1" vt= lb0=lib:celestia-app_amd/libdagpu_lb0.so
     ;;
-  onepart)  # round 5: the split at one part passes its own records to the finish (no gather copies)
+  onepart)  # round 5: the split at one part passes its own records to the finish (no gather copies; the A/B switch was removed after this run)
     timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_split.py tests/test_gpu_bench_checks.py > gpurun_out/r05_onepart_tests.log 2>&1
     rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r05_onepart_tests.log; [ $rc -eq 0 ] || exit $rc
     bash tools/gpu_ab.sh --rounds 3 "bench:--mode split --split-k 512 --steps 20 --warmup 3" new= old=DAGPU_SPLIT_GATHER=1
