@@ -70,6 +70,9 @@ hipError_t launch_forest_roots(const uint8_t* leaves, const uint8_t* inner, cons
 hipError_t launch_ns_order_check(const uint8_t* base, long nvec, long nper, long vec_stride, long elem_stride,
                                  int32_t* status, int bit, hipStream_t s);
 
+// Packed 90-B nodes -> 96-B NMT records (the forest's record format).
+hipError_t launch_node_to_rec(const uint8_t* nodes, long n, uint8_t* recs, hipStream_t s);
+
 // Gather (row, depth, position) nodes of exported row trees as packed 90-B nodes.
 hipError_t launch_node_gather(const uint8_t* nodes, int w, const uint32_t* req, long n, uint8_t* out,
                               hipStream_t s);

@@ -415,6 +415,26 @@ __global__ __launch_bounds__(256) void node_gather_kernel(const uint8_t* nodes, 
   write_root(out + t * kNodeSize, mn, mx, dg);
 }
 
+// Packed 90-B nodes (minNs | maxNs | digest) -> 96-B records (each field
+// zero padded to 32 B), one lane per node.
+__global__ __launch_bounds__(256) void node_to_rec_kernel(const uint8_t* nodes, long n, uint8_t* recs) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* nd = nodes + i * kNodeSize;
+  uint8_t* r = recs + i * kRecNmt;
+  for (int b = 0; b < 32; b++) {
+    r[b] = b < 29 ? nd[b] : 0;
+    r[32 + b] = b < 29 ? nd[29 + b] : 0;
+    r[64 + b] = nd[58 + b];
+  }
+}
+
+hipError_t launch_node_to_rec(const uint8_t* nodes, long n, uint8_t* recs, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(node_to_rec_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, nodes, n, recs);
+  return hipGetLastError();
+}
+
 hipError_t launch_node_gather(const uint8_t* nodes, int w, const uint32_t* req, long n, uint8_t* out,
                               hipStream_t s) {
   if (n <= 0) return hipSuccess;

@@ -68,7 +68,9 @@ size_t split_ws_bytes(uint32_t k, uint32_t parts, SplitWs* out, void* base) {
   SplitPlans p = make_plans(k, parts);
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t o = off; off += al256(bytes > 0 ? bytes : 1); return o; };
-  const size_t o_tmp = take(rows * w * kSS);
+  // rows_tmp also holds the square roots workspace at one part (cols step)
+  const size_t sq_ws = parts == 1 ? dagpu::nmt_workspace_bytes((int)k, 1) : 0;
+  const size_t o_tmp = take(rows * w * kSS > sq_ws ? rows * w * kSS : sq_ws);
   const size_t o_leaves = take(w * W * dagpu::kRecNmt);
   const size_t o_ci = take((size_t)p.cols.inner_records * dagpu::kRecNmt);
   const size_t o_ri = take((size_t)p.rows.inner_records * dagpu::kRecNmt);
@@ -184,6 +186,36 @@ int dagpu_split_cols_device(dagpu_ctx* ctx, uint32_t k, uint32_t parts, uint32_t
   la.grid_c0 = (long)part * W;
   la.rfc = 0;
   la.out = ws.leaves;
+  // One part (below k = 1024, DAGPU_SPLIT_SQUARE != 0): the slab is the whole
+  // EDS, so the square pipeline's roots kernels apply as they are (48-B node
+  // records with namespace references, both axes' push order at level 1): its
+  // column roots go out directly, its row roots as the 96-B records the finish
+  // step reads.  (At k >= 1024 the forest path overlaps the top half's leaves
+  // with the column encode, which measured faster.)
+  const char* sq_env = getenv("DAGPU_SPLIT_SQUARE");
+  if (parts == 1 && k < 1024 && !(sq_env && sq_env[0] == '0')) {
+    {
+      ProfScope p(ctx, 1, s);
+      HIP_TRY(ctx, launch_rs_encode((int)k, ea, s));
+    }
+    SquareArgs sa{};
+    sa.eds = d_slab;
+    sa.eds_sq_stride = w * w * (long)kSS;
+    sa.k = (int)k;
+    sa.nsq = 1;
+    nmt_workspace_carve(sa, ws.rows_tmp);  // rows_tmp is unused at one part (rows are encoded in place)
+    sa.row_roots = ws.leaves;              // 2k packed row roots, then expanded into d_row_sub
+    sa.col_roots = d_col_roots;
+    sa.status = d_status;
+    {
+      ProfScope p(ctx, 2, s);
+      HIP_TRY(ctx, launch_nmt_leaves(sa, s));
+    }
+    ProfScope p(ctx, 3, s);
+    HIP_TRY(ctx, launch_nmt_trees(sa, s));
+    HIP_TRY(ctx, dagpu::launch_node_to_rec(ws.leaves, w, d_row_sub, s));
+    return DAGPU_OK;
+  }
   const char* ov_env = getenv("DAGPU_SPLIT_OVERLAP");
   const int overlap = ctx->prof ? 0 : ov_env ? atoi(ov_env) : k >= 1024 ? 1 : 0;
   hipStream_t es = overlap ? side_stream(ctx, s, overlap == 1 ? 1 : 0) : nullptr;

@@ -47,6 +47,17 @@ def test_split_local_matches_oracle(ctx, k, parts):
     assert got_dah == dah
 
 
+@pytest.mark.parametrize("square", ["0", "1"])
+@pytest.mark.parametrize("k", [1, 2, 16, 128, 512])
+def test_split_one_part_paths(ctx, monkeypatch, k, square):
+    """One part below k = 1024: the square pipeline's roots kernels (default) and
+    the forest path (DAGPU_SPLIT_SQUARE=0) give the oracle's roots and DAH."""
+    monkeypatch.setenv("DAGPU_SPLIT_SQUARE", square)
+    ods, rr, cr, dah = _want(k, 7100 + k)
+    d = torch.from_numpy(np.ascontiguousarray(ods).reshape(-1)).cuda()
+    assert split.extend_split_local(d, k, 1, ctx) == (rr, cr, dah)
+
+
 @pytest.mark.parametrize("mode", ["0", "1", "2"])
 @pytest.mark.parametrize("k,parts", [(2, 2), (64, 1), (512, 1), (512, 4)])
 def test_split_overlap_modes(ctx, monkeypatch, k, parts, mode):
@@ -93,12 +104,13 @@ def test_split_push_order(ctx):
         split.extend_split_local(d, k, 4, ctx)
 
 
-@pytest.mark.parametrize("parts", [1, 2, 4])
-def test_split_column_push_order(ctx, parts):
+@pytest.mark.parametrize("parts,square", [(1, "1"), (1, "0"), (2, "1"), (4, "1")])
+def test_split_column_push_order(ctx, monkeypatch, parts, square):
     """Every row sorted on its own but two rows swapped: only COLUMN trees see
     the violation.  The split must raise like the single-GPU DAH and the oracle
     (the column forest's push-order flag goes to the step's one status word;
     before round 5 it went to a per-tree slot past it and was lost)."""
+    monkeypatch.setenv("DAGPU_SPLIT_SQUARE", square)
     k = 16
     ods = np.ascontiguousarray(synth.random_blob_square(k, 12)).reshape(k, k, 512).copy()
     ods[[2, 9]] = ods[[9, 2]]

@@ -143,6 +143,12 @@ case "$1" in
     rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r05_onepart_tests.log; [ $rc -eq 0 ] || exit $rc
     bash tools/gpu_ab.sh --rounds 3 "bench:--mode split --split-k 512 --steps 20 --warmup 3" new= old=DAGPU_SPLIT_GATHER=1
     ;;
+  sqpath)  # round 5: one-part split below k = 1024 through the square pipeline's roots kernels (DAGPU_SPLIT_SQUARE=0: forests)
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_split.py > gpurun_out/r05_sqpath_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r05_sqpath_tests.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error" gpurun_out/r05_sqpath_tests.log | head; exit $rc; }
+    bash tools/gpu_ab.sh --rounds 3 "bench:--mode split --split-k 512 --steps 20 --warmup 3" sq= forest=DAGPU_SPLIT_SQUARE=0 && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode split --split-k 256 --steps 20 --warmup 3" sq= forest=DAGPU_SPLIT_SQUARE=0
+    ;;
   final-a)  # round end, part 1: the whole -m gpu suite, the default bench line and its rocprofv3 kernel trace
     bash tools/gpu_final.sh
     ;;
