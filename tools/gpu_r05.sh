@@ -149,6 +149,9 @@ case "$1" in
     bash tools/gpu_ab.sh --rounds 3 "bench:--mode split --split-k 512 --steps 20 --warmup 3" sq= forest=DAGPU_SPLIT_SQUARE=0 && \
     bash tools/gpu_ab.sh --rounds 2 "bench:--mode split --split-k 256 --steps 20 --warmup 3" sq= forest=DAGPU_SPLIT_SQUARE=0
     ;;
+  slices)  # round 5: the headline's RS/NMT pipeline slice count and first-slice size, re-checked on the final kernels
+    bash tools/gpu_ab.sh --rounds 2 headline s4= s6=DAGPU_PIPE_SLICES=6 s8=DAGPU_PIPE_SLICES=8 f32=DAGPU_PIPE_FIRST=32 f48=DAGPU_PIPE_FIRST=48
+    ;;
   final-a)  # round end, part 1: the whole -m gpu suite, the default bench line and its rocprofv3 kernel trace
     bash tools/gpu_final.sh
     ;;
