@@ -152,6 +152,14 @@ case "$1" in
   slices)  # round 5: the headline's RS/NMT pipeline slice count and first-slice size, re-checked on the final kernels
     bash tools/gpu_ab.sh --rounds 2 headline s4= s6=DAGPU_PIPE_SLICES=6 s8=DAGPU_PIPE_SLICES=8 f32=DAGPU_PIPE_FIRST=32 f48=DAGPU_PIPE_FIRST=48
     ;;
+  fillskip)  # round 5: Repair rounds launch a fill direction only when the plan put vectors in it (and size pair grids by count)
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py tests/test_gpu_repair_async.py tests/test_gpu_parity.py tests/test_gpu_gf16.py > gpurun_out/r05_fillskip_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r05_fillskip_tests.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error" gpurun_out/r05_fillskip_tests.log | head; exit $rc; }
+    bash tools/gpu_ab.sh --rounds 2 repair512 fs= fe0=lib:celestia-app_amd/libdagpu_fe0.so && \
+    bash tools/gpu_ab.sh --rounds 2 repair512q3 fs= fe0=lib:celestia-app_amd/libdagpu_fe0.so && \
+    bash tools/gpu_ab.sh --rounds 2 repair128 fs= fe0=lib:celestia-app_amd/libdagpu_fe0.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 128 --batch 256 --steps 3 --warmup 1 --pattern q3" fs= fe0=lib:celestia-app_amd/libdagpu_fe0.so
+    ;;
   final-a)  # round end, part 1: the whole -m gpu suite, the default bench line and its rocprofv3 kernel trace
     bash tools/gpu_final.sh
     ;;
