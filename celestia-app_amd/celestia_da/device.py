@@ -139,12 +139,17 @@ class DeviceSquares:
         return h.value
 
     def repair_join(self, handle: int, stream: Optional[torch.cuda.Stream] = None) -> None:
-        """dagpu_repair_join: `stream` waits for the started repair (whose
-        tensors are released afterwards: free them only in `stream`'s order)."""
+        """dagpu_repair_join: `stream` waits for the started repair.  The tensors
+        held since repair_start are released in `stream`'s order: record_stream
+        makes the caching allocator wait for the work queued on the join stream
+        (which includes the repair) before it reuses their blocks, whichever
+        stream allocated them."""
+        js = stream if stream is not None else torch.cuda.current_stream()
         try:
-            self._ck(self.ctx._L.dagpu_repair_join(self.ctx.handle, handle, _stream_handle(stream)))
+            self._ck(self.ctx._L.dagpu_repair_join(self.ctx.handle, handle, int(js.cuda_stream)))
         finally:
-            self._held.pop(handle, None)
+            for t in self._held.pop(handle, ()):
+                t.record_stream(js)
 
     def repair_workspace(self, count: Optional[int] = None) -> torch.Tensor:
         ws = self.ctx._L.dagpu_repair_workspace_size(self.k, self.n if count is None else count)

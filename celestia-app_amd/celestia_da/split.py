@@ -15,6 +15,7 @@ the block layout the collective sees.
 """
 from __future__ import annotations
 
+import contextlib
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -28,6 +29,14 @@ REC = 96  # row-subtree record: minNs[32] | maxNs[32] | digest[32]
 
 def _stream(s: Optional[torch.cuda.Stream]) -> int:
     return (s or torch.cuda.current_stream()).cuda_stream
+
+
+def _on(stream: Optional[torch.cuda.Stream]):
+    """The library's split steps only queue work on `stream` (no host sync
+    inside them), so every torch-side step between them -- copies, cat/clone,
+    status reads, the torch.distributed collectives -- must run in that
+    stream's order too: torch's current stream for the block."""
+    return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
 
 
 class SplitPart:
@@ -92,6 +101,11 @@ def extend_split_local(ods: torch.Tensor, k: int, parts: int, ctx: Context,
                        stream=None) -> Tuple[bytes, bytes, bytes]:
     """All P parts in this process on one GPU (all-to-all as device copies).
     ods: k*k*512 B device tensor.  Returns (row_roots, col_roots, dah) bytes."""
+    with _on(stream):
+        return _extend_split_local(ods, k, parts, ctx, stream)
+
+
+def _extend_split_local(ods, k, parts, ctx, stream):
     dev = ods.device
     ps = [SplitPart(k, parts, g, ctx, dev) for g in range(parts)]
     rows_b = ps[0].rows * k * SHARE_SIZE
@@ -161,7 +175,14 @@ def extend_split_distributed(dist, part: SplitPart, ods_rows: torch.Tensor, grou
                              stream=None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """One rank's share of the split: `ods_rows` are this rank's k/P Q0 rows
     (device).  Returns device tensors (row_roots 2k*90, col_roots 2k*90, dah 32),
-    identical on every rank.  Raises ErrInvalidPushOrder like NewDAH."""
+    identical on every rank.  Raises ErrInvalidPushOrder like NewDAH.  With a
+    `stream`, everything (the library steps, the collectives and the status
+    read) runs in that stream's order."""
+    with _on(stream):
+        return _extend_split_distributed(dist, part, ods_rows, group, stream)
+
+
+def _extend_split_distributed(dist, part, ods_rows, group, stream):
     part.step_rows(ods_rows, stream)
     all_to_all_blocks(dist, part.slab_top, part.send, group)
     part.step_cols(stream)

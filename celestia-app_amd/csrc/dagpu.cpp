@@ -134,10 +134,8 @@ int enqueue_roots(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_eds, ui
 // DAGPU_PIPELINE_CHUNK (squares) overrides it, e.g. to exercise many chunks in tests.
 size_t pipeline_chunk(uint32_t k, size_t n) {
   size_t m = (size_t(128) << 20) / ods_bytes(k);
-  if (const char* e = getenv("DAGPU_PIPELINE_CHUNK")) {
-    const long v = atol(e);
-    if (v > 0) m = (size_t)v;
-  }
+  const long v = sw_long(SW_PIPELINE_CHUNK);
+  if (v > 0) m = (size_t)v;
   return m < 1 ? 1 : (m > n ? n : m);
 }
 
@@ -413,12 +411,12 @@ void dagpu_destroy(dagpu_ctx* c) {
   for (auto e : c->stage_ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& cs : c->side)
-    for (hipStream_t x : {cs.rs, cs.rs_hi, cs.nmt})
+    for (hipStream_t x : {cs.rs, cs.rs_hi})
       if (x) (void)hipStreamSynchronize(x);
   for (auto e : c->ev_pool) (void)hipEventDestroy(e);
   for (void* m : c->mailboxes) (void)hipHostFree(m);
   for (auto& cs : c->side)
-    for (hipStream_t x : {cs.rs, cs.rs_hi, cs.nmt})
+    for (hipStream_t x : {cs.rs, cs.rs_hi})
       if (x) (void)hipStreamDestroy(x);
   for (auto& sl : c->async_slot) {
     if (sl.fork) (void)hipEventDestroy(sl.fork);
@@ -551,6 +549,37 @@ int dagpu_roots_device(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_ed
 }
 
 extern "C++" {  // external C++ helpers (runtime.hpp): split.cpp forks onto the side streams too
+namespace dagpu {
+
+// ---- switches (switches.hpp) ----
+namespace {
+const char* const kSwNames[SW_COUNT] = {
+    "DAGPU_PIPELINE_CHUNK", "DAGPU_PIPE_SLICES", "DAGPU_REPAIR_FILL", "DAGPU_SPLIT_SQUARE", "DAGPU_SPLIT_OVERLAP",
+    "DAGPU_DAH_SPLIT",      "DAGPU_DEC_SLICED",  "DAGPU_ENC_SLICED",  "DAGPU_ENC_SLICED2",  "DAGPU_GF16_WIDE"};
+thread_local const SwSnapshot* tl_sw = nullptr;
+}  // namespace
+
+const char* sw(Switch s) {
+  if (s < 0 || s >= SW_COUNT) return nullptr;
+  if (tl_sw) return tl_sw->set[s] ? tl_sw->v[s] : nullptr;
+  return getenv(kSwNames[s]);
+}
+
+long sw_long(Switch s, long dflt) {
+  const char* e = sw(s);
+  return e ? atol(e) : dflt;
+}
+
+void sw_snapshot(SwSnapshot* out) {
+  for (int i = 0; i < SW_COUNT; i++) {
+    const char* e = getenv(kSwNames[i]);
+    out->set[i] = e != nullptr;
+    out->v[i][0] = 0;
+    if (e) snprintf(out->v[i], sizeof out->v[i], "%s", e);
+  }
+}
+
+void sw_bind(const SwSnapshot* snap) { tl_sw = snap; }
 
 hipEvent_t ev_take(dagpu_ctx* c) {
   std::lock_guard<std::mutex> g(c->ev_mu);
@@ -570,18 +599,13 @@ void ev_give(dagpu_ctx* c, hipEvent_t e) {
   c->ev_pool.push_back(e);
 }
 
-long env_long(const char* name) {
-  const char* e = getenv(name);
-  return e ? atol(e) : 0L;
-}
-
 // Slices of a device batch for the RS/NMT pipeline: RS of slice i+1.. runs on
 // a side stream while the NMT kernels of slice i run on the caller's stream
 // (bench: 256 squares at k = 128, 4 slices 11.98 -> 11.63 ms; tools/pipe_exp.py).
 // DAGPU_PIPE_SLICES overrides (1 = off; read per call, so tests can vary it).
 // Off while profiling, so that every kernel's event bracket times that kernel alone.
 size_t pipe_slices(dagpu_ctx* ctx, uint32_t k, size_t n) {
-  const long env = env_long("DAGPU_PIPE_SLICES");
+  const long env = sw_long(SW_PIPE_SLICES);
   if (ctx->prof) return 1;
   size_t s = env > 0 ? (size_t)env : (k >= 128 && n >= 64 ? 4 : 1);
   while (s > 1 && n / s < 8) s >>= 1;
@@ -589,7 +613,7 @@ size_t pipe_slices(dagpu_ctx* ctx, uint32_t k, size_t n) {
 }
 
 // The side streams paired with caller stream `s` (created on first use).
-// which: 0 = RS, 1 = RS at the device's greatest stream priority, 2 = NMT.
+// which: 0 = normal priority, 1 = the device's greatest stream priority.
 hipStream_t side_stream(dagpu_ctx* ctx, hipStream_t s, int which) {
   std::lock_guard<std::mutex> g(ctx->side_mu);
   dagpu_ctx::Side* sd = nullptr;
@@ -607,7 +631,7 @@ hipStream_t side_stream(dagpu_ctx* ctx, hipStream_t s, int which) {
       sd->caller = s;
     }
   }
-  hipStream_t* slot = which == 0 ? &sd->rs : which == 1 ? &sd->rs_hi : &sd->nmt;
+  hipStream_t* slot = which == 1 ? &sd->rs_hi : &sd->rs;
   if (!*slot) {
     hipError_t e;
     if (which == 1) {
@@ -625,6 +649,7 @@ hipStream_t side_stream(dagpu_ctx* ctx, hipStream_t s, int which) {
   return *slot;
 }
 
+}  // namespace dagpu
 }  // extern "C++"
 
 int dagpu_extend_batch_device(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_t* d_ods,
@@ -653,22 +678,15 @@ int dagpu_extend_batch_device(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_
     for (auto x : ev) ev_give(ctx, x);
     return r;
   };
-  hipStream_t rs = side_stream(ctx, s, env_long("DAGPU_RS_PRIO") > 0 ? 1 : 0);
+  hipStream_t rs = side_stream(ctx, s, 0);
   if (!rs) return done(set_err(ctx, DAGPU_ERR_DEVICE, "hipStreamCreate failed"));
   const size_t w = 2 * (size_t)k;
   if (hipEventRecord(ev[S], s) != hipSuccess || hipStreamWaitEvent(rs, ev[S], 0) != hipSuccess)
     return done(set_err(ctx, DAGPU_ERR_DEVICE, "pipeline fork failed"));
-  // slice boundaries: a smaller first slice shortens the RS run nothing overlaps
+  // equal slices (tried and dropped, profiles/pipeline_r02.log, pipe_streams_r03.log:
+  // a smaller first slice, a high-priority RS stream, a second NMT stream)
   std::vector<size_t> cut(S + 1);
-  {
-    const long first_env = env_long("DAGPU_PIPE_FIRST");
-    size_t f = first_env > 0 ? (size_t)first_env : n / S;
-    if (f < 1) f = 1;
-    if (f > n - (S - 1)) f = n - (S - 1);
-    cut[0] = 0;
-    cut[1] = f;
-    for (size_t i = 2; i <= S; i++) cut[i] = f + (n - f) * (i - 1) / (S - 1);
-  }
+  for (size_t i = 0; i <= S; i++) cut[i] = n * i / S;
   for (size_t i = 0; i < S; i++) {
     const size_t a = cut[i], b = cut[i + 1];
     rc = enqueue_rs(ctx, k, b - a, d_ods ? d_ods + a * ods_bytes(k) : nullptr, d_eds + a * eds_bytes(k), rs);
@@ -676,41 +694,16 @@ int dagpu_extend_batch_device(dagpu_ctx* ctx, uint32_t k, size_t n, const uint8_
     if (hipEventRecord(ev[i], rs) != hipSuccess) return done(set_err(ctx, DAGPU_ERR_DEVICE, "hipEventRecord failed"));
   }
   // NMT work of the slices: in order on the caller's stream, sharing the front
-  // of the workspace; or (DAGPU_PIPE_NMT2) odd slices on a second NMT stream
-  // with the workspace's second half, so the latency-bound tree levels and DAH
-  // of one slice overlap the leaves of the next.  Waiting on the last slice's
-  // event joins the RS stream; the NMT stream is joined with one more event.
-  size_t maxs = 0;
-  for (size_t i = 0; i < S; i++) maxs = std::max(maxs, cut[i + 1] - cut[i]);
-  const size_t ws_half = (nmt_workspace_bytes((int)k, (long)maxs) + 255) & ~(size_t)255;
-  hipStream_t nmt2 = nullptr;
-  if (env_long("DAGPU_PIPE_NMT2") > 0 && 2 * ws_half + 256 <= dagpu_workspace_size(k, n)) {
-    nmt2 = side_stream(ctx, s, 2);
-    if (!nmt2) return done(set_err(ctx, DAGPU_ERR_DEVICE, "hipStreamCreate failed"));
-  }
-  hipEvent_t ev_join = nullptr;
-  if (nmt2 && !(ev_join = ev_take(ctx)))
-    return done(set_err(ctx, DAGPU_ERR_DEVICE, "hipEventCreate failed"));
-  auto done2 = [&](int r) {
-    ev_give(ctx, ev_join);
-    return done(r);
-  };
+  // of the workspace; waiting on the last slice's event joins the RS stream
   for (size_t i = 0; i < S; i++) {
     const size_t a = cut[i], b = cut[i + 1];
-    const bool alt = nmt2 && (i & 1);
-    hipStream_t ns = alt ? nmt2 : s;
-    if (hipStreamWaitEvent(ns, ev[i], 0) != hipSuccess)
-      return done2(set_err(ctx, DAGPU_ERR_DEVICE, "hipStreamWaitEvent failed"));
+    if (hipStreamWaitEvent(s, ev[i], 0) != hipSuccess)
+      return done(set_err(ctx, DAGPU_ERR_DEVICE, "hipStreamWaitEvent failed"));
     rc = enqueue_roots(ctx, k, b - a, d_eds + a * eds_bytes(k), d_row_roots + a * w * kNodeSize,
-                       d_col_roots + a * w * kNodeSize, d_dah + a * 32, d_status + a,
-                       (uint8_t*)d_workspace + (alt ? ws_half : 0), ns);
-    if (rc) return done2(rc);
+                       d_col_roots + a * w * kNodeSize, d_dah + a * 32, d_status + a, (uint8_t*)d_workspace, s);
+    if (rc) return done(rc);
   }
-  if (nmt2) {
-    if (hipEventRecord(ev_join, nmt2) != hipSuccess || hipStreamWaitEvent(s, ev_join, 0) != hipSuccess)
-      return done2(set_err(ctx, DAGPU_ERR_DEVICE, "pipeline join failed"));
-  }
-  return done2(DAGPU_OK);
+  return done(DAGPU_OK);
 }
 
 int dagpu_roots(dagpu_ctx* ctx, uint32_t k, const uint8_t* eds, uint8_t* row_roots,
@@ -1202,7 +1195,7 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
   // that pattern; otherwise a compare-mode encode checks every deferred vector,
   // and a square that fails is re-run from its original presence without
   // deferral (the decoders read present shards only).
-  const char* fill_env = getenv("DAGPU_REPAIR_FILL");  // read per call (tests compare both)
+  const char* fill_env = sw(SW_REPAIR_FILL);  // read per call (tests compare both)
   const bool shortcut = !(fill_env && fill_env[0] == '0');
   const bool fill_list = k == 128;
   if (shortcut) {
@@ -1463,14 +1456,22 @@ int dagpu_repair_start(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uin
   // may escape an extern "C" entry point, and the slot stays free
   try {
     auto mb = std::make_shared<Mailbox>(ctx);
+    auto snap = std::make_shared<SwSnapshot>();
+    sw_snapshot(snap.get());  // on the caller's thread (getenv is not thread-safe against setenv)
+#ifdef DAGPU_TEST_HOOKS
+    const char* inj = getenv("DAGPU_TEST_WORKER_FAIL");
+    const bool inject_fail = inj && inj[0] == '1';
+#endif
     sl.worker = std::thread([=]() {
       on_repair_worker() = true;
+      sw_bind(snap.get());  // the switches as the start call saw them
       (void)hipSetDevice(dev);
       int r = hipStreamWaitEvent(ws, fork, 0) == hipSuccess ? DAGPU_OK : DAGPU_ERR_DEVICE;
-      // DAGPU_TEST_WORKER_FAIL=1 (tests/test_gpu_repair_async.py): the worker
-      // fails before its first kernel, so the join's error path is exercised
-      const char* inj = getenv("DAGPU_TEST_WORKER_FAIL");
-      if (r == DAGPU_OK && inj && inj[0] == '1') r = set_err(ctx, DAGPU_ERR_DEVICE, "injected worker failure");
+#ifdef DAGPU_TEST_HOOKS
+      // test build only (libdagpu_test.so, tests/test_gpu_repair_async.py): the
+      // worker fails before its first kernel, so the join's error path is exercised
+      if (r == DAGPU_OK && inject_fail) r = set_err(ctx, DAGPU_ERR_DEVICE, "injected worker failure");
+#endif
       if (r == DAGPU_OK && n)
         r = repair_device(ctx, k, n, d_eds, d_present, d_row_roots, d_col_roots, d_status, nullptr, d_workspace, ws,
                           mb.get(), slp->stats);

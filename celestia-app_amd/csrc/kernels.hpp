@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "switches.hpp"
+
 namespace dagpu {
 
 constexpr int kShareSize = 512;

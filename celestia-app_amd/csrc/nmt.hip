@@ -425,22 +425,11 @@ __global__ __launch_bounds__(kDahThreads) void dah_top_kernel(SquareArgs a) {
   if (threadIdx.x < 8) ((uint32_t*)(a.dah + sq * 32))[threadIdx.x] = root[threadIdx.x];
 }
 
-// DAGPU_LEAF_LDS_KB (experiments): dynamic LDS requested per leaf workgroup,
-// which caps the leaf kernel's occupancy (it uses no LDS) to leave room on a
-// CU for RS workgroups of a pipelined batch.
-static size_t leaf_lds_bytes() {
-  static const size_t v = [] {
-    const char* e = getenv("DAGPU_LEAF_LDS_KB");
-    return e ? (size_t)atol(e) * 1024 : (size_t)0;
-  }();
-  return v;
-}
-
 hipError_t launch_nmt_leaves(const SquareArgs& a, hipStream_t s) {
   const long w = 2L * a.k;
   const long total = w * w * a.nsq;
   const long blocks = (total + kLeafWave - 1) / kLeafWave;
-  hipLaunchKernelGGL(nmt_leaf_kernel, dim3((unsigned)blocks), dim3(kLeafWave), leaf_lds_bytes(), s, a);
+  hipLaunchKernelGGL(nmt_leaf_kernel, dim3((unsigned)blocks), dim3(kLeafWave), 0, s, a);
   return hipGetLastError();
 }
 
@@ -491,7 +480,7 @@ void nmt_workspace_carve(SquareArgs& a, void* ws) {
 }
 
 static bool dah_split_enabled() {  // DAGPU_DAH_SPLIT=0: one workgroup per square always (A/B)
-  const char* e = getenv("DAGPU_DAH_SPLIT");
+  const char* e = sw(SW_DAH_SPLIT);
   return !(e && e[0] == '0');
 }
 

@@ -243,13 +243,11 @@ void leo8_decode128_sliced_kernel(DecodeArgs a) {
   DEC8_PROBE(13);
 }
 
-// DAGPU_DEC_SLICED=0 keeps k = 128 on the packed-byte decoder (A/B runs).
+// DAGPU_DEC_SLICED=0 keeps k = 128 on the packed-byte decoder (A/B runs;
+// read per launch through sw(), see switches.hpp).
 static bool dec_sliced_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("DAGPU_DEC_SLICED");
-    return !(e && e[0] == '0');
-  }();
-  return on;
+  const char* e = sw(SW_DEC_SLICED);
+  return !(e && e[0] == '0');
 }
 
 bool leo8_decode_sliced_applicable(const DecodeArgs& a) {

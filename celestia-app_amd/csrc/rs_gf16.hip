@@ -9,14 +9,14 @@
 // reference golden vector exists for k > 128; the kernels are checked against
 // the oracle's GF(2^16) restatement and by erase/decode round trips.
 //
-// Layout.  One 256-thread workgroup transforms one 64-byte column block of one
-// vector: the m (encode) or n = 2k (decode) elements of 32 symbols live in LDS
-// as uint16 rows of 64 B.  Every radix-2 butterfly step is a pass over
-// (pair, symbol) items with a barrier between steps; the 32 lanes of a pair
-// share one skew constant.  The multiply is log/exp through 128 KiB tables in
-// global memory (L2-resident), so this path is latency/L2 bound, not VALU
-// bound -- adequate for the stress sizes, where SHA-256 over the 2-4x larger
-// square dominates anyway.
+// Kernels.  k = 256 and 512 run register-resident half-lane kernels
+// (leo16_encode_h_kernel, leo16_decode_h_kernel: a lane holds 4 symbols of two
+// elements, one per half wave, and multiplies by 3/3/2-split v_perm product
+// tables); wider squares the LDS-slice kernels of rs_gf16_wide.hip.  A decode
+// whose shard size is not a multiple of 256 B (codec API) takes the generic
+// leo16_decode_kernel: one 256-thread workgroup per 64-B column block, the
+// n = 2k elements of 32 symbols as uint16 rows in LDS, log/exp multiplies
+// through 128 KiB tables in global memory (L2-resident).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -38,7 +38,6 @@ constexpr uint32_t kMod16 = 65535u;
 __device__ uint16_t g_log16[65536];
 __device__ uint16_t g_exp16[65536];
 __device__ uint16_t g_skew16[65536];
-__device__ uint16_t g_walsh16[65536];
 // Folded Walsh weights for the n-point error-locator transform (n = 2k =
 // 512, 1024): g_wfold16[n == 1024][r] = sum_q walsh[q*n + r] mod 65535.
 __device__ uint16_t g_wfold16[2][1024];
@@ -158,83 +157,6 @@ __device__ void fft16(uint16_t* w, int m, int fo) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// Encode: parity = FFT_m(IFFT_m(data)), m = k.  Same EncodeArgs addressing as
-// the GF(2^8) encoder, including Q0 placement, compare mode and the reverse
-// fill (IFFT at skew offset 0, FFT at offset m).
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kThreads16) void leo16_encode_kernel(EncodeArgs a, int k) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t w16[];  // k rows of 32 symbols
-  const long nblk = a.shard_bytes / 64;
-  const long blk = blockIdx.x % nblk;
-  const long v = blockIdx.x / nblk;
-  const long sq = v / a.nvec, vec = v % a.nvec;
-  if (vec_skipped(a, v)) return;  // uniform
-  const uint8_t* in = a.in + sq * a.in_sq_stride + vec * a.in_vec_stride + blk * 64;
-  for (int t = threadIdx.x; t < k * 8; t += kThreads16) {
-    const int e = t >> 3, q = t & 7;
-    const uint32_t* src = (const uint32_t*)(in + (long)e * a.in_shard_stride);
-    const uint32_t lo = src[q], hi = src[q + 8];
-    block_to_lds(w16 + e * 32, lo, hi, q);
-    if (a.copy) {
-      uint32_t* dst = (uint32_t*)(a.copy + sq * a.copy_sq_stride + vec * a.copy_vec_stride +
-                                  (long)e * a.copy_shard_stride + blk * 64);
-      dst[q] = lo;
-      dst[q + 8] = hi;
-    }
-  }
-  __syncthreads();
-  ifft16(w16, k, a.reverse ? -1 : k - 1);
-  fft16(w16, k, a.reverse ? k : 0);
-  uint8_t* out = a.out + sq * a.out_sq_stride + vec * a.out_vec_stride + blk * 64;
-  bool diff = false;
-  for (int t = threadIdx.x; t < k * 8; t += kThreads16) {
-    const int e = t >> 3, q = t & 7;
-    uint32_t lo, hi;
-    lds_to_block(w16 + e * 32, lo, hi, q);
-    uint32_t* dst = (uint32_t*)(out + (long)e * a.out_shard_stride);
-    if (a.mismatch || (a.out_present && fill_given(a, sq, vec, e))) {
-      diff |= (dst[q] != lo) || (dst[q + 8] != hi);
-    } else {
-      dst[q] = lo;
-      dst[q + 8] = hi;
-    }
-  }
-  if (a.mismatch && __builtin_amdgcn_ballot_w64(diff) != 0 && (threadIdx.x & 63) == 0) {
-    atomicOr(a.mismatch + sq, a.mismatch_bit);
-    if (a.mismatch_vec) a.mismatch_vec[sq * a.nvec + vec] = 1;
-  }
-  if (a.out_present && !a.mismatch && diff) a.redo[v] = 1;  // Repair fill: a given shard differs
-}
-
-// ---------------------------------------------------------------------------
-// Error locators: one 1024-thread workgroup per vector, FWHT over the whole
-// 65536-entry field in LDS (128 KiB of uint16).  The reference's first FWHT
-// truncates at mtrunc = 2k; entries past 2k are zero, so the full transform is
-// the same function.  Values are only congruent mod 65535 to the reference's
-// (partial reduction), which is all their use as log multipliers needs.
-// ---------------------------------------------------------------------------
-constexpr int kErrThreads = 1024;
-constexpr int kErrLds = 65536 * 2 + 16;
-
-__device__ void fwht65536(uint16_t* e) {
-  for (int dist = 1; dist < 65536; dist <<= 2) {
-    const int dist4 = dist << 2;
-    for (int g = threadIdx.x; g < 16384; g += kErrThreads) {
-      const int r = (g / dist) * dist4;
-      const int i = r + (g % dist);
-      const uint32_t t0 = e[i], t1 = e[i + dist], t2 = e[i + 2 * dist], t3 = e[i + 3 * dist];
-      const uint32_t a0 = add_mod16(t0, t1), a1 = sub_mod16(t0, t1);
-      const uint32_t a2 = add_mod16(t2, t3), a3 = sub_mod16(t2, t3);
-      e[i] = (uint16_t)add_mod16(a0, a2);
-      e[i + 2 * dist] = (uint16_t)sub_mod16(a0, a2);
-      e[i + dist] = (uint16_t)add_mod16(a1, a3);
-      e[i + 3 * dist] = (uint16_t)sub_mod16(a1, a3);
-    }
-    __syncthreads();
-  }
-}
-
 // The same locators from n-point transforms (n = 2k <= 1024).  The erasure
 // vector is zero past n, so its 65536-point FWHT is n-periodic (popcount(i & j)
 // only sees the low log2(n) bits of j when i < n), and only the first n
@@ -318,48 +240,6 @@ __global__ __launch_bounds__(kFoldThreads) void leo16_errlocs_fold_kernel(Decode
   for (int i = threadIdx.x; i < N; i += kFoldThreads) out[i] = (uint16_t)e[i];
 }
 
-__global__ __launch_bounds__(kErrThreads) void leo16_errlocs_kernel(DecodeArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t e16[];  // 65536 entries + counter
-  int& cnt_s = *(int*)(e16 + 65536);
-  const long v = blockIdx.x;
-  const long sq = v / a.nvec, vec = v % a.nvec;
-  const int k = a.k, n = 2 * k;
-  const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
-  if (a.locators_only && (!a.flags[v] || !err_computes(a, v, err_vec(a, v)))) return;  // uniform
-  if (threadIdx.x == 0) cnt_s = 0;
-  __syncthreads();
-  int cnt = 0;
-  for (int i = threadIdx.x; i < 65536; i += kErrThreads) {
-    uint32_t x = 0;
-    if (i < k) x = pres[(long)(k + i) * a.p_shard_stride] ? 0u : 1u;       // parity k+i -> work i
-    else if (i < n) x = pres[(long)(i - k) * a.p_shard_stride] ? 0u : 1u;  // data i-k -> work i
-    e16[i] = (uint16_t)x;
-    if (i < n) cnt += (x == 0);
-  }
-  atomicAdd(&cnt_s, cnt);
-  __syncthreads();
-  const int present = cnt_s;
-  bool decode = true;
-  if (!a.locators_only) {
-    decode = present >= k && present < n && vec_selected(a, v);
-    if (threadIdx.x == 0) {
-      a.flags[v] = decode ? 1 : 0;
-      if (present < k && a.too_few) atomicOr(a.too_few, 1);
-      if (decode && a.ndecodable) atomicAdd(a.ndecodable, 1);
-    }
-  }
-  if (!decode) return;  // uniform
-  const long hv = err_vec(a, v);
-  if (!err_computes(a, v, hv)) return;  // shares an earlier vector's locators
-  fwht65536(e16);
-  for (int i = threadIdx.x; i < 65536; i += kErrThreads)
-    e16[i] = (uint16_t)(((uint32_t)e16[i] * (uint32_t)g_walsh16[i]) % kMod16);
-  __syncthreads();
-  fwht65536(e16);
-  uint16_t* out = (uint16_t*)(a.err + hv * (long)rs_err_bytes(k));
-  for (int i = threadIdx.x; i < n; i += kErrThreads) out[i] = e16[i];
-}
-
 // ---------------------------------------------------------------------------
 // Decode: one 256-thread workgroup per (vector, 64-B column block); LDS holds
 // work (n rows) and the formal-derivative output (n rows).
@@ -436,23 +316,11 @@ __global__ __launch_bounds__(256) void mark_present16_kernel(DecodeArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Register-resident GF(2^16) encode (k = m = 256, 512).
-//
-// A wave owns the 64 thread-columns of one 512-B chunk of a vector (lane l:
-// 64-B block l >> 3, symbols 4(l & 7) .. +3 as a lo-byte dword and a hi-byte
-// dword); a workgroup of P = m / 64 waves holds the whole transform, wave q
-// keeping 64 elements (128 VGPRs).  Index bits 0-5 are local in the "block"
-// layout (wave q holds 64q + j); a P x P block transpose through LDS makes
-// bits 6.. local ("transposed" layout: wave q holds the elements whose bits
-// 6-log2P .. 5 equal q), where the top IFFT/FFT layers run.  Multiplies use
-// per-skew-position product tables (16 dwords: for each 2-bit group of the
-// symbol, the 4 possible products' lo and hi bytes) read with scalar loads --
-// the position is wave-uniform -- and 16 v_perm lookups per 4 symbols; a
-// position whose skew is 65535 (leopard "skip") has an all-zero table.
+// Register-resident GF(2^16) transforms (k = 256, 512; the half-lane kernels
+// below).  Multiplies by a skew use per-position product tables read with
+// scalar loads (the position is wave-uniform); a position whose skew is 65535
+// (leopard "skip") has an all-zero table.
 // ---------------------------------------------------------------------------
-// Positions < 2m = 1024 cover every encoder skew index (IFFT m-1+iend+2d <
-// 2m, FFT iend-1 < m).  __constant__ so that the wave-uniform table reads
-// become scalar loads into SGPRs (64 KiB, the constant-segment limit).
 // a wave-uniform value the compiler cannot see through: values derived from it
 // in one phase are not kept live (in SGPRs, then spilled) for the next
 __device__ __forceinline__ int opaque_s(int x) {
@@ -460,33 +328,10 @@ __device__ __forceinline__ int opaque_s(int x) {
   return x;
 }
 
+// Positions < 2m = 1024 cover every encoder skew index (IFFT m-1+iend+2d <
+// 2m, FFT iend-1 < m) and every k = 512 decoder one (iend - 1 < n).
+// __constant__ so that the wave-uniform table reads become scalar loads.
 constexpr int kTabPos = 1024;
-__constant__ uint32_t g_ptab16[kTabPos * 16];
-
-// Encoder: the last IFFT layer and the first FFT layer butterfly the same
-// pairs (y ^= x; x ^= y A, then x ^= y B; y ^= x), so x ^= y (A ^ B) with one
-// table for the field element A ^ B: [0] M = 256 (positions 383 / 127), [1]
-// M = 512 (767 / 255) -- the same for the reverse fill, which swaps them.  One
-// multiply fewer per pair, and no selectors kept live from one layer to the
-// next (they spilled ~180 VGPRs).
-__constant__ uint32_t g_ptab16_merged[2 * 16];
-
-__device__ __forceinline__ void mul16_add_t(uint32_t& xlo, uint32_t& xhi, uint32_t ylo, uint32_t yhi,
-                                            const uint32_t* t) {
-  uint32_t pl[8], ph[8];
-#pragma unroll
-  for (int g = 0; g < 4; g++) {
-    const uint32_t sl = (ylo >> (2 * g)) & 0x03030303u;
-    const uint32_t sh = (yhi >> (2 * g)) & 0x03030303u;
-    pl[g] = __builtin_amdgcn_perm(t[g], t[g], sl);
-    ph[g] = __builtin_amdgcn_perm(t[8 + g], t[8 + g], sl);
-    pl[4 + g] = __builtin_amdgcn_perm(t[4 + g], t[4 + g], sh);
-    ph[4 + g] = __builtin_amdgcn_perm(t[12 + g], t[12 + g], sh);
-  }
-  // 8 products + x per output byte plane: four 3-input XORs
-  xlo = xor3(xor3(xor3(xlo, pl[0], pl[1]), xor3(pl[2], pl[3], pl[4]), pl[5]), pl[6], pl[7]);
-  xhi = xor3(xor3(xor3(xhi, ph[0], ph[1]), xor3(ph[2], ph[3], ph[4]), ph[5]), ph[6], ph[7]);
-}
 
 // 3/3/2 split (round 5): each byte of y in groups of 3, 3 and 2 bits, so a
 // symbol takes 6 lookups per output byte instead of 8.  A 3-bit group indexes
@@ -520,27 +365,17 @@ __device__ __forceinline__ void mul16x_add_t(uint32_t& xlo, uint32_t& xhi, uint3
   xhi = xor3(xor3(xor3(xhi, h0, h1), h2, h3), h4, h5);
 }
 
-// DAGPU_GF16_MUL2 builds keep the 2-bit split everywhere (A/B of round 5)
-#ifdef DAGPU_GF16_MUL2
-__device__ __forceinline__ void mul16_add(uint32_t& xlo, uint32_t& xhi, uint32_t ylo, uint32_t yhi, int pos) {
-  mul16_add_t(xlo, xhi, ylo, yhi, g_ptab16 + pos * 16);
-}
-#define MERGED_TAB(m) (g_ptab16_merged + 16 * (m))
-#define MERGED_MUL mul16_add_t
-#else
 __device__ __forceinline__ void mul16_add(uint32_t& xlo, uint32_t& xhi, uint32_t ylo, uint32_t yhi, int pos) {
   mul16x_add_t(xlo, xhi, ylo, yhi, g_ptab16x + pos * kTab16x);
 }
 #define MERGED_TAB(m) (g_ptab16x_merged + kTab16x * (m))
 #define MERGED_MUL mul16x_add_t
-#endif
 
 // NS elements per lane, 4 symbols each as a low-byte and a high-byte dword
 template <int NS>
 struct W16n {
   uint32_t lo[NS], hi[NS];
 };
-using W16 = W16n<64>;
 
 // ifftDIT2: y ^= x; x ^= y * skew[pos]
 template <class W>
@@ -567,814 +402,20 @@ __device__ __forceinline__ void ifft_fft2_16(W& w, int i, int j, const uint32_t*
   w.hi[j] ^= w.hi[i];
 }
 
-// Block layout, encoder IFFT radix-4 steps with dist D.. (up to the NS slots:
-// bits 0-5 for 64); base = m - 1 + NS q (ifftDITEncoder skew index m - 1 + iend).
-template <int D, int NS = 64, class W>
-__device__ __forceinline__ void ifft16_block(W& w, int base) {
-#pragma unroll
-  for (int r = 0; r < NS; r += 4 * D) {
-    // per unit, an opaque base: the unit's tables are loaded at the unit, not
-    // hoisted (with the 20-dword tables, hoisting spilled SGPRs and VGPRs)
-    const int p01 = opaque_s(base) + r + D, p02 = p01 + D, p23 = p01 + 2 * D;
-#pragma unroll
-    for (int i = r; i < r + D; i++) ifft2_16(w, i, i + D, p01);  // layer by layer: one table's
-#pragma unroll                                                      // VGPR copies live at a time
-    for (int i = r; i < r + D; i++) ifft2_16(w, i + 2 * D, i + 3 * D, p23);
-#pragma unroll
-    for (int i = r; i < r + D; i++) {
-      ifft2_16(w, i, i + 2 * D, p02);
-      ifft2_16(w, i + D, i + 3 * D, p02);
-    }
-    // per unit: otherwise every table of the block is loaded up front (SGPR spills)
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  if constexpr (D * 16 <= NS) ifft16_block<D * 4, NS>(w, base);
-}
+// log of the element 1 << b (the decoders' per-element table builder)
+__constant__ uint16_t g_logbit16[16];
 
-// Block layout, fftDIT radix-4 step with dist DIST (dist4 = 4 DIST) and the
-// ones below it; base = FO + NS q (skew index FO + iend - 1).  The final radix-2 layer
-// exists when the last dist4 is 2.
-template <int DIST, int NS = 64, class W>
-__device__ __forceinline__ void fft16_block(W& w, int base) {
-#pragma unroll
-  for (int r = 0; r < NS; r += 4 * DIST) {
-    const int iend = r + DIST;
-    const int b = opaque_s(base);  // as in ifft16_block
-    const int p01 = b + iend - 1, p02 = b + iend + DIST - 1, p23 = b + iend + 2 * DIST - 1;
-#pragma unroll
-    for (int i = r; i < r + DIST; i++) {  // layer by layer, as in ifft16_block
-      fft2_16(w, i, i + 2 * DIST, p02);
-      fft2_16(w, i + DIST, i + 3 * DIST, p02);
-    }
-#pragma unroll
-    for (int i = r; i < r + DIST; i++) fft2_16(w, i, i + DIST, p01);
-#pragma unroll
-    for (int i = r; i < r + DIST; i++) fft2_16(w, i + 2 * DIST, i + 3 * DIST, p23);
-    __builtin_amdgcn_sched_barrier(0);  // as in ifft16_block
-  }
-  if constexpr (DIST >= 4) {
-    fft16_block<DIST / 4, NS>(w, base);
-  } else if constexpr (DIST == 2) {
-#pragma unroll
-    for (int r = 0; r < NS; r += 2) {
-      fft2_16(w, r, r + 1, opaque_s(base) + r);
-      if (r % 8 == 6) __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-}
-
-// P x P block transpose: element (wave Q, slot (c << R) | l) <-> (wave c,
-// slot (Q << R) | l), R = log2 NS - log2 P, S group-slots per LDS round.
-template <int P, int S, int NS = 64, class W>
-__device__ __forceinline__ void xpose16(W& w, uint32_t* lds, int q, int lane) {
-  constexpr int R = __builtin_ctz(NS) - __builtin_ctz(P);
-  constexpr int G = 1 << R;
-  // lds[(dst * P + src) * S + u][2][64]
-#pragma unroll
-  for (int l0 = 0; l0 < G; l0 += S) {
-#pragma unroll
-    for (int c = 0; c < P; c++)
-#pragma unroll
-      for (int u = 0; u < S; u++) {
-        uint32_t* d = lds + (((c * P + q) * S + u) * 2) * 64 + lane;
-        d[0] = w.lo[(c << R) | (l0 + u)];
-        d[64] = w.hi[(c << R) | (l0 + u)];
-      }
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < P; c++)
-#pragma unroll
-      for (int u = 0; u < S; u++) {
-        const uint32_t* d = lds + (((q * P + c) * S + u) * 2) * 64 + lane;
-        w.lo[(c << R) | (l0 + u)] = d[0];
-        w.hi[(c << R) | (l0 + u)] = d[64];
-      }
-    __syncthreads();
-  }
-}
-
-// Register encoders' data movement.  Element j of wave q is shard NS q + j;
-// lane: 64-B block (lane >> 3) of the 512-B chunk, symbols 4 (lane & 7) .. +3.
-template <int NS>
-__device__ __forceinline__ void enc16_load(const EncodeArgs& a, W16n<NS>& w, int q, long sq, long vec, uint32_t col,
-                                           uint32_t cl, bool active) {
-  const auto in_rsrc = make_rsrc(a.in + sq * a.in_sq_stride + vec * a.in_vec_stride);
-  const uint32_t in_stride = (uint32_t)a.in_shard_stride;
-#pragma unroll
-  for (int j = 0; j < NS; j++) {
-    const uint32_t so = (uint32_t)(NS * q + j) * in_stride;
-    w.lo[j] = __builtin_amdgcn_raw_buffer_load_b32(in_rsrc, cl, so, 0);
-    w.hi[j] = __builtin_amdgcn_raw_buffer_load_b32(in_rsrc, cl + 32u, so, 0);
-  }
-  if (a.copy && active) {
-    const auto cp = make_rsrc(a.copy + sq * a.copy_sq_stride + vec * a.copy_vec_stride);
-    const uint32_t cs = (uint32_t)a.copy_shard_stride;
-#pragma unroll
-    for (int j = 0; j < NS; j++) {
-      const uint32_t so = (uint32_t)(NS * q + j) * cs;
-      __builtin_amdgcn_raw_buffer_store_b32(w.lo[j], cp, col, so, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(w.hi[j], cp, col + 32u, so, 0);
-    }
-  }
-}
-
-// Repair fill: which of the wave's NS out-half shards are given (bit j:
-// shard NS q + j), read before the transform so that the store loop does not
-// wait on presence loads.
-template <int NS>
-__device__ __forceinline__ uint64_t enc16_given(const EncodeArgs& a, int q, long sq, long vec, int lane) {
-  if (!a.out_present) return 0;
-  const bool g = lane < NS && fill_given(a, sq, vec, NS * q + (lane < NS ? lane : 0));
-  return __builtin_amdgcn_ballot_w64(g);
-}
-
-// The encoders' three output modes: compare (prerepairSanityCheck), Repair
-// fill (store missing shards, compare given ones) and plain store.
-template <int NS>
-__device__ __forceinline__ void enc16_store(const EncodeArgs& a, const W16n<NS>& w, int q, long sq, long vec, long sv,
-                                            uint32_t col, bool active, uint64_t given) {
-  if (!active) return;
-  const auto out_rsrc = make_rsrc(a.out + sq * a.out_sq_stride + vec * a.out_vec_stride);
-  const uint32_t os = (uint32_t)a.out_shard_stride;
-  if (a.mismatch) {  // prerepairSanityCheck: parity must equal Encode(data)
-    uint32_t diff = 0;
-#pragma unroll
-    for (int j = 0; j < NS; j++) {
-      const uint32_t so = (uint32_t)(NS * q + j) * os;
-      diff |= w.lo[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, col, so, 0);
-      diff |= w.hi[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, col + 32u, so, 0);
-    }
-    if (diff) {
-      atomicOr(&a.mismatch[sq], a.mismatch_bit);
-      if (a.mismatch_vec) a.mismatch_vec[sq * a.nvec + vec] = 1;
-    }
-    return;
-  }
-  if (a.out_present) {  // Repair fill: store the missing shards of the out half, compare given ones
-    uint32_t diff = 0;
-#pragma unroll
-    for (int j = 0; j < NS; j++) {
-      const uint32_t so = (uint32_t)(NS * q + j) * os;
-      if ((given >> j) & 1) {  // wave-uniform
-        diff |= w.lo[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, col, so, 0);
-        diff |= w.hi[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, col + 32u, so, 0);
-      } else {
-        __builtin_amdgcn_raw_buffer_store_b32(w.lo[j], out_rsrc, col, so, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(w.hi[j], out_rsrc, col + 32u, so, 0);
-      }
-    }
-    if (diff) a.redo[sv] = 1;
-    return;
-  }
-#pragma unroll
-  for (int j = 0; j < NS; j++) {
-    const uint32_t so = (uint32_t)(NS * q + j) * os;
-    __builtin_amdgcn_raw_buffer_store_b32(w.lo[j], out_rsrc, col, so, 0);
-    __builtin_amdgcn_raw_buffer_store_b32(w.hi[j], out_rsrc, col + 32u, so, 0);
-  }
-}
-
-
-// REV: the reverse fill (EncodeArgs.reverse): skew offsets IO = 0 for the IFFT
-// and FO = M for the FFT instead of M and 0 (positions stay below kTabPos).
-// Occupancy: 2 waves per SIMD, the whole 256-VGPR budget.  At the 168 VGPRs of
-// 3 waves per SIMD the kernel kept 948 (M = 512) / 1032 (M = 256) B per lane in
-// scratch, at 256 544 / 576 B; an M = 512 workgroup fits once per CU either way,
-// and for M = 256 two spilling less beat three (profiles/gf16_encoder_occupancy_r03.log:
-// Q3 repair k = 512 +6 %, k = 256 +8.5 %; split square k = 512 +4.5 %, k = 256 +6 %).
-template <int M, bool REV>
-__global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(2, 8))) void
-leo16_encode_reg_kernel(EncodeArgs a) {
-  constexpr int IO = REV ? 0 : M, FO = REV ? M : 0;
-  constexpr int P = M / 64;
-  constexpr int S = P == 8 ? 1 : 2;
-  __shared__ uint32_t lds[P * P * S * 2 * 64];
-  const long blk = blockIdx.x;
-  const int chunk = (int)(blk % a.nchunk);
-  const long sv = blk / a.nchunk;
-  const long vec = sv % a.nvec;
-  const long sq = sv / a.nvec;
-  if (vec_skipped(a, sv)) return;  // uniform
-  const int lane = threadIdx.x & 63;
-  const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t col = (uint32_t)chunk * 512u + (uint32_t)(lane >> 3) * 64u + (uint32_t)(lane & 7) * 4u;
-  const bool active = col < (uint32_t)a.shard_bytes;
-  const uint32_t cl = active ? col : 0u;  // inactive lanes read valid memory, store nothing
-  W16 w;
-  enc16_load(a, w, q, sq, vec, col, cl, active);
-  const uint64_t given = enc16_given<64>(a, q, sq, vec, lane);
-  // ---- IFFT (ifftDITEncoder, skew index IO - 1 + iend) ----
-  ifft16_block<1>(w, IO - 1 + 64 * q);  // bits 0-5
-  xpose16<P, S>(w, lds, q, lane);
-  if constexpr (M == 512) {  // slot 8h + b: h = bits 6-8, b = bits 0-2
-#pragma unroll
-    for (int hr = 0; hr < 8; hr += 4) {  // radix-4 dist 64 (bits 6, 7), groups r = 64 hr
-      const int p01 = IO - 1 + 64 * hr + 64, p02 = p01 + 64, p23 = p01 + 128;
-#pragma unroll
-      for (int b = 0; b < 8; b++) {
-        const int s0 = hr * 8 + b;
-        ifft2_16(w, s0, s0 + 8, p01);
-        ifft2_16(w, s0 + 16, s0 + 24, p23);
-        ifft2_16(w, s0, s0 + 16, p02);
-        ifft2_16(w, s0 + 8, s0 + 24, p02);
-      }
-    }
-    // last IFFT layer (dist 256, skew IO - 1 + 256) merged with the first FFT
-    // layer (dist 256, skew FO + 255)
-#pragma unroll
-    for (int s0 = 0; s0 < 32; s0++) ifft_fft2_16(w, s0, s0 + 32, MERGED_TAB(1));
-    // ---- FFT (fftDIT, skew index FO + iend - 1), dist4 = 512: its dist 128 layer (bit 7) ----
-#pragma unroll
-    for (int s0 = 0; s0 < 16; s0++) {
-      fft2_16(w, s0, s0 + 16, FO + 127);
-      fft2_16(w, s0 + 32, s0 + 48, FO + 383);
-    }
-#pragma unroll
-    for (int g2 = 0; g2 < 4; g2++)  // dist4 = 128 step, first sub-layer (bit 6)
-#pragma unroll
-      for (int b = 0; b < 8; b++) fft2_16(w, 16 * g2 + b, 16 * g2 + b + 8, FO + 128 * g2 + 63);
-    xpose16<P, S>(w, lds, q, lane);
-#pragma unroll
-    for (int j = 0; j < 32; j++) fft2_16(w, j, j + 32, FO + 64 * q + 31);  // its second sub-layer (bit 5)
-    fft16_block<8>(w, FO + 64 * q);                                         // bits 4 .. 0
-  } else {  // M == 256: slot 16a + b: a = bits 6-7, b = bits 0-3
-    constexpr int p01 = IO - 1 + 64, p02 = p01 + 64, p23 = p01 + 128;
-    static_assert(p02 == IO + 127, "merged table: positions IO + 127 and FO + 127");
-#pragma unroll
-    for (int b = 0; b < 16; b++) {  // radix-4 dist 64 (bits 6, 7); its dist 128 layer merged with the FFT's
-      ifft2_16(w, b, 16 + b, p01);
-      ifft2_16(w, 32 + b, 48 + b, p23);
-      ifft_fft2_16(w, b, 32 + b, MERGED_TAB(0));
-      ifft_fft2_16(w, 16 + b, 48 + b, MERGED_TAB(0));
-    }
-#pragma unroll
-    for (int b = 0; b < 16; b++) {  // FFT dist4 = 256: its dist 64 layer (bit 6)
-      fft2_16(w, b, 16 + b, FO + 63);
-      fft2_16(w, 32 + b, 48 + b, FO + 191);
-    }
-    xpose16<P, S>(w, lds, q, lane);
-    fft16_block<16>(w, FO + 64 * q);  // bits 5 .. 0
-  }
-  enc16_store(a, w, q, sq, vec, sv, col, active, given);
-}
-
-// 32 elements per wave: M = 512 over 16 waves (1,024 threads), M = 256 over 8
-// (512 threads); 64 data VGPRs per lane within the 128 of 4 waves per SIMD,
-// against 64 elements per wave at 2 waves per SIMD in leo16_encode_reg_kernel
-// (M = 256 then also fits two workgroups per CU).  Block layout: wave q holds
-// elements 32 q + j (bits 0-4).  After the P x P transpose, M = 512: wave c
-// holds the elements with bits 1-4 = c in slots 2 h + b (h = bits 5-8, b = bit
-// 0); M = 256: bits 2-4 = c, slots 4 h + l (h = bits 5-7, l = bits 0-1).
-template <int M>
-constexpr int enc32_lds_bytes() {
-  return M == 512 ? 16 * 16 * 2 * 64 * 4 : 8 * 8 * 2 * 2 * 64 * 4;  // S = 1 / 2 group-slots per round
-}
-template <int M, bool REV>
-__global__ __launch_bounds__(M * 2) void leo16_encode_reg32_kernel(EncodeArgs a) {
-  constexpr int IO = REV ? 0 : M, FO = REV ? M : 0;
-  constexpr int NS = 32, P = M / NS, S = M == 512 ? 1 : 2;
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
-  const long blk = blockIdx.x;
-  const int chunk = (int)(blk % a.nchunk);
-  const long sv = blk / a.nchunk;
-  const long vec = sv % a.nvec;
-  const long sq = sv / a.nvec;
-  if (vec_skipped(a, sv)) return;  // uniform
-  const int lane = threadIdx.x & 63;
-  const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t col = (uint32_t)chunk * 512u + (uint32_t)(lane >> 3) * 64u + (uint32_t)(lane & 7) * 4u;
-  const bool active = col < (uint32_t)a.shard_bytes;
-  const uint32_t cl = active ? col : 0u;
-  W16n<NS> w;
-  enc16_load(a, w, q, sq, vec, col, cl, active);
-  const uint64_t given = enc16_given<NS>(a, q, sq, vec, lane);
-  // ---- IFFT (ifftDITEncoder, skew index IO - 1 + iend) ----
-  ifft16_block<1, NS>(w, IO - 1 + NS * q);  // bits 0-3
-#pragma unroll
-  for (int i = 0; i < 16; i++) ifft2_16(w, i, i + 16, IO - 1 + NS * q + 16);  // bit 4
-  __builtin_amdgcn_sched_barrier(0);
-  xpose16<P, S, NS>(w, lds32, q, lane);
-  if constexpr (M == 512) {
-#pragma unroll
-    for (int hh = 0; hh < 4; hh++) {  // radix-4 bits 5, 6 (slot dist 2, 4), 128-blocks r = 128 hh
-      const int p01 = IO - 1 + 128 * hh + 32, p02 = p01 + 32, p23 = p01 + 64;
-#pragma unroll
-      for (int b = 0; b < 2; b++) {
-        const int s0 = 8 * hh + b;
-        ifft2_16(w, s0, s0 + 2, p01);
-        ifft2_16(w, s0 + 4, s0 + 6, p23);
-        ifft2_16(w, s0, s0 + 4, p02);
-        ifft2_16(w, s0 + 2, s0 + 6, p02);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // radix-4 bits 7, 8 (slot dist 8, 16); its bit-8 layer (the last IFFT
-    // layer) merged with the first FFT layer (dist 256)
-#pragma unroll
-    for (int s0 = 0; s0 < 8; s0++) {
-      ifft2_16(w, s0, s0 + 8, IO - 1 + 128);
-      ifft2_16(w, s0 + 16, s0 + 24, IO - 1 + 384);
-      ifft_fft2_16(w, s0, s0 + 16, MERGED_TAB(1));
-      ifft_fft2_16(w, s0 + 8, s0 + 24, MERGED_TAB(1));
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // ---- FFT (fftDIT, skew index FO + iend - 1) ----
-#pragma unroll
-    for (int s0 = 0; s0 < 8; s0++) {  // bit 7 (dist 128, slot dist 8)
-      fft2_16(w, s0, s0 + 8, FO + 127);
-      fft2_16(w, s0 + 16, s0 + 24, FO + 383);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int hh = 0; hh < 4; hh++) {  // radix-4 dist4 = 128 (bits 6, 5), 128-blocks r = 128 hh
-      const int p01 = FO + 128 * hh + 31, p02 = p01 + 32, p23 = p01 + 64;
-#pragma unroll
-      for (int b = 0; b < 2; b++) {
-        const int s0 = 8 * hh + b;
-        fft2_16(w, s0, s0 + 4, p02);
-        fft2_16(w, s0 + 2, s0 + 6, p02);
-        fft2_16(w, s0, s0 + 2, p01);
-        fft2_16(w, s0 + 4, s0 + 6, p23);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  } else {
-#pragma unroll
-    for (int hh = 0; hh < 2; hh++) {  // radix-4 bits 5, 6 (slot dist 4, 8), 128-blocks r = 128 hh
-      const int p01 = IO - 1 + 128 * hh + 32, p02 = p01 + 32, p23 = p01 + 64;
-#pragma unroll
-      for (int l = 0; l < 4; l++) {
-        const int s0 = 16 * hh + l;
-        ifft2_16(w, s0, s0 + 4, p01);
-        ifft2_16(w, s0 + 8, s0 + 12, p23);
-        ifft2_16(w, s0, s0 + 8, p02);
-        ifft2_16(w, s0 + 4, s0 + 12, p02);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // bit 7 (slot dist 16): the last IFFT layer merged with the first FFT layer (dist 128)
-#pragma unroll
-    for (int s0 = 0; s0 < 16; s0++) ifft_fft2_16(w, s0, s0 + 16, MERGED_TAB(0));
-    __builtin_amdgcn_sched_barrier(0);
-    // ---- FFT (fftDIT, skew index FO + iend - 1): radix-4 dist4 = 128 (bits 6, 5) ----
-#pragma unroll
-    for (int hh = 0; hh < 2; hh++) {
-      const int p01 = FO + 128 * hh + 31, p02 = p01 + 32, p23 = p01 + 64;
-#pragma unroll
-      for (int l = 0; l < 4; l++) {
-        const int s0 = 16 * hh + l;
-        fft2_16(w, s0, s0 + 8, p02);
-        fft2_16(w, s0 + 4, s0 + 12, p02);
-        fft2_16(w, s0, s0 + 4, p01);
-        fft2_16(w, s0 + 8, s0 + 12, p23);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  xpose16<P, S, NS>(w, lds32, q, lane);
-  fft16_block<8, NS>(w, FO + NS * q);  // bits 4 .. 0
-  enc16_store(a, w, q, sq, vec, sv, col, active, given);
-}
-
-// ---------------------------------------------------------------------------
-// Register-resident GF(2^16) decode for k = 256 (n = 2k = 512 work elements):
-// the encoder's M = 512 structure (8 waves x 64 elements, one 512-B chunk of
-// one vector, block / transposed layouts, P x P LDS transpose) with the
-// decoder's steps (leopard.go reconstruct, as leo16_decode_kernel above):
-//   work = shard * errLocs (0 where missing) -> ifftDITDecoder (skew index
-//   iend - 1) -> formal derivative -> fftDIT -> erased shards = work *
-//   (65535 - errLocs).
-// Runtime multiplies (errLocs are per element) use 16-dword product tables that
-// the workgroup builds in LDS, one element per thread (mul16_table_to), and
-// every lane of a wave reads for its elements (mul16_table_from).
-// The formal derivative D(x)_e = x_e ^ XOR_{s: bit s of e == 0} x_{e | 2^s}
-// runs in the transposed layout (element bits 3-5 = wave): slot bits are
-// applied in place in ascending slot order (a read of slot e | 2^t > e sees
-// an original value), the wave bits from the partner waves' originals, which
-// are staged through LDS 16 slots at a time.
-// ---------------------------------------------------------------------------
-constexpr int kDecN = 512;
-
-// (xlo, xhi) = (xlo, xhi) * exp(lm) with its 16-dword product table (mul16_table_to)
-__device__ __forceinline__ void mul16_by(uint32_t& xlo, uint32_t& xhi, const uint32_t (&t)[16]) {
-  uint32_t pl[8], ph[8];
-#pragma unroll
-  for (int g = 0; g < 4; g++) {
-    const uint32_t sl = (xlo >> (2 * g)) & 0x03030303u;
-    const uint32_t sh = (xhi >> (2 * g)) & 0x03030303u;
-    pl[g] = __builtin_amdgcn_perm(t[g], t[g], sl);
-    ph[g] = __builtin_amdgcn_perm(t[8 + g], t[8 + g], sl);
-    pl[4 + g] = __builtin_amdgcn_perm(t[4 + g], t[4 + g], sh);
-    ph[4 + g] = __builtin_amdgcn_perm(t[12 + g], t[12 + g], sh);
-  }
-  xlo = xor3(xor3(xor3(pl[0], pl[1], pl[2]), pl[3], pl[4]), xor3(pl[5], pl[6], pl[7]), 0u);
-  xhi = xor3(xor3(xor3(ph[0], ph[1], ph[2]), ph[3], ph[4]), xor3(ph[5], ph[6], ph[7]), 0u);
-}
-
-// The decoders' per-element tables are built in LDS, one element per thread
-// with all its gathers in flight at once (round 3; rounds 1-2 built them per
-// wave -- one exp() gather per lane, 4 DPP ORs and 16 v_readlane per element --
-// and the k = 512 decoder waited on memory half of its cycles).
-// out[G] byte e2 = low byte of (e2 << 2G) * exp(lm), out[8 + G] its high byte.
-// zero: the all-zero table (multiply by 0: the decoders' premultiply of a
-// missing shard, whose bytes are then never selected out of the loaded word)
-// Round 4: only the 16 products (1 << b) * exp(lm) are gathered (the e2 = 3
-// entry of a group is the XOR of its e2 = 1 and e2 = 2 entries, the multiply
-// being GF(2)-linear), their logs come from g_logbit16 (scalar loads), and a
-// zero table gathers nothing: the workgroup's table phase was bound by its
-// random 2-B gathers (tools/phase_probe.py dec512: 22 % of the k = 512 decoder).
-__constant__ uint16_t g_logbit16[16];  // log of the element 1 << b
-__device__ __forceinline__ void mul16_table_to(uint32_t* out, uint32_t lm, bool zero = false) {
-  uint32_t pb[16];
-  if (!zero) {
-#pragma unroll
-    for (int b = 0; b < 16; b++) {
-      uint32_t sidx = (uint32_t)g_logbit16[b] + lm;
-      sidx = (sidx + (sidx >> 16)) & 0xFFFFu;
-      pb[b] = g_exp16[sidx];
-    }
-  } else {
-#pragma unroll
-    for (int b = 0; b < 16; b++) pb[b] = 0u;
-  }
-  uint32_t lo[8], hi[8];
-#pragma unroll
-  for (int G = 0; G < 8; G++) {
-    const uint32_t p1 = pb[2 * G], p2 = pb[2 * G + 1], p3 = p1 ^ p2;
-    lo[G] = ((p1 & 0xFFu) << 8) | ((p2 & 0xFFu) << 16) | ((p3 & 0xFFu) << 24);
-    hi[G] = ((p1 >> 8) << 8) | ((p2 >> 8) << 16) | ((p3 >> 8) << 24);
-  }
-  uint4* o = (uint4*)out;
-  o[0] = make_uint4(lo[0], lo[1], lo[2], lo[3]);
-  o[1] = make_uint4(lo[4], lo[5], lo[6], lo[7]);
-  o[2] = make_uint4(hi[0], hi[1], hi[2], hi[3]);
-  o[3] = make_uint4(hi[4], hi[5], hi[6], hi[7]);
-}
-// the table of element e from LDS (every lane of the wave reads the same 64 B)
-__device__ __forceinline__ void mul16_table_from(const uint32_t* tab, int e, uint32_t (&t)[16]) {
-  const uint4* q = (const uint4*)(tab + e * 16);
-#pragma unroll
-  for (int h = 0; h < 4; h++) {
-    const uint4 v = q[h];
-    t[4 * h] = v.x;
-    t[4 * h + 1] = v.y;
-    t[4 * h + 2] = v.z;
-    t[4 * h + 3] = v.w;
-  }
-}
-
-// Formal derivative in the transposed layout (wave c: element bits 3-5 = c,
-// slot 8h + b: h = element bits 6-8, b = bits 0-2).
-__device__ __forceinline__ void derivative16_xposed(W16& w, uint32_t* lds, int c, int lane) {
-  constexpr int B = 16;  // slots per LDS round; lds[(wave * B + u) * 2 + lohi][64]
-#pragma unroll
-  for (int s0 = 0; s0 < 64; s0 += B) {
-#pragma unroll
-    for (int u = 0; u < B; u++) {
-      lds[((c * B + u) * 2) * 64 + lane] = w.lo[s0 + u];
-      lds[((c * B + u) * 2 + 1) * 64 + lane] = w.hi[s0 + u];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < B; u++) {
-      const int sl = s0 + u;
-      uint32_t alo = w.lo[sl], ahi = w.hi[sl];
-#pragma unroll
-      for (int bit = 1; bit < 64; bit <<= 1)  // slot bits (element bits 0-2, 6-8)
-        if ((sl & bit) == 0) {
-          alo ^= w.lo[sl | bit];
-          ahi ^= w.hi[sl | bit];
-        }
-#pragma unroll
-      for (int wb = 1; wb < 8; wb <<= 1)  // wave bits (element bits 3-5): partners' originals
-        if ((c & wb) == 0) {
-          alo ^= lds[(((c | wb) * B + u) * 2) * 64 + lane];
-          ahi ^= lds[(((c | wb) * B + u) * 2 + 1) * 64 + lane];
-        }
-      w.lo[sl] = alo;
-      w.hi[sl] = ahi;
-    }
-    __syncthreads();
-  }
-}
-
-__global__ __launch_bounds__(kDecN) __attribute__((amdgpu_waves_per_eu(2, 2))) void leo16_decode_reg_kernel(
-    DecodeArgs a) {
-  constexpr int M = kDecN, P = 8, S = 1, K = M / 2;
-  // dynamic LDS (kDecLds): derivative staging (64 KiB) >= transpose (32 KiB),
-  // then the erased elements' product tables (32 KiB), built up front
-  extern __shared__ __attribute__((aligned(16))) uint32_t dyn_lds[];
-  uint32_t* lds = dyn_lds;
-  uint32_t* post_tab = dyn_lds + P * 16 * 2 * 64;
-  const long blk = blockIdx.x;
-  const int chunk = (int)(blk % a.nchunk);
-  const long v = blk / a.nchunk;
-  if (a.flags[v] == 0) return;  // uniform: vector not decodable / complete this pass
-  const long sq = v / a.nvec, vec = v % a.nvec;
-  const int lane = threadIdx.x & 63;
-  const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t col = (uint32_t)chunk * 512u + (uint32_t)(lane >> 3) * 64u + (uint32_t)(lane & 7) * 4u;
-  const bool active = col < (uint32_t)a.shard_bytes;
-  const uint32_t cl = active ? col : 0u;
-  const auto rsrc = make_rsrc(a.data + sq * a.sq_stride + vec * a.vec_stride);
-  const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
-  const uint16_t* err = (const uint16_t*)(a.err + err_vec(a, v) * rs_err_bytes(K));
-  // work element i = 64 q + j: layout [parity k][data k]
-  const int my_i = 64 * q + lane;
-  const int my_shard = my_i < K ? K + my_i : my_i - K;
-  const uint64_t pm = __builtin_amdgcn_ballot_w64(pres[(long)my_shard * a.p_shard_stride] != 0);
-  const uint32_t my_err = err[my_i];
-  W16 w;
-#pragma unroll
-  for (int j = 0; j < 64; j++) {
-    const int i = 64 * q + j;
-    const int shard = i < K ? K + i : i - K;
-    const uint32_t so = (uint32_t)shard * (uint32_t)a.shard_stride;
-    const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(rsrc, cl, so, 0);
-    const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rsrc, cl + 32u, so, 0);
-    w.lo[j] = lo;  // a missing shard's bytes: zeroed by its premultiply table
-    w.hi[j] = hi;
-  }
-  // work *= errLocs: thread i builds element i's tables in LDS (the premultiply
-  // one in the transpose buffer, free until the first transpose; the erasure
-  // one kept to the end), each wave then reads its 64 elements' tables
-  // (gathers before the loads, as the k = 512 decoder does, measured -0.8 %)
-  mul16_table_to(lds + threadIdx.x * 16, my_err, !((pm >> lane) & 1));
-  mul16_table_to(post_tab + threadIdx.x * 16, kMod16 - my_err, (pm >> lane) & 1);  // read for missing shards only
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < 64; j++) {
-    uint32_t t[16];
-    mul16_table_from(lds, 64 * q + j, t);
-    uint32_t xl = w.lo[j], xh = w.hi[j];
-    mul16_by(xl, xh, t);
-    w.lo[j] = xl;
-    w.hi[j] = xh;
-    __builtin_amdgcn_sched_barrier(0);  // one element's table live at a time
-  }
-  __syncthreads();  // the transpose reuses lds
-  // ---- IFFT (ifftDITDecoder, skew index iend - 1) ----
-  ifft16_block<1>(w, -1 + 64 * q);  // bits 0-5
-  xpose16<P, S>(w, lds, q, lane);
-#pragma unroll
-  for (int hr = 0; hr < 8; hr += 4) {  // radix-4 dist 64 (bits 6, 7)
-    const int p01 = 64 * hr + 63, p02 = p01 + 64, p23 = p01 + 128;
-#pragma unroll
-    for (int b = 0; b < 8; b++) {
-      const int s0 = hr * 8 + b;
-      ifft2_16(w, s0, s0 + 8, p01);
-      ifft2_16(w, s0 + 16, s0 + 24, p23);
-      ifft2_16(w, s0, s0 + 16, p02);
-      ifft2_16(w, s0 + 8, s0 + 24, p02);
-    }
-  }
-#pragma unroll
-  for (int s0 = 0; s0 < 32; s0++) ifft2_16(w, s0, s0 + 32, 255);  // last layer, dist 256
-  derivative16_xposed(w, lds, q, lane);
-  // ---- FFT (fftDIT, skew index iend - 1), as the M = 512 encoder ----
-#pragma unroll
-  for (int s0 = 0; s0 < 16; s0++) {  // dist4 = 512, dist = 128 (bits 8, 7)
-    fft2_16(w, s0, s0 + 32, 255);
-    fft2_16(w, s0 + 16, s0 + 48, 255);
-    fft2_16(w, s0, s0 + 16, 127);
-    fft2_16(w, s0 + 32, s0 + 48, 383);
-  }
-#pragma unroll
-  for (int g2 = 0; g2 < 4; g2++)  // dist4 = 128 step, first sub-layer (bit 6)
-#pragma unroll
-    for (int b = 0; b < 8; b++) fft2_16(w, 16 * g2 + b, 16 * g2 + b + 8, 128 * g2 + 63);
-  xpose16<P, S>(w, lds, q, lane);
-#pragma unroll
-  for (int j = 0; j < 32; j++) fft2_16(w, j, j + 32, 64 * q + 31);  // second sub-layer (bit 5)
-  fft16_block<8>(w, 64 * q);                                         // bits 4 .. 0
-  // erased shards = work * (65535 - errLocs); only active lanes store.  pm and
-  // q made opaque here: otherwise the 64 per-element conditions and offsets
-  // of the load loop are kept live through the whole kernel (SGPR spills)
-  uint64_t pm_e = pm;
-  int q_e = q;
-  asm volatile("" : "+s"(pm_e), "+s"(q_e));
-#pragma unroll
-  for (int j = 0; j < 64; j++) {
-    if ((pm_e >> j) & 1) continue;  // uniform
-    const int i = 64 * q_e + j;
-    const int shard = i < K ? K + i : i - K;
-    uint32_t t[16];
-    mul16_table_from(post_tab, i, t);
-    uint32_t xl = w.lo[j], xh = w.hi[j];
-    mul16_by(xl, xh, t);
-    const uint32_t so = (uint32_t)shard * (uint32_t)a.shard_stride;
-    if (active) {
-      __builtin_amdgcn_raw_buffer_store_b32(xl, rsrc, col, so, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(xh, rsrc, col + 32u, so, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
-
-// ---------------------------------------------------------------------------
-// Register-resident GF(2^16) decode for k = 512 (n = 2k = 1024 work elements).
-// 1024 elements do not fit 16 waves at 2 VGPRs per element (4 symbols per
-// lane, the k = 256 layout), so here a lane holds 2 symbols in ONE dword,
-// packed [lo(2s) lo(2s+1) hi(2s) hi(2s+1)]: a wave covers 256 B of a shard
-// (lane l: 64-B block l >> 4, symbol pair l & 15), a 1024-thread workgroup of
-// 16 waves x 64 elements (64 data VGPRs) one 256-B half of a 512-B chunk.
-// Steps as leo16_decode_reg_kernel; layouts: block (wave q holds 64 q + j) and
-// transposed through LDS (wave c = element bits 2-5, slot (h << 2) | l, h =
-// bits 6-9, l = bits 0-1); n = 2^10 is radix-4 all the way (dist 1, 4, 16 in
-// block layout, 64 and 256 transposed).  A packed multiply is 8 v_perm (one per
-// 2-bit group of the symbol, selecting the low- and high-byte products of both
-// symbols at once) over the same 16-dword product tables.
-// ---------------------------------------------------------------------------
-constexpr int kDec1k = 1024;
-
-// y * c for a packed dword, t = c's 16-dword product table (t[G] low bytes,
-// t[8 + G] high bytes of (e2 << 2G) * c, e2 = 0..3).  One selector serves two
-// bit groups: (y >> 2G) & 0x03030303 holds group G of both symbols' low bytes
-// (bytes 0, 1) and group G + 4 of their high bytes (bytes 2, 3); with 4 added
-// to bytes 2, 3 they index src0, so perm(t[G + 4], t[G], sel) looks up group G
-// of the two symbols in t[G] and group G + 4 in t[G + 4] at once.  Summed over
-// G = 0..3, bytes 0, 1 hold the low-byte products of the low groups and bytes
-// 2, 3 those of the high groups (the same for the high-byte tables); two byte
-// permutes fold the halves: 22 ops per 2 symbols (36 with one group per perm).
-__device__ __forceinline__ uint32_t mulp_sel(uint32_t y, int G) {
-  return __builtin_amdgcn_bitop3_b32(y >> (2 * G), 0x03030303u, 0x04040000u, 0xEA);  // (a & b) | c
-}
-// acc ^ y * c; T: anything indexable by 0..15 (the table of c)
-template <class T>
-__device__ __forceinline__ uint32_t mulp_add_t(uint32_t acc, uint32_t y, const T& t) {
-  const uint32_t s0 = mulp_sel(y, 0), s1 = mulp_sel(y, 1), s2 = mulp_sel(y, 2), s3 = mulp_sel(y, 3);
-  const uint32_t a = xor3(xor3(__builtin_amdgcn_perm(t[4], t[0], s0), __builtin_amdgcn_perm(t[5], t[1], s1),
-                               __builtin_amdgcn_perm(t[6], t[2], s2)),
-                          __builtin_amdgcn_perm(t[7], t[3], s3), 0u);
-  const uint32_t b = xor3(xor3(__builtin_amdgcn_perm(t[12], t[8], s0), __builtin_amdgcn_perm(t[13], t[9], s1),
-                               __builtin_amdgcn_perm(t[14], t[10], s2)),
-                          __builtin_amdgcn_perm(t[15], t[11], s3), 0u);
-  // acc ^ [a0 ^ a2, a1 ^ a3, b0 ^ b2, b1 ^ b3]
-  return xor3(acc, __builtin_amdgcn_perm(b, a, 0x05040100u), __builtin_amdgcn_perm(b, a, 0x07060302u));
-}
-__device__ __forceinline__ uint32_t mulp(uint32_t y, const uint32_t (&t)[16]) { return mulp_add_t(0u, y, t); }
-
-// A skew position's table for the packed multiplies, loaded per radix-4 unit:
-// the position is made opaque so that each unit loads its tables afresh
-// (scalar-cache hits) instead of the compiler keeping every table of the
-// kernel live (1,100 SGPR spills through v_writelane / v_readlane).
-struct PTab {
-  uint32_t s[16];
-  __device__ __forceinline__ uint32_t operator[](int i) const { return s[i]; }
-};
-__device__ __forceinline__ PTab ptab(int pos) {
-  const uint4* t = (const uint4*)(g_ptab16 + pos * 16);
-  PTab p;
-#pragma unroll
-  for (int h = 0; h < 4; h++) {
-    const uint4 x = t[h];
-    p.s[4 * h] = x.x;
-    p.s[4 * h + 1] = x.y;
-    p.s[4 * h + 2] = x.z;
-    p.s[4 * h + 3] = x.w;
-  }
-  return p;
-}
-
-// tok: a value written by the previous radix-4 unit's last phase.  A unit's
-// table positions pass through an asm that reads a value written just before
-// (tok for its first table, its own first phase's output for the next), so no
-// scalar table load can be hoisted above that point and at most two tables are
-// live: without the tokens every unit's tables of a step were loaded up front
-// and spilled to VGPR lanes (848 v_writelane + 848 v_readlane, 22,320 -> 20,624
-// static VALU; repair k = 512 +1.8 %, profiles/gf16_dec512_tok_r04.log).
-struct W1k {
-  uint32_t v[64];
-  uint32_t tok;
-};
+// tok: a value written by the previous phase.  A table position passes through
+// an asm that reads it, so no scalar table load is hoisted above that point and
+// the tables of a layer are not all live at once (round 4: 848 v_writelane +
+// 848 v_readlane spills without it, profiles/gf16_dec512_tok_r04.log).
 __device__ __forceinline__ int opaque_tok(int x, uint32_t tok) {
   asm volatile("" : "+s"(x) : "v"(tok));
   return x;
 }
 
-// ifftDIT2: y ^= x; x ^= y * skew[pos]     fftDIT2: x ^= y * skew[pos]; y ^= x
-__device__ __forceinline__ void ifft2_p(W1k& w, int i, int j, const PTab& t) {
-  w.v[j] ^= w.v[i];
-  w.v[i] = mulp_add_t(w.v[i], w.v[j], t);
-}
-__device__ __forceinline__ void fft2_p(W1k& w, int i, int j, const PTab& t) {
-  w.v[i] = mulp_add_t(w.v[i], w.v[j], t);
-  w.v[j] ^= w.v[i];
-}
-
-// Radix-4 steps layer by layer: every butterfly of one skew position, then
-// the next position; each phase's table is loaded during the phase before it.
-// IFFT: (i, i+D) at p01, (i+2D, i+3D) at p23, then (i, i+2D), (i+D, i+3D) at
-// p02; i over N butterflies starting at s0 with stride ST.
-template <int N, int ST, int D>
-__device__ __forceinline__ void ifftp_r4(W1k& w, int s0, int p01, int p02, int p23) {
-  const PTab t01 = ptab(opaque_tok(p01, w.tok));
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int u = 0; u < N; u++) ifft2_p(w, s0 + ST * u, s0 + ST * u + D, t01);
-  const PTab t23 = ptab(opaque_tok(p23, w.v[s0 + D]));
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int u = 0; u < N; u++) ifft2_p(w, s0 + ST * u + 2 * D, s0 + ST * u + 3 * D, t23);
-  const PTab t02 = ptab(opaque_tok(p02, w.v[s0 + 3 * D]));
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int u = 0; u < N; u++) {
-    ifft2_p(w, s0 + ST * u, s0 + ST * u + 2 * D, t02);
-    ifft2_p(w, s0 + ST * u + D, s0 + ST * u + 3 * D, t02);
-  }
-  w.tok = w.v[s0 + ST * (N - 1) + D];
-  __builtin_amdgcn_sched_barrier(0);
-}
-// FFT: (i, i+2D), (i+D, i+3D) at p02, then (i, i+D) at p01, (i+2D, i+3D) at p23
-template <int N, int ST, int D>
-__device__ __forceinline__ void fftp_r4(W1k& w, int s0, int p01, int p02, int p23) {
-  const PTab t02 = ptab(opaque_tok(p02, w.tok));
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int u = 0; u < N; u++) {
-    fft2_p(w, s0 + ST * u, s0 + ST * u + 2 * D, t02);
-    fft2_p(w, s0 + ST * u + D, s0 + ST * u + 3 * D, t02);
-  }
-  const PTab t01 = ptab(opaque_tok(p01, w.v[s0 + 2 * D]));
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int u = 0; u < N; u++) fft2_p(w, s0 + ST * u, s0 + ST * u + D, t01);
-  const PTab t23 = ptab(opaque_tok(p23, w.v[s0 + D]));
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int u = 0; u < N; u++) fft2_p(w, s0 + ST * u + 2 * D, s0 + ST * u + 3 * D, t23);
-  w.tok = w.v[s0 + ST * (N - 1) + 3 * D];
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-// block layout, decoder IFFT radix-4 steps dist D..16 (skew index iend - 1)
-template <int D>
-__device__ __forceinline__ void ifftp_block(W1k& w, int base) {
-#pragma unroll
-  for (int r = 0; r < 64; r += 4 * D) {
-    const int b = opaque_s(base);
-    ifftp_r4<D, 1, D>(w, r, b + r + D, b + r + 2 * D, b + r + 3 * D);
-  }
-  if constexpr (D * 16 <= 64) ifftp_block<D * 4>(w, base);
-}
-
-template <int DIST>
-__device__ __forceinline__ void fftp_block(W1k& w, int base) {
-#pragma unroll
-  for (int r = 0; r < 64; r += 4 * DIST) {
-    const int iend = r + DIST;
-    const int b = opaque_s(base);
-    fftp_r4<DIST, 1, DIST>(w, r, b + iend - 1, b + iend + DIST - 1, b + iend + 2 * DIST - 1);
-  }
-  if constexpr (DIST >= 4) fftp_block<DIST / 4>(w, base);
-}
-
-// 16 x 16 block transpose: element (wave Q, slot (c << 2) | l) <-> (wave c,
-// slot (Q << 2) | l); one slot l per LDS round (64 KiB).
-__device__ __forceinline__ void xposep(W1k& w, uint32_t* lds, int q, int lane) {
-#pragma unroll
-  for (int l = 0; l < 4; l++) {
-#pragma unroll
-    for (int c = 0; c < 16; c++) lds[(c * 16 + q) * 64 + lane] = w.v[(c << 2) | l];
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < 16; c++) w.v[(c << 2) | l] = lds[(q * 16 + c) * 64 + lane];
-    __syncthreads();
-  }
-  w.tok = w.v[63];
-}
-
-// formal derivative in the transposed layout (wave c = element bits 2-5; slot
-// bits = element bits 0-1 and 6-9), partner waves' originals through LDS
-__device__ __forceinline__ void derivativep(W1k& w, uint32_t* lds, int c, int lane) {
-  constexpr int B = 16;
-#pragma unroll
-  for (int s0 = 0; s0 < 64; s0 += B) {
-#pragma unroll
-    for (int u = 0; u < B; u++) lds[(c * B + u) * 64 + lane] = w.v[s0 + u];
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < B; u++) {
-      const int sl = s0 + u;
-      uint32_t acc = w.v[sl];
-#pragma unroll
-      for (int bit = 1; bit < 64; bit <<= 1)
-        if ((sl & bit) == 0) acc ^= w.v[sl | bit];
-#pragma unroll
-      for (int wb = 1; wb < 16; wb <<= 1)
-        if ((c & wb) == 0) acc ^= lds[((c | wb) * B + u) * 64 + lane];
-      w.v[sl] = acc;
-    }
-    __syncthreads();
-  }
-  w.tok = w.v[63];
-}
-
-// DAGPU_PHASE_PROBE builds (tools/phase_probe.py dec512, never the product
-// library): lane 0 of waves 0 and 15 stamp s_memtime at the decoder's phase
-// boundaries, [block][wave 0 / 15][phase].
+// DAGPU_PHASE_PROBE builds (tools/phase_probe.py, never the product library):
+// lane 0 of the first and last wave stamp s_memtime at the phase boundaries.
 #ifdef DAGPU_PHASE_PROBE
 constexpr int kProbePhases = 14;
 __device__ uint64_t g_probe[8192 * 2 * kProbePhases];
@@ -1385,132 +426,9 @@ __device__ uint64_t g_probe_e[8192 * 2 * kProbePhases];  // the half-lane encode
     if ((threadIdx.x & 63) == 0 && (q == 0 || q == (QL)) && blockIdx.x < 8192)                  \
       buf[(blockIdx.x * 2 + (q == (QL))) * kProbePhases + (i)] = __builtin_amdgcn_s_memtime();  \
   } while (0)
-#define DEC_PROBE(i)                                                                            \
-  do {                                                                                          \
-    if ((threadIdx.x & 63) == 0 && (q == 0 || q == 15) && blk < 8192)                           \
-      g_probe[(blk * 2 + (q == 15)) * kProbePhases + (i)] = __builtin_amdgcn_s_memtime();       \
-  } while (0)
 #else
-#define DEC_PROBE(i) ((void)0)
 #define H_PROBE(buf, i, QL) ((void)0)
 #endif
-
-__global__ __launch_bounds__(kDec1k) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_decode_reg1k_kernel(
-    DecodeArgs a) {
-  constexpr int K = kDec1k / 2;
-  // dynamic LDS (kDec1kLds): transpose rounds and derivative staging (64 KiB),
-  // then the erased elements' product tables (64 KiB), built up front
-  extern __shared__ __attribute__((aligned(16))) uint32_t dyn_lds[];
-  uint32_t* lds = dyn_lds;
-  uint32_t* post_tab = dyn_lds + 16 * 16 * 64;
-  const long blk = blockIdx.x;
-  const int half = (int)(blk % a.nchunk);  // nchunk = 256-B pieces of the shard
-  const long v = blk / a.nchunk;
-  if (a.flags[v] == 0) return;  // uniform
-  const long sq = v / a.nvec, vec = v % a.nvec;
-  const int lane = threadIdx.x & 63;
-  const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  DEC_PROBE(0);
-  // lane: 64-B block (lane >> 4) of this 256-B piece, symbols 2 (lane & 15) and +1
-  // (memory: lane pair 2m, 2m+1 moves the dword of low bytes and the dword of
-  // high bytes of symbols 4m .. 4m+3, even lane the low one)
-  const bool odd = lane & 1;
-  const uint32_t wcol = (uint32_t)half * 256u + (uint32_t)(lane >> 4) * 64u + (uint32_t)(lane & 14) * 2u + (odd ? 32u : 0u);
-  const auto rsrc = make_rsrc(a.data + sq * a.sq_stride + vec * a.vec_stride);
-  const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
-  const uint16_t* err = (const uint16_t*)(a.err + err_vec(a, v) * rs_err_bytes(K));
-  const int my_i = 64 * q + lane;
-  const int my_shard = my_i < K ? K + my_i : my_i - K;
-  const uint64_t pm = __builtin_amdgcn_ballot_w64(pres[(long)my_shard * a.p_shard_stride] != 0);
-  const uint32_t my_err = err[my_i];
-  // work *= errLocs: thread i builds element i's tables in LDS (the premultiply
-  // one in the transpose buffer, free until the first transpose; the erasure
-  // one kept to the end), each wave then reads its 64 elements' tables.  The
-  // tables' gathers go out before the data loads, so the barrier below waits
-  // for them only and each element's premultiply for its own load.
-  mul16_table_to(lds + threadIdx.x * 16, my_err, !((pm >> lane) & 1));
-  mul16_table_to(post_tab + threadIdx.x * 16, kMod16 - my_err, (pm >> lane) & 1);  // read for missing shards only
-  W1k w;
-  const int q_ld = opaque_s(q);
-#pragma unroll
-  for (int j = 0; j < 64; j++) {
-    const int i = 64 * q_ld + j;
-    const int shard = i < K ? K + i : i - K;
-    const uint32_t so = (uint32_t)shard * (uint32_t)a.shard_stride;
-    // one dword per lane (even lanes the low bytes, odd lanes the high bytes
-    // of symbols 4m .. 4m+3), paired with the neighbour lane's dword:
-    // one VGPR per element in flight (two 16-bit loads per element kept two
-    // and spilled the load loop, serialising its loads)
-    w.v[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, wcol, so, 0);  // paired below
-  }
-  __syncthreads();
-  DEC_PROBE(1);
-  const int q_pm = opaque_s(q);
-#pragma unroll
-  for (int j = 0; j < 64; j++) {
-    uint32_t t[16];
-    mul16_table_from(lds, 64 * q_pm + j, t);
-    const uint32_t mine = w.v[j];
-    const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mine, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-    w.v[j] = mulp(odd ? __builtin_amdgcn_perm(mine, other, 0x07060302u) : __builtin_amdgcn_perm(other, mine, 0x05040100u), t);
-    __builtin_amdgcn_sched_barrier(0);  // one element's table live at a time
-  }
-  w.tok = w.v[63];
-  __syncthreads();  // the transpose reuses lds
-  DEC_PROBE(2);
-  // ---- IFFT (ifftDITDecoder, skew index iend - 1) ----
-  ifftp_block<1>(w, -1 + 64 * q);  // bits 0-5
-  DEC_PROBE(3);
-  xposep(w, lds, q, lane);
-  DEC_PROBE(4);
-#pragma unroll
-  for (int hr = 0; hr < 4; hr++) {  // radix-4 dist 64 (bits 6, 7), r = 256 hr: slots 16 hr + b, b < 4
-    const int p01 = opaque_s(256 * hr + 63);
-    ifftp_r4<4, 1, 4>(w, 16 * hr, p01, p01 + 64, p01 + 128);
-  }
-  {  // radix-4 dist 256 (bits 8, 9): slots s0 < 16
-    const int p01 = opaque_s(255);
-    ifftp_r4<16, 1, 16>(w, 0, p01, p01 + 256, p01 + 512);
-  }
-  DEC_PROBE(5);
-  derivativep(w, lds, q, lane);
-  DEC_PROBE(6);
-  // ---- FFT (fftDIT, skew index iend - 1) ----
-  {  // dist 256
-    const int p01 = opaque_s(255);
-    fftp_r4<16, 1, 16>(w, 0, p01, p01 + 256, p01 + 512);
-  }
-#pragma unroll
-  for (int hr = 0; hr < 4; hr++) {  // dist 64
-    const int p01 = opaque_s(256 * hr + 63);
-    fftp_r4<4, 1, 4>(w, 16 * hr, p01, p01 + 64, p01 + 128);
-  }
-  DEC_PROBE(7);
-  xposep(w, lds, q, lane);
-  DEC_PROBE(8);
-  fftp_block<16>(w, 64 * q);  // dist 16, 4, 1 (bits 5 .. 0)
-  DEC_PROBE(9);
-  // erased shards = work * (65535 - errLocs); pm, q opaque as in leo16_decode_reg_kernel
-  uint64_t pm_e = pm;
-  int q_e = q;
-  asm volatile("" : "+s"(pm_e), "+s"(q_e));
-#pragma unroll
-  for (int j = 0; j < 64; j++) {
-    if ((pm_e >> j) & 1) continue;  // uniform
-    const int i = 64 * q_e + j;
-    const int shard = i < K ? K + i : i - K;
-    uint32_t t[16];
-    mul16_table_from(post_tab, i, t);
-    const uint32_t r = mulp(w.v[j], t);
-    const uint32_t so = (uint32_t)shard * (uint32_t)a.shard_stride;
-    // back to [low bytes of 4m..4m+3] (even lane) / [high bytes] (odd lane)
-    const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0xB1, 0xF, 0xF, false);
-    const uint32_t out = odd ? __builtin_amdgcn_perm(r, other, 0x07060302u) : __builtin_amdgcn_perm(other, r, 0x05040100u);
-    __builtin_amdgcn_raw_buffer_store_b32(out, rsrc, wcol, so, 0);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  DEC_PROBE(10);
-}
 
 // ---------------------------------------------------------------------------
 // k = 512 / 256 decoder, round 5 (leo16_decode_h_kernel<K>): unpacked symbols with
@@ -1794,15 +712,14 @@ __device__ __forceinline__ void mul16x_by(uint32_t& xl, uint32_t& xh, const uint
 // LR = 2: 512 threads at <= 128 VGPRs and 64 KiB of LDS, two workgroups per CU).
 template <int K>
 constexpr size_t dec_h_lds_bytes() { return (size_t)(2 * K) * (16 + kTab16x) * sizeof(uint32_t); }
-// LD (load mode): 0 = every shard loaded; 1 (default) = a missing shard's load
-// gets an out-of-range voffset (the buffer returns 0 without touching memory),
-// halving a maximal-erasure vector's load traffic.  (8-byte lane-pair loads with
-// a DPP swap, half the vector-memory instructions, measured no faster:
+// A missing shard's load gets an out-of-range voffset (the buffer returns 0
+// without touching memory), halving a maximal-erasure vector's load traffic
+// (+0.4 %, profiles/gf16_skip_ab_r05.log).  (8-byte lane-pair loads with a DPP
+// swap, half the vector-memory instructions, measured no faster:
 // profiles/gf16_load64_ab_r05.log.)
-template <int K, int LD = 1>
+template <int K>
 __global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_decode_h_kernel(
     DecodeArgs a) {
-  constexpr bool SKIP = LD >= 1;
   constexpr int NQ = K / 32, LR = K == 512 ? 1 : 2, RPR = K == 512 ? 1 : 2;
   // dynamic LDS (dec_h_lds_bytes): [0, n x 64 B) the transposes and the
   // derivative staging (each <= n x 64 B); then n x 80 B of per-element tables
@@ -1843,7 +760,7 @@ __global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     const int shard = i < K ? K + i : i - K;
     const uint32_t so = (uint32_t)shard * (uint32_t)a.shard_stride;
     // missing: voffset >= 2^31 > num_records (soffset < 2^30 here), so out of range
-    const uint32_t vj = (!SKIP || ((pmh_ld >> s_local(j, 0)) & 1)) ? voff : (voff | 0x80000000u);
+    const uint32_t vj = ((pmh_ld >> s_local(j, 0)) & 1) ? voff : (voff | 0x80000000u);
     w.lo[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, vj, so, 0);
     w.hi[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, vj + 32u, so, 0);
   }
@@ -1855,11 +772,6 @@ __global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     uint32_t t[kTab16x];
     mul16x_table_from(tab, 64 * q_pm + s_local(j, 0) + 32 * hl, t);
     uint32_t xl = w.lo[j], xh = w.hi[j];
-    if constexpr (!SKIP) {  // a missing element's loaded bytes are not zero here
-      const bool p = (pmh_ld >> s_local(j, 0)) & 1;
-      xl = p ? xl : 0u;
-      xh = p ? xh : 0u;
-    }
     mul16x_by(xl, xh, t);
     asm volatile("" : "+v"(xl), "+v"(xh));  // one element's table live at a time
     w.lo[j] = xl;
@@ -2087,7 +999,6 @@ hipError_t ensure_tables() {
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_log16), t.log.data(), 65536 * 2)) != hipSuccess) return e;
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_exp16), t.exp.data(), 65536 * 2)) != hipSuccess) return e;
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_skew16), t.skew.data(), 65536 * 2)) != hipSuccess) return e;
-  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_walsh16), t.walsh.data(), 65536 * 2)) != hipSuccess) return e;
   {
     std::vector<uint16_t> wf(2 * 1024, 0);
     for (int f = 0; f < 2; f++) {
@@ -2100,48 +1011,10 @@ hipError_t ensure_tables() {
     }
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_wfold16), wf.data(), wf.size() * 2)) != hipSuccess) return e;
   }
-  {  // per skew position: products of every 2-bit group value with skew[pos]
-    std::vector<uint32_t> pt((size_t)kTabPos * 16, 0u);
-    for (int pos = 0; pos < kTabPos; pos++) {
-      const unsigned lm = t.skew[pos];
-      if (lm == kMod16) continue;  // leopard skips the multiply: zero table
-      for (int g = 0; g < 8; g++)
-        for (int e2 = 0; e2 < 4; e2++) {
-          const unsigned x = (unsigned)e2 << (2 * g);
-          unsigned prod = 0;
-          if (x) {
-            unsigned sidx = (unsigned)t.log[x] + lm;
-            sidx = (sidx + (sidx >> 16)) & 0xFFFFu;
-            prod = t.exp[sidx];
-          }
-          // g < 4: groups of the symbol's low byte -> t[g] (lo) / t[8+g] (hi)
-          // g >= 4: groups of the high byte        -> t[4+g-4] (lo) / t[12+g-4] (hi)
-          const int lo_idx = g < 4 ? g : 4 + (g - 4), hi_idx = 8 + lo_idx;
-          pt[(size_t)pos * 16 + lo_idx] |= (prod & 0xFFu) << (8 * e2);
-          pt[(size_t)pos * 16 + hi_idx] |= ((prod >> 8) & 0xFFu) << (8 * e2);
-        }
-    }
-    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_ptab16), pt.data(), pt.size() * 4)) != hipSuccess) return e;
+  {
     // merged encoder tables: the element exp(skew[p]) ^ exp(skew[q]) (skew kMod16 = element 0)
     auto elem = [&](int pos) -> unsigned { return t.skew[pos] == kMod16 ? 0u : (unsigned)t.exp[t.skew[pos]]; };
-    std::vector<uint32_t> mt(2 * 16, 0u);
     const int pairs[2][2] = {{383, 127}, {767, 255}};
-    for (int m = 0; m < 2; m++) {
-      const unsigned c = elem(pairs[m][0]) ^ elem(pairs[m][1]);
-      if (!c) continue;
-      const unsigned lc = t.log[c];
-      for (int g = 0; g < 8; g++)
-        for (int e2 = 1; e2 < 4; e2++) {
-          const unsigned x = (unsigned)e2 << (2 * g);
-          unsigned sidx = (unsigned)t.log[x] + lc;
-          sidx = (sidx + (sidx >> 16)) & 0xFFFFu;
-          const unsigned prod = t.exp[sidx];
-          const int lo_idx = g < 4 ? g : 4 + (g - 4), hi_idx = 8 + lo_idx;
-          mt[(size_t)m * 16 + lo_idx] |= (prod & 0xFFu) << (8 * e2);
-          mt[(size_t)m * 16 + hi_idx] |= ((prod >> 8) & 0xFFu) << (8 * e2);
-        }
-    }
-    if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_ptab16_merged), mt.data(), mt.size() * 4)) != hipSuccess) return e;
     // 3/3/2-split tables (mul16x_add_t): per skew position and for the two merged elements
     auto tab332 = [&](unsigned c, uint32_t* out) {  // c = field element (0: zero table)
       for (int i = 0; i < kTab16x; i++) out[i] = 0;
@@ -2172,21 +1045,16 @@ hipError_t ensure_tables() {
     for (int b = 0; b < 16; b++) lb[b] = (uint16_t)t.log[1u << b];
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_logbit16), lb, sizeof lb)) != hipSuccess) return e;
   }
-  // > 64 KiB of dynamic LDS (errlocs 128 KiB, k = 512 decode 128 KiB)
-  if ((e = hipFuncSetAttribute((const void*)leo16_errlocs_kernel,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, kErrLds)) != hipSuccess)
-    return e;
+  // > 64 KiB of dynamic LDS: the generic decoder (k = 512: 128 KiB) and the half-lane ones
   if ((e = hipFuncSetAttribute((const void*)leo16_decode_kernel,  // k <= 512 here (wider: rs_gf16_wide.hip)
                                hipFuncAttributeMaxDynamicSharedMemorySize, 512 * 256)) != hipSuccess)
     return e;
-  {
-    const void* f[4] = {(const void*)leo16_encode_reg32_kernel<512, false>, (const void*)leo16_encode_reg32_kernel<512, true>,
-                        (const void*)leo16_encode_reg32_kernel<256, false>, (const void*)leo16_encode_reg32_kernel<256, true>};
-    for (int i = 0; i < 4; i++)
-      if ((e = hipFuncSetAttribute(f[i], hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   i < 2 ? enc32_lds_bytes<512>() : enc32_lds_bytes<256>())) != hipSuccess)
-        return e;
-  }
+  if ((e = hipFuncSetAttribute((const void*)leo16_decode_h_kernel<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)dec_h_lds_bytes<512>())) != hipSuccess)
+    return e;
+  if ((e = hipFuncSetAttribute((const void*)leo16_decode_h_kernel<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)dec_h_lds_bytes<256>())) != hipSuccess)
+    return e;
   g_tab_done[dev] = true;
   return hipSuccess;
 }
@@ -2199,73 +1067,29 @@ bool gf16_k_ok(int k) { return k >= 256 && k <= 512 && (k & (k - 1)) == 0; }
 // k = 256 / 512): the LDS-slice kernels of rs_gf16_wide.hip.
 static bool use_wide(int k) {
   if (k > 512) return true;
-  const char* e = getenv("DAGPU_GF16_WIDE");
+  const char* e = sw(SW_GF16_WIDE);
   return e && e[0] == '1';
 }
 
-// Register encoders: 32 elements per wave at k = 512, 64 at k = 256
-// (profiles/gf16_enc16_r04.log: k = 512 split 2.00 -> 1.92 ms, Q3 Repair
-// +7 %; k = 256 split 0.77 -> 0.75 ms but Q3 Repair -4.5 %).
-// DAGPU_GF16_ENC32=0 / 1 forces either at both widths (A/B).
-static bool enc32_waves(int k) {
-  const char* e = getenv("DAGPU_GF16_ENC32");
-  if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
-  return k == 512;
-}
-
-// k = 256 / 512 encoders: the half-lane kernels (round 5); DAGPU_GF16_ENCH=0
-// selects the register kernels of round 4 (A/B)
-static bool ench_on() {  // read per launch: the tests switch it in-process
-  const char* e = getenv("DAGPU_GF16_ENCH");
-  return !(e && e[0] == '0');
-}
-
+// k = 256 / 512 encoders: the half-lane kernels, one workgroup per 256-B piece
+// of a vector's shards (a last partial piece: inactive lanes store nothing)
 hipError_t launch_leo16_encode(int k, const EncodeArgs& a, hipStream_t s) {
   if (use_wide(k)) return launch_leo16w_encode(k, a, s);
   if (!gf16_k_ok(k) || a.shard_bytes % 64) return hipErrorInvalidValue;
   if (a.reverse && !a.out_present) return hipErrorInvalidValue;  // reverse transform: Repair fill only
   hipError_t e = ensure_tables();
   if (e != hipSuccess) return e;
-#ifndef DAGPU_GF16_LDS_ENCODE
-  {  // register-resident kernel; nchunk = 512-B chunks of the shard
-    EncodeArgs b = a;
-    b.nchunk = (a.shard_bytes + 511) / 512;
-    const long blocks = b.nsq * b.nvec * b.nchunk;
-    if (blocks <= 0) return hipSuccess;
-    if (ench_on()) {  // half-lane kernels, 256-B pieces
-      b.nchunk = (a.shard_bytes + 255) / 256;
-      const long hb = b.nsq * b.nvec * b.nchunk;
-      if (k == 512) {
-        if (a.reverse) hipLaunchKernelGGL((leo16_encode_h_kernel<512, true>), dim3((unsigned)hb), dim3(512), 0, s, b);
-        else hipLaunchKernelGGL((leo16_encode_h_kernel<512, false>), dim3((unsigned)hb), dim3(512), 0, s, b);
-      } else {
-        if (a.reverse) hipLaunchKernelGGL((leo16_encode_h_kernel<256, true>), dim3((unsigned)hb), dim3(256), 0, s, b);
-        else hipLaunchKernelGGL((leo16_encode_h_kernel<256, false>), dim3((unsigned)hb), dim3(256), 0, s, b);
-      }
-    } else if (enc32_waves(k)) {
-      if (k == 256) {
-        constexpr int L = enc32_lds_bytes<256>();
-        if (a.reverse) hipLaunchKernelGGL((leo16_encode_reg32_kernel<256, true>), dim3((unsigned)blocks), dim3(512), L, s, b);
-        else hipLaunchKernelGGL((leo16_encode_reg32_kernel<256, false>), dim3((unsigned)blocks), dim3(512), L, s, b);
-      } else {
-        constexpr int L = enc32_lds_bytes<512>();
-        if (a.reverse) hipLaunchKernelGGL((leo16_encode_reg32_kernel<512, true>), dim3((unsigned)blocks), dim3(1024), L, s, b);
-        else hipLaunchKernelGGL((leo16_encode_reg32_kernel<512, false>), dim3((unsigned)blocks), dim3(1024), L, s, b);
-      }
-    } else if (k == 256) {
-      if (a.reverse) hipLaunchKernelGGL((leo16_encode_reg_kernel<256, true>), dim3((unsigned)blocks), dim3(256), 0, s, b);
-      else hipLaunchKernelGGL((leo16_encode_reg_kernel<256, false>), dim3((unsigned)blocks), dim3(256), 0, s, b);
-    } else {
-      if (a.reverse) hipLaunchKernelGGL((leo16_encode_reg_kernel<512, true>), dim3((unsigned)blocks), dim3(512), 0, s, b);
-      else hipLaunchKernelGGL((leo16_encode_reg_kernel<512, false>), dim3((unsigned)blocks), dim3(512), 0, s, b);
-    }
-    return hipGetLastError();
+  EncodeArgs b = a;
+  b.nchunk = (a.shard_bytes + 255) / 256;
+  const long hb = b.nsq * b.nvec * b.nchunk;
+  if (hb <= 0) return hipSuccess;
+  if (k == 512) {
+    if (a.reverse) hipLaunchKernelGGL((leo16_encode_h_kernel<512, true>), dim3((unsigned)hb), dim3(512), 0, s, b);
+    else hipLaunchKernelGGL((leo16_encode_h_kernel<512, false>), dim3((unsigned)hb), dim3(512), 0, s, b);
+  } else {
+    if (a.reverse) hipLaunchKernelGGL((leo16_encode_h_kernel<256, true>), dim3((unsigned)hb), dim3(256), 0, s, b);
+    else hipLaunchKernelGGL((leo16_encode_h_kernel<256, false>), dim3((unsigned)hb), dim3(256), 0, s, b);
   }
-#endif
-  const long blocks = a.nsq * a.nvec * (a.shard_bytes / 64);
-  if (blocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(leo16_encode_kernel, dim3((unsigned)blocks), dim3(kThreads16),
-                     (size_t)k * 64, s, a, k);
   return hipGetLastError();
 }
 
@@ -2276,59 +1100,11 @@ hipError_t launch_leo16_errlocs(const DecodeArgs& a, hipStream_t s) {
   if (e != hipSuccess) return e;
   const long nv = a.nsq * a.nvec;
   if (nv <= 0) return hipSuccess;
-  if (a.k == 256 && !getenv("DAGPU_ERRLOC_FULL"))
+  if (a.k == 256)
     hipLaunchKernelGGL(leo16_errlocs_fold_kernel<512>, dim3((unsigned)nv), dim3(kFoldThreads), 0, s, a);
-  else if (a.k == 512 && !getenv("DAGPU_ERRLOC_FULL"))
-    hipLaunchKernelGGL(leo16_errlocs_fold_kernel<1024>, dim3((unsigned)nv), dim3(kFoldThreads), 0, s, a);
-  else  // DAGPU_ERRLOC_FULL=1: the 65536-point form (A/B and cross-check)
-    hipLaunchKernelGGL(leo16_errlocs_kernel, dim3((unsigned)nv), dim3(kErrThreads), kErrLds, s, a);
-  return hipGetLastError();
-}
-
-// dynamic LDS of the register-resident decoders: staging + erasure tables
-constexpr size_t kDecLds = (8 * 16 * 2 * 64 + kDecN * 16) * sizeof(uint32_t);    // 96 KiB
-constexpr size_t kDec1kLds = (16 * 16 * 64 + kDec1k * 16) * sizeof(uint32_t);     // 128 KiB
-static hipError_t dec_lds_attr() {  // above the 64 KiB default: once per process
-  static std::once_flag once;
-  static hipError_t err = hipSuccess;
-  std::call_once(once, [] {
-    err = hipFuncSetAttribute((const void*)leo16_decode_reg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)kDecLds);
-    if (err == hipSuccess)
-      err = hipFuncSetAttribute((const void*)leo16_decode_reg1k_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDec1kLds);
-    const void* h512[2] = {(const void*)leo16_decode_h_kernel<512, 0>, (const void*)leo16_decode_h_kernel<512, 1>};
-    const void* h256[2] = {(const void*)leo16_decode_h_kernel<256, 0>, (const void*)leo16_decode_h_kernel<256, 1>};
-    for (int i = 0; i < 2 && err == hipSuccess; i++) {
-      err = hipFuncSetAttribute(h512[i], hipFuncAttributeMaxDynamicSharedMemorySize, (int)dec_h_lds_bytes<512>());
-      if (err == hipSuccess)
-        err = hipFuncSetAttribute(h256[i], hipFuncAttributeMaxDynamicSharedMemorySize, (int)dec_h_lds_bytes<256>());
-    }
-  });
-  return err;
-}
-
-// half-lane decoders: DAGPU_DEC_LOADALL=1 loads missing shards too (LD = 0, A/B
-// of the out-of-range skip); read per launch
-template <int K>
-static void launch_dec_h(const DecodeArgs& b, long grid, hipStream_t s) {
-  const char* e = getenv("DAGPU_DEC_LOADALL");
-  if (e && e[0] == '1')
-    hipLaunchKernelGGL((leo16_decode_h_kernel<K, 0>), dim3((unsigned)grid), dim3(2 * K), dec_h_lds_bytes<K>(), s, b);
   else
-    hipLaunchKernelGGL((leo16_decode_h_kernel<K, 1>), dim3((unsigned)grid), dim3(2 * K), dec_h_lds_bytes<K>(), s, b);
-}
-// k = 256 decoder: the half-lane kernel (round 5); DAGPU_DEC256_REG=1 selects
-// leo16_decode_reg_kernel (A/B)
-static bool dec256_reg() {
-  const char* e = getenv("DAGPU_DEC256_REG");
-  return e && e[0] == '1';
-}
-// k = 512 decoder: the half-lane unpacked kernel (round 5); DAGPU_DEC1K_PACKED=1
-// selects the packed one of rounds 2-4 (A/B)
-static bool dec1k_packed() {  // read per launch: the tests switch it in-process
-  const char* e = getenv("DAGPU_DEC1K_PACKED");
-  return e && e[0] == '1';
+    hipLaunchKernelGGL(leo16_errlocs_fold_kernel<1024>, dim3((unsigned)nv), dim3(kFoldThreads), 0, s, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mark_present) {
@@ -2338,28 +1114,15 @@ hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mar
   if (e != hipSuccess) return e;
   const long nv = a.nsq * a.nvec;
   if (nv <= 0) return hipSuccess;
-#ifndef DAGPU_GF16_LDS_DECODE
-  if (a.k == 256 && a.shard_bytes % 256 == 0 && !dec256_reg()) {  // half-lane decoder, 256-B pieces
+  if (a.shard_bytes % 256 == 0) {  // half-lane decoders, 256-B pieces
     DecodeArgs b = a;
     b.nchunk = a.shard_bytes / 256;
-    if ((e = dec_lds_attr()) != hipSuccess) return e;
-    launch_dec_h<256>(b, nv * b.nchunk, s);
-  } else if (a.k == kDecN / 2) {  // register-resident decoder; nchunk = 512-B chunks of the shard
-    DecodeArgs b = a;
-    b.nchunk = (a.shard_bytes + 511) / 512;
-    if ((e = dec_lds_attr()) != hipSuccess) return e;
-    hipLaunchKernelGGL(leo16_decode_reg_kernel, dim3((unsigned)(nv * b.nchunk)), dim3(kDecN), kDecLds, s, b);
-  } else if (a.k == kDec1k / 2 && a.shard_bytes % 256 == 0) {  // k = 512: 256-B pieces
-    DecodeArgs b = a;
-    b.nchunk = a.shard_bytes / 256;
-    if ((e = dec_lds_attr()) != hipSuccess) return e;
-    if (dec1k_packed())
-      hipLaunchKernelGGL(leo16_decode_reg1k_kernel, dim3((unsigned)(nv * b.nchunk)), dim3(kDec1k), kDec1kLds, s, b);
+    const long grid = nv * b.nchunk;
+    if (a.k == 512)
+      hipLaunchKernelGGL((leo16_decode_h_kernel<512>), dim3((unsigned)grid), dim3(1024), dec_h_lds_bytes<512>(), s, b);
     else
-      launch_dec_h<512>(b, nv * b.nchunk, s);
-  } else
-#endif
-  {
+      hipLaunchKernelGGL((leo16_decode_h_kernel<256>), dim3((unsigned)grid), dim3(512), dec_h_lds_bytes<256>(), s, b);
+  } else {  // shard sizes off the 256-B grid (codec API): the generic LDS decoder
     const long blocks = nv * (a.shard_bytes / 64);
     hipLaunchKernelGGL(leo16_decode_kernel, dim3((unsigned)blocks), dim3(kThreads16),
                        (size_t)a.k * 2 * 64 * 2, s, a);
@@ -2520,7 +1283,6 @@ hipError_t launch_errloc_heads(const DecodeArgs& a, hipStream_t s) {
 hipError_t launch_rs_prepare(int k) {
   if (k <= 128) return hipSuccess;  // GF(2^8): constexpr tables
   hipError_t e = ensure_tables();
-  if (e == hipSuccess) e = dec_lds_attr();
   if (e == hipSuccess) e = leo16w_prepare();
   return e;
 }

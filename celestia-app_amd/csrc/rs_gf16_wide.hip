@@ -76,6 +76,10 @@ __device__ __forceinline__ void pmul_add(uint32_t& xlo, uint32_t& xhi, uint32_t 
 
 // The only zero skews (log 0) sit at positions 2^m - 1 (Leopard skips their
 // multiply): the block at offset 0 of every layer, all of the top layer.
+// Leopard's initFFTSkew zeroes FFTSkew[2^m - 1] only for m <= kBits - 2 = 14
+// (position 32767 has a nonzero skew), so the bit test holds only while every
+// position a transform uses stays below 2^14.
+static_assert(kPtabPos <= (1 << 14), "zero_skew: FFTSkew[2^m - 1] is log 0 only for m <= 14");
 __device__ __forceinline__ bool zero_skew(int pos) { return ((pos + 1) & pos) == 0; }
 __device__ __forceinline__ void load_tab(const WideTabs& T, int pos, uint32_t (&t)[kTabW]) {
   const uint4* p = (const uint4*)(T.ptab + (long)pos * kTabW);

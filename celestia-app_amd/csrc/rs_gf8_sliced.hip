@@ -363,10 +363,8 @@ static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 // 512-B chunks, vectors in groups of 4, 16-B aligned rows, no compare mode or
 // vector mask.  DAGPU_ENC_SLICED=0 selects the packed-byte kernel for A/B runs.
 bool leo8_sliced_applicable(int k, const EncodeArgs& a) {
-  static const bool enabled = [] {
-    const char* e = getenv("DAGPU_ENC_SLICED");
-    return !(e && e[0] == '0');
-  }();
+  const char* e = sw(SW_ENC_SLICED);
+  const bool enabled = !(e && e[0] == '0');
   if (!enabled || k < 16 || k > 128) return false;
   if (a.shard_bytes <= 0 || a.shard_bytes % 512 || a.nvec % 4 || a.vec_flags || a.mismatch || a.out_present ||
       a.reverse)
@@ -389,11 +387,8 @@ bool leo8_sliced_applicable(int k, const EncodeArgs& a) {
 
 // DAGPU_ENC_SLICED2=0 keeps k = 128 on the 4-vector kernel (A/B runs).
 static bool sliced2_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("DAGPU_ENC_SLICED2");
-    return !(e && e[0] == '0');
-  }();
-  return on;
+  const char* e = sw(SW_ENC_SLICED2);
+  return !(e && e[0] == '0');
 }
 
 hipError_t launch_leo8_encode_sliced(int k, const EncodeArgs& a, hipStream_t s) {

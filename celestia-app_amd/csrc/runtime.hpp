@@ -91,7 +91,7 @@ struct dagpu_ctx {
   // fill few CUs, overlap the leaves of slice i+1) and a high-priority RS stream.
   static constexpr size_t kMaxSideStreams = 16;
   struct Side {
-    hipStream_t caller = nullptr, rs = nullptr, rs_hi = nullptr, nmt = nullptr;
+    hipStream_t caller = nullptr, rs = nullptr, rs_hi = nullptr;
   };
   std::mutex side_mu;
   std::vector<Side> side;
@@ -211,12 +211,13 @@ inline bool& on_repair_worker() {
 }
 
 // dagpu.cpp: timing-disabled events recycled per call, and the side streams
-// paired with a caller stream (which: 0 RS, 1 RS at the greatest priority, 2 NMT).
+// paired with a caller stream (which: 0 normal, 1 the greatest priority).
+namespace dagpu {
 hipEvent_t ev_take(dagpu_ctx* c);
 void ev_give(dagpu_ctx* c, hipEvent_t e);
 hipStream_t side_stream(dagpu_ctx* ctx, hipStream_t s, int which = 0);
-long env_long(const char* name);
 size_t pipe_slices(dagpu_ctx* ctx, uint32_t k, size_t n);
+}  // namespace dagpu
 
 inline hipEvent_t pool_get(dagpu_ctx* c) {
   if (!c->pool.empty()) {

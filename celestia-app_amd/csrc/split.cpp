@@ -192,7 +192,7 @@ int dagpu_split_cols_device(dagpu_ctx* ctx, uint32_t k, uint32_t parts, uint32_t
   // column roots go out directly, its row roots as the 96-B records the finish
   // step reads.  (At k >= 1024 the forest path overlaps the top half's leaves
   // with the column encode, which measured faster.)
-  const char* sq_env = getenv("DAGPU_SPLIT_SQUARE");
+  const char* sq_env = sw(SW_SPLIT_SQUARE);
   if (parts == 1 && k < 1024 && !(sq_env && sq_env[0] == '0')) {
     {
       ProfScope p(ctx, 1, s);
@@ -216,7 +216,7 @@ int dagpu_split_cols_device(dagpu_ctx* ctx, uint32_t k, uint32_t parts, uint32_t
     HIP_TRY(ctx, dagpu::launch_node_to_rec(ws.leaves, w, d_row_sub, s));
     return DAGPU_OK;
   }
-  const char* ov_env = getenv("DAGPU_SPLIT_OVERLAP");
+  const char* ov_env = sw(SW_SPLIT_OVERLAP);
   const int overlap = ctx->prof ? 0 : ov_env ? atoi(ov_env) : k >= 1024 ? 1 : 0;
   hipStream_t es = overlap ? side_stream(ctx, s, overlap == 1 ? 1 : 0) : nullptr;
   hipEvent_t fork = es ? ev_take(ctx) : nullptr, joined = es ? ev_take(ctx) : nullptr;

@@ -207,8 +207,13 @@ int dagpu_repair_batch_device_ex(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* 
  * its last command and makes stream2 wait for the repair; it returns the
  * repair's call status (per-square results in d_status).  Repairs started back
  * to back (slices of a batch, squares of several blocks) run side by side; a
- * context serves 64 started, not yet joined repairs.  The buffers must stay
- * valid until the joined stream has passed the repair.  Joins from several
+ * context serves 64 started, not yet joined repairs.  Buffer lifetime: d_eds,
+ * d_present, d_status and d_workspace (and the roots) must stay valid until
+ * stream2 -- the stream passed to dagpu_repair_join -- has passed the repair.
+ * Free or reuse them only in stream2's order (work queued on stream2 after the
+ * join, or after hipStreamSynchronize(stream2)); an allocator that frees in
+ * another stream's order must first make that stream wait for stream2 (the
+ * Python wrapper calls record_stream(stream2) on each buffer).  Joins from several
  * host threads wait side by side (the slot table is locked only to claim a
  * slot); a failed repair's message is re-raised on the joining thread
  * (dagpu_last_error), and a worker that cannot be started returns

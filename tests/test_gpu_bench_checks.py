@@ -233,31 +233,25 @@ def test_device_batch_in_place_matches(ctx):
     assert (b.dah.cpu().numpy() == hdah).all()
 
 
-@pytest.mark.parametrize("n,slices,first,in_place,nmt2,prio", [
-    (64, None, None, True, None, None),     # the headline shape: 4 slices of 16, ODS in Q0
-    (67, None, None, True, None, None),     # uneven slices
-    (70, "2", None, False, None, None),
-    (65, "8", None, True, None, None),
-    (66, "4", "3", True, None, None),       # small first slice (DAGPU_PIPE_FIRST)
-    (64, "3", None, False, None, None),     # slice count that does not divide n
-    (64, "1", None, True, None, None),      # pipeline off
-    (64, None, None, True, "0", "0"),       # one NMT stream, normal-priority RS
-    (67, None, None, True, "1", "1"),       # two NMT streams (odd slices, 2nd workspace half), RS priority
-    (70, "2", "50", False, "1", "0"),       # 2nd NMT stream disabled: workspace holds one 50-square slice only
-    (65, "5", None, True, "1", "1"),
+@pytest.mark.parametrize("n,slices,in_place", [
+    (64, None, True),     # the headline shape: 4 slices of 16, ODS in Q0
+    (67, None, True),     # uneven slices
+    (70, "2", False),
+    (65, "8", True),
+    (64, "3", False),     # slice count that does not divide n
+    (64, "1", True),      # pipeline off
+    (65, "5", True),
 ])
-def test_pipelined_device_batch(ctx, monkeypatch, n, slices, first, in_place, nmt2, prio):
+def test_pipelined_device_batch(ctx, monkeypatch, n, slices, in_place):
     """The RS/NMT slice pipeline of dagpu_extend_batch_device at k = 128 under
-    several slice and stream settings (read per call), with the ODS in place or
-    separate, over two steps: every DAH and root equals the host API's
+    several slice counts (DAGPU_PIPE_SLICES, read per call), with the ODS in
+    place or separate, over two steps: every DAH and root equals the host API's
     (unsliced chain), and two squares equal the oracle's."""
     k = 128
-    for name, v in (("DAGPU_PIPE_SLICES", slices), ("DAGPU_PIPE_FIRST", first),
-                    ("DAGPU_PIPE_NMT2", nmt2), ("DAGPU_RS_PRIO", prio)):
-        if v is None:
-            monkeypatch.delenv(name, raising=False)
-        else:
-            monkeypatch.setenv(name, v)
+    if slices is None:
+        monkeypatch.delenv("DAGPU_PIPE_SLICES", raising=False)
+    else:
+        monkeypatch.setenv("DAGPU_PIPE_SLICES", slices)
     ods = synth.blob_squares(k, 6400 + n, 0, n, threads=16)
     ds = DeviceSquares(k, n, ctx=ctx, in_place=in_place)
     ds.load_ods(ods)

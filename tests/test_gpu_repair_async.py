@@ -92,24 +92,70 @@ def test_start_returns_at_once_and_slices_run_side_by_side(ctx):
     assert torch.equal(ds.eds, ref) and (status.cpu().numpy() == 0).all() and bool(present.all())
 
 
-def test_worker_failure_reaches_the_joining_thread(ctx, monkeypatch):
-    # the worker's message is re-raised on the caller's thread at the join,
-    # and the slot is free again afterwards
-    k, n = 8, 2
-    ds, pres_t, ref, damaged = _setup(ctx, k, n, 32)
-    present, status = _inputs(ds, pres_t, damaged)
-    monkeypatch.setenv("DAGPU_TEST_WORKER_FAIL", "1")
-    h = ds.repair_start(present, status, ds.repair_workspace())
-    with pytest.raises(da.DAError, match="injected worker failure"):
-        ds.repair_join(h)
+_WORKER_FAIL_SCRIPT = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+from celestia_da import _abi, da, synth
+from celestia_da.device import DeviceSquares
+import os
+ctx = da.Context(0)
+k, n, w = 8, 2, 16
+ds = DeviceSquares(k, n, ctx=ctx)
+ds.load_ods(synth.blob_squares(k, 32, 0, n))
+ds.extend()
+torch.cuda.synchronize()
+ref = ds.eds.clone()
+pres = np.zeros((n, w, w), np.uint8)
+pres[:, :k, :k] = 1
+pres_t = torch.from_numpy(pres.reshape(n, -1)).cuda()
+damaged = (ds.eds.view(n, w * w, 512) * pres_t.view(n, w * w, 1)).view(n, -1).clone()
+def inputs():
+    ds.eds.copy_(damaged)
+    st = torch.full((n,), 99, dtype=torch.int32, device="cuda")
     torch.cuda.synchronize()
-    assert (status.cpu().numpy() == _abi.ERR_DEVICE).all()
-    monkeypatch.delenv("DAGPU_TEST_WORKER_FAIL")
-    present, status = _inputs(ds, pres_t, damaged)
-    h = ds.repair_start(present, status, ds.repair_workspace())
+    return pres_t.clone(), st
+present, status = inputs()
+os.environ["DAGPU_TEST_WORKER_FAIL"] = "1"
+h = ds.repair_start(present, status, ds.repair_workspace())
+del os.environ["DAGPU_TEST_WORKER_FAIL"]  # the start call took it already
+try:
     ds.repair_join(h)
-    torch.cuda.synchronize()
-    assert torch.equal(ds.eds, ref) and (status.cpu().numpy() == 0).all()
+    print("JOIN_OK")
+except da.DAError as e:
+    print("JOIN_ERR", e)
+torch.cuda.synchronize()
+print("STATUS", status.cpu().numpy().tolist())
+present, status = inputs()
+h = ds.repair_start(present, status, ds.repair_workspace())
+ds.repair_join(h)
+torch.cuda.synchronize()
+print("AFTER", bool(torch.equal(ds.eds, ref)), status.cpu().numpy().tolist())
+ctx.close()
+"""
+
+
+@pytest.mark.parametrize("lib", ["libdagpu_test.so", "libdagpu.so"])
+def test_worker_failure_reaches_the_joining_thread(lib):
+    """The test build (DAGPU_TEST_HOOKS, libdagpu_test.so) injects a worker
+    failure: its message is re-raised on the caller's thread at the join, the
+    statuses say ERR_DEVICE, and the slot serves the next repair.  The product
+    library carries no such hook: the same environment repairs normally."""
+    import os
+    import subprocess
+    import sys
+
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "celestia-app_amd")
+    env = dict(os.environ, DAGPU_LIB=os.path.join(pkg, lib))
+    r = subprocess.run([sys.executable, "-c", _WORKER_FAIL_SCRIPT, pkg], env=env, capture_output=True,
+                       text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = r.stdout
+    if lib == "libdagpu_test.so":
+        assert "JOIN_ERR" in out and "injected worker failure" in out, out
+        assert f"STATUS {[_abi.ERR_DEVICE] * 2}" in out, out
+    else:
+        assert "JOIN_OK" in out and "STATUS [0, 0]" in out, out
+    assert "AFTER True [0, 0]" in out, out
 
 
 def test_joins_from_threads_run_side_by_side(ctx):
@@ -196,3 +242,24 @@ def test_started_repair_holds_its_tensors(ctx):
     torch.cuda.synchronize()
     assert torch.equal(ds.eds, ref) and (status.cpu().numpy() == 0).all()
     assert h not in ds._held
+
+
+def test_join_on_another_stream_keeps_tensors_until_it(ctx):
+    """A repair started on the default stream and joined on a side stream: the
+    wrapper releases its held tensors with record_stream(join stream), so the
+    caching allocator does not hand the workspace to a same-size allocation on
+    the default stream (filled with junk at once, while the repair still runs on
+    the library's stream) before the joined stream has passed the repair."""
+    k, n = 128, 16
+    ds, pres_t, ref, damaged = _setup(ctx, k, n, 617)
+    for _ in range(2):
+        present, status = _inputs(ds, pres_t, damaged)
+        side = torch.cuda.Stream()
+        h = ds.repair_start(present, status, ds.repair_workspace())  # temporary workspace
+        ds.repair_join(h, stream=side)
+        junk = torch.empty((ctx._L.dagpu_repair_workspace_size(k, n),), dtype=torch.uint8, device="cuda")
+        junk.fill_(0x5A)
+        side.synchronize()
+        torch.cuda.synchronize()
+        assert torch.equal(ds.eds, ref) and (status.cpu().numpy() == 0).all()
+        del junk

@@ -47,6 +47,32 @@ def test_split_local_matches_oracle(ctx, k, parts):
     assert got_dah == dah
 
 
+@pytest.mark.parametrize("k,parts", [(16, 1), (256, 1), (256, 4), (512, 2)])
+def test_split_on_a_side_stream(ctx, k, parts):
+    """advisor r05: the split's library steps only queue work on the caller's
+    stream, so the torch-side steps between them run in that stream's order
+    too.  A side stream held back by a GPU sleep, the ODS written on it first:
+    a read on any other stream would see the old bytes or race the kernels."""
+    ods, rr, cr, dah = _want(k, 7300 + k)
+    side = torch.cuda.Stream()
+    d = torch.zeros(ods.size, dtype=torch.uint8, device="cuda")
+    host = torch.from_numpy(np.ascontiguousarray(ods).reshape(-1)).pin_memory()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(int(5e7))
+        d.copy_(host, non_blocking=True)
+    assert split.extend_split_local(d, k, parts, ctx, stream=side) == (rr, cr, dah)
+    part = split.SplitPart(k, 1, 0, ctx, d.device)
+    with torch.cuda.stream(side):
+        d.zero_()
+        torch.cuda._sleep(int(5e7))
+        d.copy_(host, non_blocking=True)
+    got_rr, got_cr, got_dah = split.extend_split_distributed(None, part, d, stream=side)
+    side.synchronize()
+    assert (got_rr.cpu().numpy().tobytes(), got_cr.cpu().numpy().tobytes(), got_dah.cpu().numpy().tobytes()) == \
+        (rr, cr, dah)
+
+
 @pytest.mark.parametrize("square", ["0", "1"])
 @pytest.mark.parametrize("k", [1, 2, 16, 128, 512])
 def test_split_one_part_paths(ctx, monkeypatch, k, square):
