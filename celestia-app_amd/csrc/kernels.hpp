@@ -17,7 +17,17 @@ constexpr int kDigest = 32;
 constexpr int kMaxK = 8192;
 
 // Bytes of error-locator workspace per decoded vector.
-constexpr long rs_err_bytes(int k) { return k <= 128 ? 256 : 4L * k; }
+// Error-locator workspace per vector: GF(2^8) 256 B; GF(2^16) the n = 2k uint16
+// locators (4k B) and after them, at rs_err_tab_off(k), what the decoders'
+// per-element multiplies need, built once per erasure pattern by the locator
+// kernel (round 6) instead of in every decoder workgroup: at k = 256 / 512 the
+// n x 80-B image of the product tables (exp(errLoc) for a present element,
+// exp(-errLoc) for a missing one) that a half-lane decoder copies into LDS;
+// at k >= 1024 the n x 32-B basis products (1 << b) * that factor, b < 16, from
+// which a wide decoder workgroup builds an element's table without gathers.
+constexpr long rs_err_tab_off(int k) { return 4L * k; }
+constexpr long rs_err_elem_bytes(int k) { return k <= 512 ? 80 : 32; }
+constexpr long rs_err_bytes(int k) { return k <= 128 ? 256 : 4L * k + 2L * k * rs_err_elem_bytes(k); }
 
 // Per-square status bits written by the kernels (0 = OK).
 constexpr int kStatusPushOrder = 1;

@@ -198,6 +198,9 @@ __device__ __forceinline__ void fwht_n(uint32_t* e) {
   }
 }
 
+constexpr int kTab16x = 20;  // dwords per 3/3/2 product table (mul16x_add_t)
+__device__ __forceinline__ void mul16x_table_to(uint32_t* out, uint32_t lm);
+
 template <int N>
 __global__ __launch_bounds__(kFoldThreads) void leo16_errlocs_fold_kernel(DecodeArgs a) {
   __shared__ uint32_t e[N];
@@ -210,10 +213,12 @@ __global__ __launch_bounds__(kFoldThreads) void leo16_errlocs_fold_kernel(Decode
   if (threadIdx.x == 0) cnt_s = 0;
   __syncthreads();
   int cnt = 0;
-  for (int i = threadIdx.x; i < N; i += kFoldThreads) {
+  uint32_t miss = 0;  // bit r: element threadIdx.x + r * kFoldThreads is missing
+  for (int i = threadIdx.x, r = 0; i < N; i += kFoldThreads, r++) {
     const uint32_t x = i < k ? (pres[(long)(k + i) * a.p_shard_stride] ? 0u : 1u)   // parity k+i -> work i
                              : (pres[(long)(i - k) * a.p_shard_stride] ? 0u : 1u);  // data i-k -> work i
     e[i] = x;
+    miss |= x << r;
     cnt += (x == 0);
   }
   atomicAdd(&cnt_s, cnt);
@@ -238,6 +243,17 @@ __global__ __launch_bounds__(kFoldThreads) void leo16_errlocs_fold_kernel(Decode
   fwht_n<N>(e);
   uint16_t* out = (uint16_t*)(a.err + hv * (long)rs_err_bytes(k));
   for (int i = threadIdx.x; i < N; i += kFoldThreads) out[i] = (uint16_t)e[i];
+  // Round 6: the half-lane decoders' per-element product tables, built here
+  // once per erasure pattern (not in every decoder workgroup: 16 random exp
+  // gathers per element were the decoder's slowest phase, tools/phase_probe.py
+  // dec512h) -- exp(errLoc) for a present element (premultiply), exp(-errLoc)
+  // for a missing one (postmultiply), element-major, 80 B each: the LDS image
+  // the decoder copies with global_load_lds.
+  uint32_t* tabs = (uint32_t*)(a.err + hv * (long)rs_err_bytes(k) + rs_err_tab_off(k));
+  for (int i = threadIdx.x, r = 0; i < N; i += kFoldThreads, r++) {
+    const uint32_t lm = e[i] & 0xFFFFu;
+    mul16x_table_to(tabs + (long)i * kTab16x, ((miss >> r) & 1) ? kMod16 - lm : lm);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -346,7 +362,6 @@ constexpr int kTabPos = 1024;
 //   [4,5] group 1 (bits 3-5) lo / [6,7] hi           [8] group 2 (bits 6-7) lo, [9] hi
 //   [10..13] group 3 (bits 8-10), [14..17] group 4 (bits 11-13), [18, 19] group 5 (bits 14-15)
 // entry e of a group at byte e of its pool: product (e << shift) * c.
-constexpr int kTab16x = 20;
 __constant__ uint32_t g_ptab16x[kTabPos * kTab16x];
 __constant__ uint32_t g_ptab16x_merged[2 * kTab16x];
 
@@ -607,15 +622,51 @@ __device__ __forceinline__ void xpose_bt(W32& w, uint32_t* lds, int q, int lane)
   }
 }
 
+// xpose_bt over two LDS buffers of one round each (round r in buffer (B0 + r)
+// & 1, buffer 1 at lds + NQ * NQ * RPR * 64): a barrier between a round's
+// writes and reads, none after the reads -- the next round writes the other
+// buffer, and the one after it writes this buffer only past the next round's
+// barrier, which every wave reaches after its reads here (round 6: the k = 512
+// decoder's transposes and derivative 8 -> 4 barriers each).
+template <int LR, int RPR, int B0>
+__device__ __forceinline__ void xpose_bt_db(W32& w, uint32_t* lds, int q, int lane) {
+  constexpr int NQ = 32 >> LR;
+  constexpr int RW = NQ * NQ * RPR * 64;  // dwords per round
+#pragma unroll
+  for (int r0 = 0; r0 < (1 << LR); r0 += RPR) {
+#pragma unroll
+    for (int lh = 0; lh < 2; lh++) {
+      uint32_t* buf = lds + ((B0 + 2 * (r0 / RPR) + lh) & 1) * RW;
+#pragma unroll
+      for (int c = 0; c < NQ; c++)
+#pragma unroll
+        for (int u = 0; u < RPR; u++)
+          buf[((c * NQ + q) * RPR + u) * 64 + lane] = lh ? w.hi[(c << LR) | (r0 + u)] : w.lo[(c << LR) | (r0 + u)];
+      __syncthreads();
+#pragma unroll
+      for (int c = 0; c < NQ; c++)
+#pragma unroll
+        for (int u = 0; u < RPR; u++) {
+          const uint32_t v = buf[((q * NQ + c) * RPR + u) * 64 + lane];
+          if (lh) w.hi[(c << LR) | (r0 + u)] = v;
+          else w.lo[(c << LR) | (r0 + u)] = v;
+        }
+    }
+  }
+}
+
 // Formal derivative in layout T, D(x)_e = x_e ^ XOR_{s: bit s of e = 0} x_{e | 2^s}:
 // register bits (element bits 1..LR and 6..) in place in ascending register
 // order, wave bits (LR+1 .. 5) and the half bit (0, lanes 0-31 read lane + 32)
 // from the originals staged in LDS, 8 register pairs per round (NQ waves).
-template <int NQ>
-__device__ __forceinline__ void derivative_t(W32& w, uint32_t* lds, int c, int lane, uint32_t lowmask) {
+// DB: two buffers of one round each, alternating as in xpose_bt_db (round r in
+// buffer r & 1, no barrier after a round's reads); otherwise one buffer.
+template <int NQ, bool DB = false>
+__device__ __forceinline__ void derivative_t(W32& w, uint32_t* lds0, int c, int lane, uint32_t lowmask) {
   constexpr int B = 8;
 #pragma unroll
   for (int s0 = 0; s0 < 32; s0 += B) {
+    uint32_t* lds = lds0 + (DB ? ((s0 / B) & 1) * (NQ * B * 2 * 64) : 0);
 #pragma unroll
     for (int u = 0; u < B; u++) {
       lds[((c * B + u) * 2) * 64 + lane] = w.lo[s0 + u];
@@ -645,7 +696,7 @@ __device__ __forceinline__ void derivative_t(W32& w, uint32_t* lds, int c, int l
       w.lo[j] = alo;
       w.hi[j] = ahi;
     }
-    __syncthreads();
+    if constexpr (!DB) __syncthreads();
   }
 }
 
@@ -709,9 +760,97 @@ __device__ __forceinline__ void mul16x_by(uint32_t& xl, uint32_t& xh, const uint
 }
 
 // K = 512 (n = 1024, 16 waves, LR = 1) and, round 5, K = 256 (n = 512, 8 waves,
-// LR = 2: 512 threads at <= 128 VGPRs and 64 KiB of LDS, two workgroups per CU).
+// LR = 2: 512 threads at <= 128 VGPRs and 72 KiB of LDS, two workgroups per CU).
+// Dynamic LDS, round 6:
+//   K = 512 (one workgroup per CU, 160 KiB): buffers A = [0, 64 KiB) and
+//     B = [64, 128 KiB) of the double-buffered transposes and derivative
+//     (xpose_bt_db), the n x 80-B tables at [80, 160 KiB) -- at the start for
+//     the premultiply and reloaded after the last transpose for the
+//     postmultiply (the first round that writes B follows a barrier every wave
+//     reaches after its premultiply);
+//   K = 256: [0, n x 64 B) single-buffered staging, then the n x 80-B tables.
+// bit-0 layer in layout S with its tables from LDS (round 6): `posl` holds the
+// tables of the even positions OFF + 2 i at i x 80 B (pos_tables_to_lds), so a
+// lane reads its pair's table with ds_read_b128 (the two halves of a wave read
+// two tables) instead of five buffer loads from the constant tables per pair,
+// whose latency each pair waited for (one table live at a time).
+template <bool INV>
+__device__ __forceinline__ void layer0_sl(W32& w, int q, int hl, const uint32_t* posl) {
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    uint32_t t[kTab16x];
+    mul16x_table_from(posl, opaque_v(32 * q + j + 16 * hl, w.lo[j > 0 ? j - 1 : 0]), t);
+    if constexpr (INV) {
+      w.lo[j + 16] ^= w.lo[j];
+      w.hi[j + 16] ^= w.hi[j];
+      mul16x_add_t(w.lo[j], w.hi[j], w.lo[j + 16], w.hi[j + 16], t);
+    } else {
+      mul16x_add_t(w.lo[j], w.hi[j], w.lo[j + 16], w.hi[j + 16], t);
+      w.lo[j + 16] ^= w.lo[j];
+      w.hi[j + 16] ^= w.hi[j];
+    }
+    asm volatile("" : "+v"(w.lo[j]), "+v"(w.hi[j]), "+v"(w.lo[j + 16]), "+v"(w.hi[j + 16]));
+  }
+}
+
+typedef __attribute__((address_space(3))) void* lds_vptr;
+typedef __attribute__((address_space(1))) void* glb_vptr;
+// The constant tables of the NPOS even positions OFF, OFF + 2, .. into LDS
+// (i x 80 B) with global_load_lds, THREADS threads: 16-B chunk c (table c / 5,
+// part c % 5) lane-linear within each wave.
+template <int NPOS, int THREADS, int OFF>
+__device__ __forceinline__ void pos_tables_to_lds(uint32_t* dst, int q, int lane) {
+  constexpr int NCH = NPOS * 5;
+  static_assert(NCH % 64 == 0, "whole waves of chunks");
+  const uint8_t* src = (const uint8_t*)(const void*)g_ptab16x;
+#pragma unroll
+  for (int i = 0; i < (NCH + THREADS - 1) / THREADS; i++) {
+    const int c0 = i * THREADS + 64 * q;  // the wave's first chunk (uniform)
+    if (c0 < NCH) {
+      const int c = c0 + lane;
+      const uint8_t* g = src + (long)(OFF + 2 * (c / 5)) * (kTab16x * 4) + (c % 5) * 16;
+      __builtin_amdgcn_global_load_lds((glb_vptr)g, (lds_vptr)(dst + c0 * 4), 16, 0, 0);
+    }
+  }
+}
+
+// The tables of one wave's 32 bit-0-layer positions OFF + 2 i, i in [32 q, 32 q + 32)
+// (the half-lane encoders' layout S), into the LDS image of pos_tables_to_lds by
+// the wave itself: 160 chunks of 16 B, so the wave needs no workgroup barrier,
+// only its own vmcnt wait (wait_dma) before reading them.
+template <int OFF>
+__device__ __forceinline__ void pos_tables_wave(uint32_t* dst, int q, int lane) {
+  const uint8_t* src = (const uint8_t*)(const void*)g_ptab16x;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const int c0 = 160 * q + 64 * i;  // uniform
+    const int c = c0 + lane;
+    if (i < 2 || lane < 32) {
+      const uint8_t* g = src + (long)(OFF + 2 * (c / 5)) * (kTab16x * 4) + (c % 5) * 16;
+      __builtin_amdgcn_global_load_lds((glb_vptr)g, (lds_vptr)(dst + c0 * 4), 16, 0, 0);
+    }
+  }
+}
+__device__ __forceinline__ void wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 template <int K>
-constexpr size_t dec_h_lds_bytes() { return (size_t)(2 * K) * (16 + kTab16x) * sizeof(uint32_t); }
+constexpr size_t dec_h_tab_off() { return K == 512 ? 80 * 1024 : (size_t)(2 * K) * 64; }
+template <int K>
+constexpr size_t dec_h_lds_bytes() { return dec_h_tab_off<K>() + (size_t)(2 * K) * kTab16x * sizeof(uint32_t); }
+static_assert(dec_h_lds_bytes<512>() == 160 * 1024 && dec_h_lds_bytes<256>() == 72 * 1024, "decoder LDS");
+
+// The n x 80-B table image of vector v's erasure pattern (leo16_errlocs_fold_kernel)
+// into LDS with global_load_lds (no VGPRs, 5 x 16 B per thread): chunk
+// c = i * 2K + thread, lane-linear within each wave as the DMA writes it.
+template <int K>
+__device__ __forceinline__ void dec_h_load_tables(uint32_t* tab, const uint8_t* img, int q, int lane) {
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    const long c = (long)i * (2 * K) + 64 * q;  // the wave's first chunk
+    __builtin_amdgcn_global_load_lds((glb_vptr)(img + (c + lane) * 16), (lds_vptr)(tab + c * 4), 16, 0, 0);
+  }
+}
+
 // A missing shard's load gets an out-of-range voffset (the buffer returns 0
 // without touching memory), halving a maximal-erasure vector's load traffic
 // (+0.4 %, profiles/gf16_skip_ab_r05.log).  (8-byte lane-pair loads with a DPP
@@ -721,13 +860,10 @@ template <int K>
 __global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_decode_h_kernel(
     DecodeArgs a) {
   constexpr int NQ = K / 32, LR = K == 512 ? 1 : 2, RPR = K == 512 ? 1 : 2;
-  // dynamic LDS (dec_h_lds_bytes): [0, n x 64 B) the transposes and the
-  // derivative staging (each <= n x 64 B); then n x 80 B of per-element tables
-  // (mul16x_table_to: the premultiply's for present, the postmultiply's for
-  // missing elements)
+  static_assert(2 * K * kTab16x * 4 == 5 * 16 * 2 * K, "five 16-B chunks per thread");
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn_lds[];
   uint32_t* lds = dyn_lds;
-  uint32_t* tab = dyn_lds + 2 * K * 16;
+  uint32_t* tab = dyn_lds + dec_h_tab_off<K>() / 4;
   const long blk = blockIdx.x;
   const int piece = (int)(blk % a.nchunk);  // nchunk = 256-B pieces of the shard
   const long v = blk / a.nchunk;
@@ -743,14 +879,12 @@ __global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   const uint32_t voff = col + (uint32_t)hl * 32u * (uint32_t)a.shard_stride;  // upper half: shard + 32
   const auto rsrc = make_rsrc(a.data + sq * a.sq_stride + vec * a.vec_stride);
   const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
-  const uint16_t* err = (const uint16_t*)(a.err + err_vec(a, v) * rs_err_bytes(K));
-  // thread t builds element t's table
+  const uint8_t* img = a.err + err_vec(a, v) * rs_err_bytes(K) + rs_err_tab_off(K);
+  dec_h_load_tables<K>(tab, img, q, lane);
+  pos_tables_to_lds<K, 2 * K, 0>(lds, q, lane);  // the bit-0 layers' tables into the staging area
   const int my_i = 64 * q + lane;
   const int my_shard = my_i < K ? K + my_i : my_i - K;
-  const bool my_present = pres[(long)my_shard * a.p_shard_stride] != 0;
-  const uint64_t pm = __builtin_amdgcn_ballot_w64(my_present);
-  const uint32_t my_err = err[my_i];
-  mul16x_table_to(tab + threadIdx.x * kTab16x, my_present ? my_err : kMod16 - my_err);
+  const uint64_t pm = __builtin_amdgcn_ballot_w64(pres[(long)my_shard * a.p_shard_stride] != 0);
   W32 w;
   const int q_ld = opaque_s(q);
   const uint32_t pmh_ld = hl ? (uint32_t)(pm >> 32) : (uint32_t)pm;
@@ -764,6 +898,9 @@ __global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     w.lo[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, vj, so, 0);
     w.hi[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, vj + 32u, so, 0);
   }
+  // every wave's table DMA has landed (an explicit vmcnt(0): hipcc's barrier
+  // fence waits only for lgkmcnt here, checked in the ISA) before any wave reads
+  wait_dma();
   __syncthreads();
   H_PROBE(g_probe, 1, NQ - 1);
   const int q_pm = opaque_s(q);
@@ -779,7 +916,7 @@ __global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   }
   H_PROBE(g_probe, 2, NQ - 1);
   // ---- IFFT (ifftDITDecoder, skew index iend - 1) ----
-  layer0_s<true>(w, q, hl);
+  layer0_sl<true>(w, q, hl, lds);
   swap_sb(w);
   H_PROBE(g_probe, 3, NQ - 1);
   layer_b<true, 2>(w, q);
@@ -788,14 +925,16 @@ __global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   layer_b<true, 16>(w, q);
   layer_b<true, 32>(w, q);
   H_PROBE(g_probe, 4, NQ - 1);
-  xpose_bt<LR, RPR>(w, lds, q, lane);
+  __syncthreads();  // every wave's reads of the position tables are done
+  if constexpr (K == 512) xpose_bt_db<LR, RPR, 0>(w, lds, q, lane);  // rounds A B A B
+  else xpose_bt<LR, RPR>(w, lds, q, lane);
   H_PROBE(g_probe, 5, NQ - 1);
   layer_t<true, 64, LR>(w);
   layer_t<true, 128, LR>(w);
   layer_t<true, 256, LR>(w);
   if constexpr (K == 512) layer_t<true, 512, LR>(w);
   H_PROBE(g_probe, 6, NQ - 1);
-  derivative_t<NQ>(w, lds, q, lane, lowmask);
+  derivative_t<NQ, K == 512>(w, lds, q, lane, lowmask);  // A B A B
   H_PROBE(g_probe, 7, NQ - 1);
   // ---- FFT (fftDIT, skew index iend - 1) ----
   if constexpr (K == 512) layer_t<false, 512, LR>(w);
@@ -803,7 +942,16 @@ __global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   layer_t<false, 128, LR>(w);
   layer_t<false, 64, LR>(w);
   H_PROBE(g_probe, 8, NQ - 1);
-  xpose_bt<LR, RPR>(w, lds, q, lane);
+  if constexpr (K == 512) {
+    xpose_bt_db<LR, RPR, 0>(w, lds, q, lane);  // A B A B
+    // every wave's reads of B are done: the tables come back over it while the
+    // B and S layers run (their DMA is waited for at the barrier below)
+    __syncthreads();
+  } else {
+    xpose_bt<LR, RPR>(w, lds, q, lane);
+  }
+  if constexpr (K == 512) dec_h_load_tables<K>(tab, img, q, lane);  // (K = 256: never overwritten)
+  pos_tables_to_lds<K, 2 * K, 0>(lds, q, lane);
   H_PROBE(g_probe, 9, NQ - 1);
   layer_b<false, 32>(w, q);
   layer_b<false, 16>(w, q);
@@ -812,7 +960,9 @@ __global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   layer_b<false, 2>(w, q);
   H_PROBE(g_probe, 10, NQ - 1);
   swap_sb(w);
-  layer0_s<false>(w, q, hl);
+  wait_dma();  // the tables' DMA has landed in every wave before any reads them
+  __syncthreads();
+  layer0_sl<false>(w, q, hl, lds);
   H_PROBE(g_probe, 11, NQ - 1);
   // erased shards = work * (65535 - errLocs), per lane; a register whose two
   // elements are both given is skipped (wave-uniform)
@@ -842,6 +992,331 @@ __global__ __launch_bounds__(2 * K) __attribute__((amdgpu_waves_per_eu(4, 4))) v
 }
 
 // ---------------------------------------------------------------------------
+// k = 512 decoder, round 6 (leo16_decode_q_kernel): QUARTER lanes, so that two
+// workgroups share a CU and one's barrier waits, loads and stores overlap the
+// other's butterflies (leo16_decode_h_kernel's 1,024 threads own a CU alone;
+// verdict r05: 0.59 VALU instructions per clock per CU, 37 % of wave cycles
+// waiting).  A lane quarter (16 lanes) holds 128 B of a shard -- lane l: quarter
+// ql = l >> 4, 64-B block (l >> 3) & 1, symbols 4 (l & 7) .. +3 -- and every
+// register four elements, one per quarter: 8 waves x 32 registers x 4 quarters
+// = the n = 1024 elements of one 128-B piece in 64 data VGPRs at <= 128 VGPRs,
+// 512 threads and 64 KiB of LDS per workgroup.  Layouts (q = wave, j = register):
+//   S  e = (j >> 3) + 4 (j & 7) + 32 ql + 128 q   loads, stores, pre/post
+//                                                 multiplies, layers on bits 0, 1
+//   B  e = ql + 4 j + 128 q                        layers on bits 2-6
+//   T  e = ql + 4 (j & 3) + 16 q + 128 (j >> 2)    layers on bits 7-9, derivative
+// S <-> B: a 4 x 4 transpose of (j >> 3, ql) per register group j & 7
+// (v_permlane32_swap, then v_permlane16_swap); B <-> T: xpose_bt_db (LR = 2,
+// NQ = 8 waves).  In S the quarters of a register are different butterflies,
+// so the bit-0 and bit-1 layers read per-lane tables, from LDS images each
+// wave fills for its own positions (pos_tables_wave-style).  The erasure
+// multiplies read the head's per-element table image (leo16_errlocs_fold_kernel)
+// per lane from L2.  Host emulation of the layouts: tests/test_quarterlane_emu.py.
+// ---------------------------------------------------------------------------
+using WQ = W16n<32>;
+
+__device__ __forceinline__ constexpr int q_elem_s(int j, int ql) { return (j >> 3) + 4 * (j & 7) + 32 * ql; }
+
+// S <-> B (its own inverse): per register group g, registers g, g+8, g+16, g+24
+__device__ __forceinline__ void swap_sb_q(WQ& w) {
+#pragma unroll
+  for (int g = 0; g < 8; g++) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      uint32_t* v = h ? w.hi : w.lo;
+      const auto a = __builtin_amdgcn_permlane32_swap(v[g], v[g + 16], false, false);
+      const auto b = __builtin_amdgcn_permlane32_swap(v[g + 8], v[g + 24], false, false);
+      const auto c = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
+      const auto d = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
+      v[g] = c[0];
+      v[g + 8] = c[1];
+      v[g + 16] = d[0];
+      v[g + 24] = d[1];
+    }
+  }
+}
+
+// A table from a per-lane byte offset into an LDS image
+__device__ __forceinline__ void lds_tab(const uint32_t* img, uint32_t byte_off, uint32_t (&t)[kTab16x]) {
+  const uint4* p = (const uint4*)((const uint8_t*)img + byte_off);
+#pragma unroll
+  for (int h = 0; h < kTab16x / 4; h++) {
+    const uint4 v = p[h];
+    t[4 * h] = v.x;
+    t[4 * h + 1] = v.y;
+    t[4 * h + 2] = v.z;
+    t[4 * h + 3] = v.w;
+  }
+}
+
+// Layer on element bit b (0 or 1) in S: x = register j, y = j + 8 (b = 0) /
+// j + 16 (b = 1).  Position (e & ~(2d - 1)) + d - 1 per lane; the wave's images:
+// bit 0 at img0 + (e(x) - 128 q) / 2 * 80, bit 1 at img1 + (e(x) - 128 q) / 4 * 80.
+template <bool INV, int B>
+__device__ __forceinline__ void layer_s_q(WQ& w, int ql, const uint32_t* img) {
+  constexpr int RD = 8 << B;  // register distance of the pair
+#pragma unroll
+  for (int j = 0; j < 32; j++) {
+    if ((j >> 3) & (1 << B)) continue;
+    const int le = q_elem_s(j, 0) + 32 * ql;  // e(x) - 128 q
+    uint32_t t[kTab16x];
+    lds_tab(img, (uint32_t)opaque_v((le >> (B + 1)) * (kTab16x * 4), w.lo[j > 0 ? j - 1 : 0]), t);
+    if constexpr (INV) {
+      w.lo[j + RD] ^= w.lo[j];
+      w.hi[j + RD] ^= w.hi[j];
+      mul16x_add_t(w.lo[j], w.hi[j], w.lo[j + RD], w.hi[j + RD], t);
+    } else {
+      mul16x_add_t(w.lo[j], w.hi[j], w.lo[j + RD], w.hi[j + RD], t);
+      w.lo[j + RD] ^= w.lo[j];
+      w.hi[j + RD] ^= w.hi[j];
+    }
+    asm volatile("" : "+v"(w.lo[j]), "+v"(w.hi[j]), "+v"(w.lo[j + RD]), "+v"(w.hi[j + RD]));
+  }
+}
+
+// Layer on element bit b in 2..6 in B: registers j, j + 2^(b-2); position
+// 128 q + 4 jb + d - 1 for the register block jb (wave-uniform, scalar tables)
+template <bool INV, int B>
+__device__ __forceinline__ void layer_b_q(WQ& w, int q) {
+  constexpr int RD = 1 << (B - 2), D = 1 << B;
+#pragma unroll
+  for (int jb = 0; jb < 32; jb += 2 * RD) {
+    const int pos = opaque_tok(128 * q + 4 * jb + D - 1, w.lo[jb]);
+#pragma unroll
+    for (int j = jb; j < jb + RD; j++) {
+      if constexpr (INV) ifft2_16(w, j, j + RD, pos);
+      else fft2_16(w, j, j + RD, pos);
+      pin_pair(w, j, j + RD);
+    }
+  }
+}
+
+// Layer on element bit b in 7..9 in T: registers j, j + 4 * 2^(b-7);
+// compile-time positions 128 (jb >> 2) + d - 1; block start 0 is a zero skew
+template <bool INV, int B>
+__device__ __forceinline__ void layer_t_q(WQ& w) {
+  constexpr int RD = 4 << (B - 7), D = 1 << B;
+#pragma unroll
+  for (int jb = 0; jb < 32; jb += 2 * RD) {
+    const bool zero = jb == 0;
+    const int pos = zero ? 0 : opaque_tok(128 * (jb >> 2) + D - 1, w.lo[jb]);
+#pragma unroll
+    for (int j = jb; j < 32; j++) {
+      if ((j & ~(2 * RD - 1)) != jb || (j & RD)) continue;
+      if (zero) {
+        w.lo[j + RD] ^= w.lo[j];
+        w.hi[j + RD] ^= w.hi[j];
+      } else if constexpr (INV) {
+        ifft2_16(w, j, j + RD, pos);
+      } else {
+        fft2_16(w, j, j + RD, pos);
+      }
+      pin_pair(w, j, j + RD);
+    }
+  }
+}
+
+// Formal derivative in T: register bits (element bits 2, 3, 7-9) in place in
+// ascending register order; wave bits (4-6) and quarter bits (0: lane ^ 16,
+// 1: lane ^ 32) from the originals staged in LDS, 8 registers per round in two
+// alternating 32-KiB buffers (no barrier after a round's reads).
+__device__ __forceinline__ void derivative_tq(WQ& w, uint32_t* lds0, int c, int lane) {
+  constexpr int B = 8, RW = 8 * B * 2 * 64;
+  const uint32_t m16 = ((lane >> 4) & 1) ? 0u : 0xFFFFFFFFu, m32 = ((lane >> 5) & 1) ? 0u : 0xFFFFFFFFu;
+#pragma unroll
+  for (int s0 = 0; s0 < 32; s0 += B) {
+    uint32_t* lds = lds0 + ((s0 / B) & 1) * RW;
+#pragma unroll
+    for (int u = 0; u < B; u++) {
+      lds[((c * B + u) * 2) * 64 + lane] = w.lo[s0 + u];
+      lds[((c * B + u) * 2 + 1) * 64 + lane] = w.hi[s0 + u];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < B; u++) {
+      const int j = s0 + u;
+      uint32_t alo = w.lo[j], ahi = w.hi[j];
+#pragma unroll
+      for (int bit = 1; bit < 32; bit <<= 1)
+        if ((j & bit) == 0) {
+          alo ^= w.lo[j | bit];
+          ahi ^= w.hi[j | bit];
+        }
+#pragma unroll
+      for (int wb = 1; wb < 8; wb <<= 1)
+        if ((c & wb) == 0) {
+          alo ^= lds[(((c | wb) * B + u) * 2) * 64 + lane];
+          ahi ^= lds[(((c | wb) * B + u) * 2 + 1) * 64 + lane];
+        }
+      const uint32_t* me = lds + ((c * B + u) * 2) * 64;
+      alo ^= (me[lane ^ 16] & m16) ^ (me[lane ^ 32] & m32);
+      ahi ^= (me[64 + (lane ^ 16)] & m16) ^ (me[64 + (lane ^ 32)] & m32);
+      asm volatile("" : "+v"(alo), "+v"(ahi));
+      w.lo[j] = alo;
+      w.hi[j] = ahi;
+    }
+  }
+}
+
+// The wave's S-layer tables into its LDS images: bit 0, the 64 even positions
+// 128 q + 2 i, at img0 = lds + q * 64 * 80 B; bit 1, the 32 positions
+// 128 q + 4 i + 1, at img1 = lds + 40 KiB + q * 32 * 80 B (global_load_lds,
+// 16-B chunks lane-linear; the wave waits for its own DMA before reading).
+__device__ __forceinline__ void q_pos_tables(uint32_t* lds, int q, int lane) {
+  const uint8_t* src = (const uint8_t*)(const void*)g_ptab16x;
+  asm volatile("" : "+v"(lane));  // the two calls' addresses are not kept live in between
+  uint32_t* img0 = lds + q * 64 * kTab16x;
+  uint32_t* img1 = lds + 40 * 1024 / 4 + q * 32 * kTab16x;
+#pragma unroll
+  for (int i = 0; i < 5; i++) {  // 320 chunks
+    const int c = 64 * i + lane;
+    const uint8_t* g = src + (long)(128 * q + 2 * (c / 5)) * (kTab16x * 4) + (c % 5) * 16;
+    __builtin_amdgcn_global_load_lds((glb_vptr)g, (lds_vptr)(img0 + 64 * i * 4), 16, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < 3; i++) {  // 160 chunks
+    const int c = 64 * i + lane;
+    if (i < 2 || lane < 32) {
+      const uint8_t* g = src + (long)(128 * q + 4 * (c / 5) + 1) * (kTab16x * 4) + (c % 5) * 16;
+      __builtin_amdgcn_global_load_lds((glb_vptr)g, (lds_vptr)(img1 + 64 * i * 4), 16, 0, 0);
+    }
+  }
+}
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_decode_q_kernel(
+    DecodeArgs a) {
+  constexpr int K = 512;
+  // two 32-KiB rounds of the transposes / derivative; the S-layer images
+  // (60 KiB) in the same space before the first transpose and after the last
+  __shared__ __attribute__((aligned(16))) uint32_t lds[16384];
+  const uint32_t* img0_base = lds;
+  const uint32_t* img1_base = lds + 40 * 1024 / 4;
+  const long blk = blockIdx.x;
+  const int piece = (int)(blk % a.nchunk);  // nchunk = 128-B pieces of the shard
+  const long v = blk / a.nchunk;
+  if (a.flags[v] == 0) return;  // uniform
+  const long sq = v / a.nvec, vec = v % a.nvec;
+  const int lane = threadIdx.x & 63;
+  const int ql = lane >> 4;
+  const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  q_pos_tables(lds, q, lane);
+  const uint32_t col = (uint32_t)piece * 128u + (uint32_t)((lane >> 3) & 1) * 64u + (uint32_t)(lane & 7) * 4u;
+  const uint32_t voff = col + (uint32_t)ql * 32u * (uint32_t)a.shard_stride;  // quarter ql: shard + 32 ql
+  const auto rsrc = make_rsrc(a.data + sq * a.sq_stride + vec * a.vec_stride);
+  const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
+  const auto trs = make_rsrc(a.err + err_vec(a, v) * rs_err_bytes(K) + rs_err_tab_off(K));
+  // presence of the wave's 128 elements, li = e - 128 q = 32 ql + m(j) with
+  // m(j) = q_elem_s(j, 0) < 32: the lane's 32 registers are bits 32 ql .. +31
+  // (pw, per lane), and allq bit m = all four quarters of register m present
+  const int e0 = 128 * q + lane, e1 = e0 + 64;
+  const uint64_t pm0 = __builtin_amdgcn_ballot_w64(pres[(long)(e0 < K ? K + e0 : e0 - K) * a.p_shard_stride] != 0);
+  const uint64_t pm1 = __builtin_amdgcn_ballot_w64(pres[(long)(e1 < K ? K + e1 : e1 - K) * a.p_shard_stride] != 0);
+  const uint32_t pw0 = (uint32_t)pm0, pw1 = (uint32_t)(pm0 >> 32), pw2 = (uint32_t)pm1, pw3 = (uint32_t)(pm1 >> 32);
+  const uint32_t pw = ql == 0 ? pw0 : ql == 1 ? pw1 : ql == 2 ? pw2 : pw3;
+  uint32_t allq = pw0 & pw1 & pw2 & pw3;
+  WQ w;
+  const int q_ld = opaque_s(q);
+#pragma unroll
+  for (int j = 0; j < 32; j++) {
+    const int i = 128 * q_ld + q_elem_s(j, 0);  // quarter 0's element
+    const int shard = i < K ? K + i : i - K;
+    const uint32_t so = (uint32_t)shard * (uint32_t)a.shard_stride;
+    const uint32_t vj = ((pw >> q_elem_s(j, 0)) & 1) ? voff : (voff | 0x80000000u);
+    w.lo[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, vj, so, 0);
+    w.hi[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, vj + 32u, so, 0);
+  }
+  // premultiply: every element by its table (present: exp(errLoc); a missing
+  // element's bytes are zero, so its postmultiply table leaves them zero)
+  const int q_pm = opaque_s(q);
+#pragma unroll
+  for (int j = 0; j < 32; j++) {
+    const uint32_t e = (uint32_t)(128 * q_pm + q_elem_s(j, ql));
+    uint32_t t[kTab16x];
+    {
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+      for (int h = 0; h < kTab16x / 4; h++) {
+        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(trs, e * (kTab16x * 4) + 16u * h, 0, 0);
+        t[4 * h] = x.x;
+        t[4 * h + 1] = x.y;
+        t[4 * h + 2] = x.z;
+        t[4 * h + 3] = x.w;
+      }
+    }
+    uint32_t xl = w.lo[j], xh = w.hi[j];
+    mul16x_by(xl, xh, t);
+    asm volatile("" : "+v"(xl), "+v"(xh));
+    w.lo[j] = xl;
+    w.hi[j] = xh;
+  }
+  // ---- IFFT (ifftDITDecoder, skew index iend - 1) ----
+  wait_dma();
+  layer_s_q<true, 0>(w, ql, img0_base + q * 64 * kTab16x);
+  layer_s_q<true, 1>(w, ql, img1_base + q * 32 * kTab16x);
+  swap_sb_q(w);
+  layer_b_q<true, 2>(w, q);
+  layer_b_q<true, 3>(w, q);
+  layer_b_q<true, 4>(w, q);
+  layer_b_q<true, 5>(w, q);
+  layer_b_q<true, 6>(w, q);
+  __syncthreads();  // every wave's reads of its S-layer images are done
+  xpose_bt_db<2, 2, 0>(w, lds, q, lane);  // rounds A B A B
+  layer_t_q<true, 7>(w);
+  layer_t_q<true, 8>(w);
+  layer_t_q<true, 9>(w);
+  derivative_tq(w, lds, q, lane);  // A B A B
+  // ---- FFT (fftDIT, skew index iend - 1) ----
+  layer_t_q<false, 9>(w);
+  layer_t_q<false, 8>(w);
+  layer_t_q<false, 7>(w);
+  xpose_bt_db<2, 2, 0>(w, lds, q, lane);  // A B A B
+  __syncthreads();  // every wave's reads of B are done: the images come back over it
+  q_pos_tables(lds, q, lane);
+  layer_b_q<false, 6>(w, q);
+  layer_b_q<false, 5>(w, q);
+  layer_b_q<false, 4>(w, q);
+  layer_b_q<false, 3>(w, q);
+  layer_b_q<false, 2>(w, q);
+  swap_sb_q(w);
+  wait_dma();
+  layer_s_q<false, 1>(w, ql, img1_base + q * 32 * kTab16x);
+  layer_s_q<false, 0>(w, ql, img0_base + q * 64 * kTab16x);
+  // erased shards = work * (65535 - errLocs): the stored table of a missing
+  // element; a register whose four elements are all given is skipped (uniform)
+  const int q_e = opaque_s(q);
+  asm volatile("" : "+s"(allq));
+#pragma unroll
+  for (int j = 0; j < 32; j++) {
+    const int l0 = q_elem_s(j, 0);
+    if ((allq >> l0) & 1) continue;  // uniform
+    const uint32_t e = (uint32_t)(128 * q_e + q_elem_s(j, ql));
+    uint32_t t[kTab16x];
+    {
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+      for (int h = 0; h < kTab16x / 4; h++) {
+        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(trs, e * (kTab16x * 4) + 16u * h, 0, 0);
+        t[4 * h] = x.x;
+        t[4 * h + 1] = x.y;
+        t[4 * h + 2] = x.z;
+        t[4 * h + 3] = x.w;
+      }
+    }
+    uint32_t xl = w.lo[j], xh = w.hi[j];
+    mul16x_by(xl, xh, t);
+    asm volatile("" : "+v"(xl), "+v"(xh));
+    const int i = 128 * q_e + l0;
+    const int shard = i < K ? K + i : i - K;
+    const uint32_t so = (uint32_t)shard * (uint32_t)a.shard_stride;
+    if (!((pw >> l0) & 1)) {
+      __builtin_amdgcn_raw_buffer_store_b32(xl, rsrc, voff, so, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(xh, rsrc, voff + 32u, so, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k = 512 encoder, round 5 (leo16_encode_h_kernel): the half-lane layouts of
 // leo16_decode_h_kernel over m = 512 elements -- 8 waves (512 threads) x 32
 // register pairs x 2 halves, 64 data VGPRs within the 128 of 4 waves per SIMD
@@ -860,7 +1335,11 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
     EncodeArgs a) {
   constexpr int IO = REV ? 0 : M, FO = REV ? M : 0;
   constexpr int LR = M == 512 ? 2 : 3, RPR = M == 512 ? 2 : 8;
-  __shared__ __attribute__((aligned(16))) uint32_t lds[8 * 8 * 2 * 64];  // 32 KiB per transpose round
+  // M = 512: two 32-KiB transpose rounds (xpose_bt_db, round 6: 8 -> 4
+  // barriers per transpose), 64 KiB, so two workgroups still share a CU;
+  // M = 256 keeps one (32 KiB: four workgroups per CU)
+  constexpr bool DB = M == 512;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[(DB ? 2 : 1) * 8 * 8 * 2 * 64];
   const long blk = blockIdx.x;
   const int piece = (int)(blk % a.nchunk);  // nchunk = 256-B pieces of the shard
   const long sv = blk / a.nchunk;
@@ -873,6 +1352,7 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
   const uint32_t col = (uint32_t)piece * 256u + (uint32_t)((lane & 31) >> 3) * 64u + (uint32_t)(lane & 7) * 4u;
   const bool active = col < (uint32_t)a.shard_bytes;
   H_PROBE(g_probe_e, 0, M / 64 - 1);
+  pos_tables_wave<IO>(lds, q, lane);  // this wave's IFFT bit-0 tables (round 6)
   const uint32_t cl = active ? col : 0u;  // inactive lanes read valid memory, store nothing
   W32 w;
   {
@@ -901,7 +1381,8 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
   const uint64_t given = a.out_present ? __builtin_amdgcn_ballot_w64(fill_given(a, sq, vec, 64 * q + lane)) : 0ull;
   H_PROBE(g_probe_e, 1, M / 64 - 1);
   // ---- IFFT (ifftDITEncoder, skew index IO - 1 + iend) ----
-  layer0_s<true, IO>(w, q, hl);
+  wait_dma();
+  layer0_sl<true>(w, q, hl, lds);
   swap_sb(w);
   H_PROBE(g_probe_e, 2, M / 64 - 1);
   layer_b<true, 2, IO>(w, q);
@@ -910,7 +1391,9 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
   layer_b<true, 16, IO>(w, q);
   layer_b<true, 32, IO>(w, q);
   H_PROBE(g_probe_e, 3, M / 64 - 1);
-  xpose_bt<LR, RPR>(w, lds, q, lane);
+  __syncthreads();  // every wave's reads of its bit-0 tables are done before the staging is rewritten
+  if constexpr (DB) xpose_bt_db<LR, RPR, 0>(w, lds, q, lane);  // rounds A B A B
+  else xpose_bt<LR, RPR>(w, lds, q, lane);
   H_PROBE(g_probe_e, 4, M / 64 - 1);
   layer_t<true, 64, LR, IO>(w);
   if constexpr (M == 512) layer_t<true, 128, LR, IO>(w);
@@ -925,7 +1408,11 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
   if constexpr (M == 512) layer_t<false, 128, LR, FO>(w);
   layer_t<false, 64, LR, FO>(w);
   H_PROBE(g_probe_e, 5, M / 64 - 1);
-  xpose_bt<LR, RPR>(w, lds, q, lane);
+  if constexpr (DB) xpose_bt_db<LR, RPR, 0>(w, lds, q, lane);  // A B A B
+  else xpose_bt<LR, RPR>(w, lds, q, lane);                      // (ends with a barrier)
+  // the FFT bit-0 tables into A (DB: its last reads, round 2's, precede round
+  // 3's barrier), landing while the B layers run
+  pos_tables_wave<FO>(lds, q, lane);
   H_PROBE(g_probe_e, 6, M / 64 - 1);
   layer_b<false, 32, FO>(w, q);
   layer_b<false, 16, FO>(w, q);
@@ -934,7 +1421,8 @@ __global__ __launch_bounds__(M) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
   layer_b<false, 2, FO>(w, q);
   H_PROBE(g_probe_e, 7, M / 64 - 1);
   swap_sb(w);
-  layer0_s<false, FO>(w, q, hl);
+  wait_dma();
+  layer0_sl<false>(w, q, hl, lds);
   H_PROBE(g_probe_e, 8, M / 64 - 1);
   if (!active) return;
   // ---- store: compare (prerepairSanityCheck), Repair fill, or plain ----
@@ -1118,8 +1606,14 @@ hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mar
     DecodeArgs b = a;
     b.nchunk = a.shard_bytes / 256;
     const long grid = nv * b.nchunk;
-    if (a.k == 512)
+    if (a.k == 512) {
+#ifndef DAGPU_DEC512_HALF  // (A/B builds: the half-lane k = 512 decoder)
+      b.nchunk = a.shard_bytes / 128;  // quarter-lane decoder, 128-B pieces, two workgroups per CU
+      hipLaunchKernelGGL(leo16_decode_q_kernel, dim3((unsigned)(nv * b.nchunk)), dim3(512), 0, s, b);
+#else
       hipLaunchKernelGGL((leo16_decode_h_kernel<512>), dim3((unsigned)grid), dim3(1024), dec_h_lds_bytes<512>(), s, b);
+#endif
+    }
     else
       hipLaunchKernelGGL((leo16_decode_h_kernel<256>), dim3((unsigned)grid), dim3(512), dec_h_lds_bytes<256>(), s, b);
   } else {  // shard sizes off the 256-B grid (codec API): the generic LDS decoder

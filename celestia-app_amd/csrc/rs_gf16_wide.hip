@@ -129,6 +129,49 @@ __device__ __forceinline__ void elem_tab(const WideTabs& T, uint32_t lm, uint32_
   quad(pb[14], pb[15], t[18], t[19]);
 }
 
+// The same table from the element's 16 basis products (1 << b) * exp(lm), as
+// leo16w_errlocs_kernel stores them (round 6: two 16-B loads, no gathers).
+__device__ __forceinline__ void elem_tab_pb(const uint8_t* pb32, uint32_t (&t)[kTabW]) {
+  const uint4 u0 = ((const uint4*)pb32)[0], u1 = ((const uint4*)pb32)[1];
+  const uint32_t w[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+  uint32_t pb[16];
+#pragma unroll
+  for (int b = 0; b < 16; b++) pb[b] = (w[b >> 1] >> (16 * (b & 1))) & 0xFFFFu;
+  auto quad = [&](uint32_t p0, uint32_t p1, uint32_t& lo, uint32_t& hi) {
+    const uint32_t q = p0 ^ p1;
+    lo = __builtin_amdgcn_perm(q, __builtin_amdgcn_perm(p1, p0, 0x0C04000Cu), 0x04020100u);
+    hi = __builtin_amdgcn_perm(q, __builtin_amdgcn_perm(p1, p0, 0x0C05010Cu), 0x05020100u);
+  };
+  auto grp3 = [&](int b0, int base) {
+    uint32_t lo, hi;
+    quad(pb[b0], pb[b0 + 1], lo, hi);
+    t[base] = lo;
+    t[base + 1] = lo ^ __builtin_amdgcn_perm(pb[b0 + 2], pb[b0 + 2], 0x00000000u);
+    t[base + 2] = hi;
+    t[base + 3] = hi ^ __builtin_amdgcn_perm(pb[b0 + 2], pb[b0 + 2], 0x01010101u);
+  };
+  grp3(0, 0);
+  grp3(3, 4);
+  quad(pb[6], pb[7], t[8], t[9]);
+  grp3(8, 10);
+  grp3(11, 14);
+  quad(pb[14], pb[15], t[18], t[19]);
+}
+
+// (lo, hi) *= the element's factor through its table from the basis products
+template <int NG>
+__device__ __forceinline__ void mul_elem_pb(const uint8_t* pb32, uint32_t (&lo)[NG], uint32_t (&hi)[NG]) {
+  uint32_t t[kTabW];
+  elem_tab_pb(pb32, t);
+#pragma unroll
+  for (int g = 0; g < NG; g++) {
+    uint32_t rl = 0, rh = 0;
+    pmul_add(rl, rh, lo[g], hi[g], t);
+    lo[g] = rl;
+    hi[g] = rh;
+  }
+}
+
 // mulLog on one 16-bit symbol (leopard.go mulLog): a * exp(lm), 0 stays 0
 __device__ __forceinline__ uint32_t mul_log(const WideTabs& T, uint32_t a, uint32_t lm) {
   if (a == 0) return 0;
@@ -171,10 +214,11 @@ __device__ __forceinline__ void mul_elem(const WideTabs& T, uint32_t (&lo)[NG], 
 }
 
 // LDS planes: lo[e * NGP + g], hi[...] (NG = S / 4 dword groups, NGP = NG + 1
-// for odd element strides, so lanes on different elements spread over banks)
+// for odd element strides, so lanes on different elements spread over banks;
+// NG = 2 is used only at n = 8192, where a pad dword would not fit 160 KiB)
 template <int NG>
 struct Planes {
-  static constexpr int NGP = NG == 1 ? 1 : NG + 1;
+  static constexpr int NGP = NG <= 2 ? NG : NG + 1;
   uint32_t* lo;
   uint32_t* hi;
   __device__ __forceinline__ int at(int e, int g) const { return e * NGP + g; }
@@ -489,10 +533,12 @@ __global__ __launch_bounds__(kFoldThreads) void leo16w_errlocs_kernel(DecodeArgs
   if (threadIdx.x == 0) cnt_s = 0;
   __syncthreads();
   int cnt = 0;
-  for (int i = threadIdx.x; i < n; i += kFoldThreads) {
+  uint32_t miss = 0;  // bit r: element threadIdx.x + r * kFoldThreads is missing (n <= 32 * kFoldThreads)
+  for (int i = threadIdx.x, r = 0; i < n; i += kFoldThreads, r++) {
     const uint32_t x = i < k ? (pres[(long)(k + i) * a.p_shard_stride] ? 0u : 1u)   // parity k+i -> work i
                              : (pres[(long)(i - k) * a.p_shard_stride] ? 0u : 1u);  // data i-k -> work i
     e[i] = x;
+    miss |= x << r;
     cnt += (x == 0);
   }
   atomicAdd(&cnt_s, cnt);
@@ -517,6 +563,28 @@ __global__ __launch_bounds__(kFoldThreads) void leo16w_errlocs_kernel(DecodeArgs
   fwht_rt(e, n);
   uint16_t* out = (uint16_t*)(a.err + hv * (long)rs_err_bytes(k));
   for (int i = threadIdx.x; i < n; i += kFoldThreads) out[i] = (uint16_t)e[i];
+  // Round 6: each element's 16 basis products (1 << b) * exp(+-errLoc) -- the
+  // premultiply's factor for a present element, the postmultiply's for a missing
+  // one -- once per erasure pattern, so the decoder's workgroups (one per
+  // column slice) build their tables from two coalesced 16-B loads instead of
+  // 16 random exp gathers per element each.
+  if (a.k >= 1024) {
+    uint4* pbo = (uint4*)(a.err + hv * (long)rs_err_bytes(k) + rs_err_tab_off(k));
+    for (int i = threadIdx.x, r = 0; i < n; i += kFoldThreads, r++) {
+      const uint32_t lm0 = e[i] & 0xFFFFu;
+      const uint32_t lm = ((miss >> r) & 1) ? kMod - lm0 : lm0;
+      uint32_t p[8];
+#pragma unroll
+      for (int b = 0; b < 16; b += 2) {
+        uint32_t s0 = (uint32_t)T.log[1u << b] + lm, s1 = (uint32_t)T.log[1u << (b + 1)] + lm;
+        s0 = (s0 + (s0 >> 16)) & 0xFFFFu;
+        s1 = (s1 + (s1 >> 16)) & 0xFFFFu;
+        p[b / 2] = (uint32_t)T.exp[s0] | ((uint32_t)T.exp[s1] << 16);
+      }
+      pbo[2 * i] = make_uint4(p[0], p[1], p[2], p[3]);
+      pbo[2 * i + 1] = make_uint4(p[4], p[5], p[6], p[7]);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -542,6 +610,9 @@ __global__ __launch_bounds__(kWideThreads) void leo16w_decode_kernel(DecodeArgs 
   uint8_t* base = a.data + sq * a.sq_stride + vec * a.vec_stride + col;
   const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
   const uint16_t* err = (const uint16_t*)(a.err + err_vec(a, v) * (long)rs_err_bytes(k));
+  // k >= 1024: the basis products leo16w_errlocs_kernel stored per element;
+  // k = 256 / 512 (DAGPU_GF16_WIDE A/B) has the register kernels' tables there
+  const uint8_t* pbase = k >= 1024 ? (const uint8_t*)err + rs_err_tab_off(k) : nullptr;
   // one thread per element: its table once, then its NG dword pairs
   for (int i = threadIdx.x; i < n; i += kWideThreads) {
     const long shard = i < k ? k + i : i - k;
@@ -553,7 +624,8 @@ __global__ __launch_bounds__(kWideThreads) void leo16w_decode_kernel(DecodeArgs 
         lo[g] = src[g];
         hi[g] = src[8 + g];
       }
-      mul_elem<NG>(T, lo, hi, err[i]);
+      if (pbase) mul_elem_pb<NG>(pbase + (long)i * 32, lo, hi);
+      else mul_elem<NG>(T, lo, hi, err[i]);
 #pragma unroll
       for (int g = 0; g < NG; g++) {
         P.lo[P.at(i, g)] = lo[g];
@@ -612,7 +684,8 @@ __global__ __launch_bounds__(kWideThreads) void leo16w_decode_kernel(DecodeArgs 
       lo[g] = P.lo[P.at(i, g)];
       hi[g] = P.hi[P.at(i, g)];
     }
-    mul_elem<NG>(T, lo, hi, kMod - err[i]);
+    if (pbase) mul_elem_pb<NG>(pbase + (long)i * 32, lo, hi);  // (the stored factor is the postmultiply's)
+    else mul_elem<NG>(T, lo, hi, kMod - err[i]);
     uint32_t* dst = (uint32_t*)(base + shard * a.shard_stride);
 #pragma unroll
     for (int g = 0; g < NG; g++) {
@@ -699,11 +772,18 @@ hipError_t tables(WideTabs& out) {
   return hipSuccess;
 }
 
-// Slice width per element count: S = 4 NG symbols, LDS = 2 planes x n x (NG + 1)
-// dwords <= 144 KiB (n <= 2048: 32 symbols; 4096: 8; 8192: 4 (64 KiB); 16384: 4 (128 KiB)).
-int slice_ng(int n) { return n <= 2048 ? 8 : n <= 4096 ? 2 : 1; }
+// Slice width per element count: S = 4 NG symbols, LDS = 2 planes x n x NGP
+// dwords <= 160 KiB.  Round 6: the widest slice that fits (n <= 2048: 32
+// symbols, 144 KiB; 4096: 16, 160 KiB; 8192: 8 without the pad dword, 128 KiB;
+// 16384: 4, 128 KiB), so that every skew table a unit loads, every
+// per-element errLocs table and every 64-B block's load serve more symbols
+// (round 5: 8 / 4 symbols at n = 4096 / 8192; profiles/gf16_wide_ab_r06.log).
+int slice_ng(int n) { return n <= 2048 ? 8 : n <= 4096 ? 4 : n <= 8192 ? 2 : 1; }
 
-size_t lds_bytes(int n, int ng) { return (size_t)2 * n * (ng == 1 ? 1 : ng + 1) * sizeof(uint32_t); }
+size_t lds_bytes(int n, int ng) {
+  const int ngp = ng <= 2 ? ng : ng + 1;  // Planes<NG>::NGP
+  return (size_t)2 * n * ngp * sizeof(uint32_t);
+}
 
 template <class K>
 hipError_t lds_attr(K kernel, size_t bytes) {
@@ -735,6 +815,12 @@ hipError_t launch_dec(const DecodeArgs& a, const WideTabs& T, hipStream_t s) {
   return hipGetLastError();
 }
 
+// dword groups per radix-4 unit at 32-symbol slices: the decoder 8 (round 6:
+// one unit per column of a slice, so a skew table serves 8 groups; k = 1024
+// Repair 74.9 -> 81-82 squares/s), the encoder 4 (at 8 it held 136 VGPRs and
+// the k = 1024 split square went 5.0 -> 7.2 ms; profiles/gf16_wide_ab_r06.log)
+constexpr int WG8 = 8, WG8E = 4;
+
 bool wide_k_ok(int k) { return k >= 256 && k <= kMaxK && (k & (k - 1)) == 0; }
 
 }  // namespace
@@ -744,11 +830,13 @@ hipError_t leo16w_prepare() {
   hipError_t e = tables(T);
   // LDS attributes of every instantiation (hipFuncSetAttribute at launch time otherwise)
   const size_t big = 2 * 16384 * 4;  // <= the largest slice any width asks for
-  if (e == hipSuccess) e = lds_attr(leo16w_encode_kernel<8, 4>, lds_bytes(2048, 8));
-  if (e == hipSuccess) e = lds_attr(leo16w_encode_kernel<2, 2>, lds_bytes(4096, 2));
+  if (e == hipSuccess) e = lds_attr(leo16w_encode_kernel<8, WG8E>, lds_bytes(2048, 8));
+  if (e == hipSuccess) e = lds_attr(leo16w_encode_kernel<4, 4>, lds_bytes(4096, 4));
+  if (e == hipSuccess) e = lds_attr(leo16w_encode_kernel<2, 2>, lds_bytes(8192, 2));
   if (e == hipSuccess) e = lds_attr(leo16w_encode_kernel<1, 1>, big);
-  if (e == hipSuccess) e = lds_attr(leo16w_decode_kernel<8, 4>, lds_bytes(2048, 8));
-  if (e == hipSuccess) e = lds_attr(leo16w_decode_kernel<2, 2>, lds_bytes(4096, 2));
+  if (e == hipSuccess) e = lds_attr(leo16w_decode_kernel<8, WG8>, lds_bytes(2048, 8));
+  if (e == hipSuccess) e = lds_attr(leo16w_decode_kernel<4, 4>, lds_bytes(4096, 4));
+  if (e == hipSuccess) e = lds_attr(leo16w_decode_kernel<2, 2>, lds_bytes(8192, 2));
   if (e == hipSuccess) e = lds_attr(leo16w_decode_kernel<1, 1>, big);
   if (e == hipSuccess) e = lds_attr(leo16w_errlocs_kernel, (size_t)4 * 2 * kMaxK);
   return e;
@@ -761,7 +849,8 @@ hipError_t launch_leo16w_encode(int k, const EncodeArgs& a, hipStream_t s) {
   hipError_t e = tables(T);
   if (e != hipSuccess) return e;
   switch (slice_ng(k)) {
-    case 8: return launch_enc<8, 4>(a, T, k, s);
+    case 8: return launch_enc<8, WG8E>(a, T, k, s);
+    case 4: return launch_enc<4, 4>(a, T, k, s);
     case 2: return launch_enc<2, 2>(a, T, k, s);
     default: return launch_enc<1, 1>(a, T, k, s);
   }
@@ -789,7 +878,8 @@ hipError_t launch_leo16w_decode_only(const DecodeArgs& a, hipStream_t s, bool ma
   const long nv = a.nsq * a.nvec;
   if (nv <= 0) return hipSuccess;
   switch (slice_ng(2 * a.k)) {
-    case 8: e = launch_dec<8, 4>(a, T, s); break;
+    case 8: e = launch_dec<8, WG8>(a, T, s); break;
+    case 4: e = launch_dec<4, 4>(a, T, s); break;
     case 2: e = launch_dec<2, 2>(a, T, s); break;
     default: e = launch_dec<1, 1>(a, T, s); break;
   }

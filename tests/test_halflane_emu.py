@@ -372,3 +372,34 @@ def test_device_table332_equals_host_definition(lm):
         lo, hi = mul16x(ylo, yhi, t)
         got = [((lo >> (8 * i)) & 0xFF) | (((hi >> (8 * i)) & 0xFF) << 8) for i in range(4)]
         assert got == [mul(v, lm) for v in syms]
+
+
+@pytest.mark.parametrize("nq,threads,off", [(16, 1024, 0), (8, 512, 0), (8, 512, 512), (4, 256, 256)])
+def test_lds_position_tables_map(nq, threads, off):
+    """Round 6: the bit-0 layers read their tables from an LDS image instead of
+    the constant tables.  The image holds position OFF + 2 i at i x 80 B; its
+    global_load_lds fills (cooperative: pos_tables_to_lds, chunk c = i x
+    threads + 64 q + lane; per wave: pos_tables_wave, chunks 160 q ..) copy
+    16-B chunk c of table c // 5 to LDS byte 16 c, and layer0_sl reads table
+    32 q + j + 16 hl for the pair (j, j + 16) of half hl -- the position
+    layer0_s computes, OFF + 64 q + 2 j + 32 hl."""
+    tab = 80
+    ntab = nq * 32
+    image = {}
+    for c0 in range(0, 5 * ntab, 64):  # cooperative fill, wave-linear
+        for lane in range(64):
+            c = c0 + lane
+            src = (off + 2 * (c // 5)) * tab + (c % 5) * 16
+            image[16 * c] = src
+    for q in range(nq):  # per-wave fill covers the same chunks
+        for i in range(3):
+            for lane in range(64 if i < 2 else 32):
+                c = 160 * q + 64 * i + lane
+                assert image[16 * c] == (off + 2 * (c // 5)) * tab + (c % 5) * 16
+    for q in range(nq):
+        for j in range(16):
+            for hl in range(2):
+                idx = 32 * q + j + 16 * hl
+                pos = off + 64 * q + 2 * j + 32 * hl
+                for part in range(5):
+                    assert image[idx * tab + 16 * part] == pos * tab + 16 * part

@@ -1,0 +1,184 @@
+"""Host emulation of the round-6 quarter-lane GF(2^16) k = 512 decoder's data
+movement (csrc/rs_gf16.hip leo16_decode_q_kernel): n = 1024 elements over
+8 waves x 32 registers x 4 lane quarters (a lane quarter = 16 lanes = 128 B of
+a shard), so a workgroup of 512 threads holds one 128-B piece of a vector and
+two workgroups share a CU.  Layouts (q = wave, j = register, ql = quarter):
+  S  e = (j >> 3) + 4 (j & 7) + 32 ql + 128 q   loads, stores, pre/post
+                                                multiplies, layers on bits 0, 1
+  B  e = ql + 4 j + 128 q                        layers on bits 2-6
+  T  e = ql + 4 (j & 3) + 16 q + 128 (j >> 2)    layers on bits 7-9, derivative
+S <-> B is a 4 x 4 transpose of (j >> 3, ql) per register group j & 7
+(v_permlane32_swap then v_permlane16_swap), B <-> T the 8 x 8 LDS transpose of
+q with j >> 2.  Checked here on one symbol column against the plain Leopard
+loops (test_halflane_emu's references); the kernel itself bit-exact against
+the oracle on the GPU (tests/test_gpu_gf16.py)."""
+import pytest
+
+from test_halflane_emu import SKEW, bfly, ref_derivative, ref_fft, ref_ifft  # noqa: F401
+
+import numpy as np
+
+NQ = 8
+
+
+def e_s(q, j, ql):
+    return (j >> 3) + 4 * (j & 7) + 32 * ql + 128 * q
+
+
+def e_b(q, j, ql):
+    return ql + 4 * j + 128 * q
+
+
+def e_t(q, j, ql):
+    return ql + 4 * (j & 3) + 16 * q + 128 * (j >> 2)
+
+
+def permlane32_swap(a, b):
+    # rows (16 lanes) 2,3 of a <-> rows 0,1 of b
+    return [a[0], a[1], b[0], b[1]], [a[2], a[3], b[2], b[3]]
+
+
+def permlane16_swap(a, b):
+    # odd rows of a <-> even rows of b
+    return [a[0], b[0], a[2], b[2]], [a[1], b[1], a[3], b[3]]
+
+
+def swap_sb(R):
+    """S <-> B (its own inverse): per register group g, registers g + 8u."""
+    for reg in R:
+        for g in range(8):
+            r0, r1, r2, r3 = reg[g], reg[g + 8], reg[g + 16], reg[g + 24]
+            r0, r2 = permlane32_swap(r0, r2)
+            r1, r3 = permlane32_swap(r1, r3)
+            r0, r1 = permlane16_swap(r0, r1)
+            r2, r3 = permlane16_swap(r2, r3)
+            reg[g], reg[g + 8], reg[g + 16], reg[g + 24] = r0, r1, r2, r3
+
+
+def xpose_bt(R):
+    """B <-> T: wave q, register (jj << 2) | r <-> wave jj, register (q << 2) | r."""
+    S = [[None] * 32 for _ in range(NQ)]
+    for q in range(NQ):
+        for jj in range(NQ):
+            for r in range(4):
+                S[jj][(q << 2) | r] = list(R[q][(jj << 2) | r])
+    return S
+
+
+def layer_s(R, b, inv):
+    """Layers on element bits 0 (registers j, j + 8) and 1 (j, j + 16) in S:
+    per-lane positions (the quarter is element bits 5-6)."""
+    d = 1 << b
+    for q, reg in enumerate(R):
+        for j in range(32):
+            if (j >> 3) & d:
+                continue
+            for ql in range(4):
+                e = e_s(q, j, ql)
+                pos = (e & ~(2 * d - 1)) + d - 1
+                w = [reg[j][ql], reg[j + 8 * d][ql]]
+                bfly(w, 0, 1, pos, inv)
+                reg[j][ql], reg[j + 8 * d][ql] = w
+
+
+def layer_b(R, b, inv):
+    """Layers on bits 2-6 in B: registers j, j + 2^(b-2); position from the
+    register bits above and q (wave-uniform)."""
+    rd = 1 << (b - 2)
+    d = 1 << b
+    for q, reg in enumerate(R):
+        for j in range(32):
+            if j & rd:
+                continue
+            pos = ((128 * q + 4 * j) & ~(2 * d - 1)) + d - 1
+            for ql in range(4):
+                assert (e_b(q, j, ql) & ~(2 * d - 1)) + d - 1 == pos
+                w = [reg[j][ql], reg[j + rd][ql]]
+                bfly(w, 0, 1, pos, inv)
+                reg[j][ql], reg[j + rd][ql] = w
+
+
+def layer_t(R, b, inv):
+    """Layers on bits 7-9 in T: registers j, j + 4 * 2^(b-7); compile-time positions."""
+    rd = 4 << (b - 7)
+    d = 1 << b
+    for q, reg in enumerate(R):
+        for j in range(32):
+            if j & rd:
+                continue
+            pos = ((128 * (j >> 2)) & ~(2 * d - 1)) + d - 1
+            for ql in range(4):
+                assert (e_t(q, j, ql) & ~(2 * d - 1)) + d - 1 == pos
+                w = [reg[j][ql], reg[j + rd][ql]]
+                bfly(w, 0, 1, pos, inv)
+                reg[j][ql], reg[j + rd][ql] = w
+
+
+def derivative_t(R):
+    """D(x)_e = x_e ^ XOR_{s: bit s of e = 0} x_{e | 2^s}: register bits (2, 3,
+    7, 8, 9) in place, wave bits (4-6) and quarter bits (0-1: lanes ^ 16, ^ 32)
+    from the staged originals."""
+    orig = [[list(x) for x in reg] for reg in R]
+    for c, reg in enumerate(R):
+        for j in range(32):
+            for ql in range(4):
+                acc = orig[c][j][ql]
+                for bit in (1, 2, 4, 8, 16):
+                    if not j & bit:
+                        acc ^= orig[c][j | bit][ql]
+                for wb in (1, 2, 4):
+                    if not c & wb:
+                        acc ^= orig[c | wb][j][ql]
+                for qb in (1, 2):
+                    if not ql & qb:
+                        acc ^= orig[c][j][ql | qb]
+                reg[j][ql] = acc
+
+
+def gather(R, f):
+    out = {}
+    for q, reg in enumerate(R):
+        for j in range(32):
+            for ql in range(4):
+                out[f(q, j, ql)] = reg[j][ql]
+    return [out[e] for e in range(len(out))]
+
+
+def test_quarter_layouts_are_bijections_and_swaps_map():
+    for f in (e_s, e_b, e_t):
+        assert {f(q, j, ql) for q in range(NQ) for j in range(32) for ql in range(4)} == set(range(1024))
+    R = [[[e_s(q, j, ql) for ql in range(4)] for j in range(32)] for q in range(NQ)]
+    swap_sb(R)
+    assert all(R[q][j][ql] == e_b(q, j, ql) for q in range(NQ) for j in range(32) for ql in range(4))
+    T = xpose_bt(R)
+    assert all(T[q][j][ql] == e_t(q, j, ql) for q in range(NQ) for j in range(32) for ql in range(4))
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_quarterlane_decoder_equals_leopard_loops(seed):
+    rng = np.random.default_rng(seed)
+    n = 1024
+    x = [int(v) for v in rng.integers(0, 65536, n)]
+    ref = list(x)
+    ref_ifft(ref, 0)
+    ref_derivative(ref)
+    ref_fft(ref, 0)
+    R = [[[x[e_s(q, j, ql)] for ql in range(4)] for j in range(32)] for q in range(NQ)]
+    layer_s(R, 0, True)
+    layer_s(R, 1, True)
+    swap_sb(R)
+    for b in range(2, 7):
+        layer_b(R, b, True)
+    R = xpose_bt(R)
+    for b in (7, 8, 9):
+        layer_t(R, b, True)
+    derivative_t(R)
+    for b in (9, 8, 7):
+        layer_t(R, b, False)
+    R = xpose_bt(R)
+    for b in range(6, 1, -1):
+        layer_b(R, b, False)
+    swap_sb(R)
+    layer_s(R, 1, False)
+    layer_s(R, 0, False)
+    assert gather(R, e_s) == ref

@@ -11,5 +11,35 @@ case "$1" in
     timeout -k 10 600 python -u bench.py > gpurun_out/r06_clean_bench.log 2>&1 || { echo "bench failed"; tail -5 gpurun_out/r06_clean_bench.log; exit 1; }
     tail -c 600 gpurun_out/r06_clean_bench.log
     ;;
+  dec1)  # round 6: per-pattern decoder tables (glds), double-buffered transposes, LDS bit-0 tables (decoder + encoder)
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_gf16.py tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py tests/test_gpu_repair_async.py tests/test_gpu_split.py > gpurun_out/r06_dec1_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r06_dec1_tests.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 600 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_wide.py -k "not k8192 and not k4096" > gpurun_out/r06_dec1_wide.log 2>&1
+    rc=$?; echo "wide tests rc=$rc"; tail -3 gpurun_out/r06_dec1_wide.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 3 repair512 new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 2 repair512q3 new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode split --split-k 512 --steps 30 --warmup 3" new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 256 --batch 8 --steps 10 --warmup 2" new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 1024 --batch 1 --steps 3 --warmup 1" new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 1 "bench:--mode repair --k 2048 --batch 1 --steps 2 --warmup 1" new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode split --split-k 1024 --steps 10 --warmup 2" new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    for w in dec512h enc512h; do
+      for v in probe probebase; do
+        DAGPU_LIB=celestia-app_amd/libdagpu_$v.so timeout -k 10 300 python -u tools/phase_probe.py $w > gpurun_out/phase_probe_${w}_${v}_r06.log 2>&1 || { echo "probe $w $v failed"; tail -5 gpurun_out/phase_probe_${w}_${v}_r06.log; exit 1; }
+        echo "== $w $v"; cat gpurun_out/phase_probe_${w}_${v}_r06.log | grep -v amdgpu.ids
+      done
+    done
+    ;;
+  dec2)  # round 6: quarter-lane k = 512 decoder (two workgroups per CU) vs the half-lane one (round-6 form) vs round 5
+    timeout -k 10 60 ./tools/permlane_check > gpurun_out/r06_permlane.log 2>&1; echo "permlane rc=$?"; head -c 1200 gpurun_out/r06_permlane.log
+    DAGPU_LIB=celestia-app_amd/libdagpu_q.so timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_gf16.py tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py > gpurun_out/r06_dec2_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r06_dec2_tests.log; [ $rc -eq 0 ] || exit $rc
+    DAGPU_LIB=celestia-app_amd/libdagpu_q.so timeout -k 10 600 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_wide.py -k "not k8192 and not k4096" > gpurun_out/r06_dec2_wide.log 2>&1
+    rc=$?; echo "wide tests rc=$rc"; tail -3 gpurun_out/r06_dec2_wide.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 3 repair512 q=lib:celestia-app_amd/libdagpu_q.so half=lib:celestia-app_amd/libdagpu_half.so base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 1024 --batch 1 --steps 3 --warmup 1" q=lib:celestia-app_amd/libdagpu_q.so base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 1 "bench:--mode repair --k 2048 --batch 1 --steps 2 --warmup 1" q=lib:celestia-app_amd/libdagpu_q.so base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode split --split-k 1024 --steps 10 --warmup 2" q=lib:celestia-app_amd/libdagpu_q.so base=lib:celestia-app_amd/libdagpu_base.so
+    ;;
   *) echo "unknown step $1"; exit 2;;
 esac

@@ -15,7 +15,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["DAGPU_LIB"] = os.path.join(ROOT, "celestia-app_amd", "libdagpu_probe.so")
+os.environ.setdefault("DAGPU_LIB", os.path.join(ROOT, "celestia-app_amd", "libdagpu_probe.so"))
 for p in (ROOT, os.path.join(ROOT, "celestia-app_amd")):
     sys.path.insert(0, p)
 
