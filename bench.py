@@ -257,22 +257,18 @@ def load_stress_pmc(kernel: str):
 
 def gf16_kernel_names(k: int):
     """(forward encoder, decoder) kernel names the library runs at width k
-    (csrc/rs_gf16.hip launch selection, its A/B switches included), as
-    rocprofv3 / tools/pmc_stress.py name them."""
-    ld = 0 if os.environ.get("DAGPU_DEC_LOADALL") == "1" else 1
-    if k == 512:
-        enc = ("leo16_encode_reg32_kernel<512, false>" if os.environ.get("DAGPU_GF16_ENCH") == "0"
-               else "leo16_encode_h_kernel<512, false>")
-        dec = ("leo16_decode_reg1k_kernel" if os.environ.get("DAGPU_DEC1K_PACKED") == "1"
-               else f"leo16_decode_h_kernel<512, {ld}>")
-        return enc, dec
+    (csrc/rs_gf16.hip / rs_gf16_wide.hip launch selection), as rocprofv3 /
+    tools/pmc_stress.py name them."""
+    if k == 512:  # round 6: the quarter-lane kernels
+        return "leo16_encode_q_kernel<false>", "leo16_decode_q_kernel"
     if k == 256:
-        enc = ("leo16_encode_reg_kernel<256, false>" if os.environ.get("DAGPU_GF16_ENCH") == "0"
-               else "leo16_encode_h_kernel<256, false>")
-        dec = ("leo16_decode_reg_kernel" if os.environ.get("DAGPU_DEC256_REG") == "1"
-               else f"leo16_decode_h_kernel<256, {ld}>")
-        return enc, dec
-    return f"leo16w encode k={k}", f"leo16w decode k={k}"
+        return "leo16_encode_h_kernel<256, false>", "leo16_decode_h_kernel<256>"
+    ng = {1024: 8, 2048: 8, 4096: 4, 8192: 2}  # slice widths (encoder m = k, decoder n = 2k)
+    eg = {8: 4, 4: 4, 2: 2, 1: 1}
+    dg = {8: 8, 4: 4, 2: 2, 1: 1}
+    e_ng = ng.get(k, 1)
+    d_ng = ng.get(2 * k, 1)
+    return (f"leo16w_encode_kernel<{e_ng}, {eg[e_ng]}>", f"leo16w_decode_kernel<{d_ng}, {dg[d_ng]}>")
 
 
 def stress_roofline(kernel: str, alg_bytes: float, ms: float, launches: int, pmc_name: str, work: str):

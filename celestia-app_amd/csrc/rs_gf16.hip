@@ -1076,12 +1076,12 @@ __device__ __forceinline__ void layer_s_q(WQ& w, int ql, const uint32_t* img) {
 
 // Layer on element bit b in 2..6 in B: registers j, j + 2^(b-2); position
 // 128 q + 4 jb + d - 1 for the register block jb (wave-uniform, scalar tables)
-template <bool INV, int B>
+template <bool INV, int B, int OFF = 0>
 __device__ __forceinline__ void layer_b_q(WQ& w, int q) {
   constexpr int RD = 1 << (B - 2), D = 1 << B;
 #pragma unroll
   for (int jb = 0; jb < 32; jb += 2 * RD) {
-    const int pos = opaque_tok(128 * q + 4 * jb + D - 1, w.lo[jb]);
+    const int pos = opaque_tok(OFF + 128 * q + 4 * jb + D - 1, w.lo[jb]);
 #pragma unroll
     for (int j = jb; j < jb + RD; j++) {
       if constexpr (INV) ifft2_16(w, j, j + RD, pos);
@@ -1162,22 +1162,25 @@ __device__ __forceinline__ void derivative_tq(WQ& w, uint32_t* lds0, int c, int 
 // 128 q + 2 i, at img0 = lds + q * 64 * 80 B; bit 1, the 32 positions
 // 128 q + 4 i + 1, at img1 = lds + 40 KiB + q * 32 * 80 B (global_load_lds,
 // 16-B chunks lane-linear; the wave waits for its own DMA before reading).
+// (OFF: the transform's skew offset; IMG1: byte offset of the bit-1 images =
+// 5 KiB x waves; the decoder: OFF = 0, 8 waves)
+template <int OFF = 0, int IMG1 = 40 * 1024>
 __device__ __forceinline__ void q_pos_tables(uint32_t* lds, int q, int lane) {
   const uint8_t* src = (const uint8_t*)(const void*)g_ptab16x;
   asm volatile("" : "+v"(lane));  // the two calls' addresses are not kept live in between
   uint32_t* img0 = lds + q * 64 * kTab16x;
-  uint32_t* img1 = lds + 40 * 1024 / 4 + q * 32 * kTab16x;
+  uint32_t* img1 = lds + IMG1 / 4 + q * 32 * kTab16x;
 #pragma unroll
   for (int i = 0; i < 5; i++) {  // 320 chunks
     const int c = 64 * i + lane;
-    const uint8_t* g = src + (long)(128 * q + 2 * (c / 5)) * (kTab16x * 4) + (c % 5) * 16;
+    const uint8_t* g = src + (long)(OFF + 128 * q + 2 * (c / 5)) * (kTab16x * 4) + (c % 5) * 16;
     __builtin_amdgcn_global_load_lds((glb_vptr)g, (lds_vptr)(img0 + 64 * i * 4), 16, 0, 0);
   }
 #pragma unroll
   for (int i = 0; i < 3; i++) {  // 160 chunks
     const int c = 64 * i + lane;
     if (i < 2 || lane < 32) {
-      const uint8_t* g = src + (long)(128 * q + 4 * (c / 5) + 1) * (kTab16x * 4) + (c % 5) * 16;
+      const uint8_t* g = src + (long)(OFF + 128 * q + 4 * (c / 5) + 1) * (kTab16x * 4) + (c % 5) * 16;
       __builtin_amdgcn_global_load_lds((glb_vptr)g, (lds_vptr)(img1 + 64 * i * 4), 16, 0, 0);
     }
   }
@@ -1313,6 +1316,168 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       __builtin_amdgcn_raw_buffer_store_b32(xh, rsrc, voff + 32u, so, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k = 512 encoder, round 6 (leo16_encode_q_kernel): the quarter-lane layouts of
+// leo16_decode_q_kernel over m = 512 elements -- 4 waves (256 threads) x 32
+// registers x 4 quarters, one 128-B piece of a vector per workgroup, 32 KiB of
+// LDS -- so FOUR workgroups share a CU (the half-lane encoder: two).
+//   S, B as the decoder's;  T  e = ql + 4 (j & 7) + 32 q + 128 (j >> 3)
+// (B <-> T: xpose_bt_db with LR = 3, NQ = 4).  The last IFFT layer and the
+// first FFT layer (bit 8, registers j, j + 16 in T) are merged as in the other
+// encoders.  Host emulation: tests/test_quarterlane_emu.py.
+// ---------------------------------------------------------------------------
+// bits 7, 8 in T: registers j, j + 8 << (b - 7); position OFF + 128 (jb >> 3) + d - 1
+template <bool INV, int B, int OFF>
+__device__ __forceinline__ void layer_te_q(WQ& w) {
+  constexpr int RD = 8 << (B - 7), D = 1 << B;
+#pragma unroll
+  for (int jb = 0; jb < 32; jb += 2 * RD) {
+    const bool zero = OFF + 128 * (jb >> 3) == 0;
+    const int pos = zero ? 0 : opaque_tok(OFF + 128 * (jb >> 3) + D - 1, w.lo[jb]);
+#pragma unroll
+    for (int j = jb; j < jb + RD; j++) {
+      if (zero) {
+        w.lo[j + RD] ^= w.lo[j];
+        w.hi[j + RD] ^= w.hi[j];
+      } else if constexpr (INV) {
+        ifft2_16(w, j, j + RD, pos);
+      } else {
+        fft2_16(w, j, j + RD, pos);
+      }
+      pin_pair(w, j, j + RD);
+    }
+  }
+}
+
+template <bool REV>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_encode_q_kernel(
+    EncodeArgs a) {
+  constexpr int M = 512, IO = REV ? 0 : M, FO = REV ? M : 0;
+  // two 16-KiB transpose rounds (xpose_bt_db, LR = 3, RPR = 4); the S-layer
+  // images (30 KiB: bit 0 at q x 5 KiB, bit 1 at 20 KiB + q x 2.5 KiB) in the
+  // same space before the first transpose and after the last
+  __shared__ __attribute__((aligned(16))) uint32_t lds[8192];
+  constexpr int IMG1 = 20 * 1024;
+  const long blk = blockIdx.x;
+  const int piece = (int)(blk % a.nchunk);  // nchunk = 128-B pieces of the shard
+  const long sv = blk / a.nchunk;
+  const long vec = sv % a.nvec;
+  const long sq = sv / a.nvec;
+  if (vec_skipped(a, sv)) return;  // uniform
+  const int lane = threadIdx.x & 63;
+  const int ql = lane >> 4;
+  const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t col = (uint32_t)piece * 128u + (uint32_t)((lane >> 3) & 1) * 64u + (uint32_t)(lane & 7) * 4u;
+  const bool active = col < (uint32_t)a.shard_bytes;
+  q_pos_tables<IO, IMG1>(lds, q, lane);
+  const uint32_t cl = active ? col : 0u;  // inactive lanes read valid memory, store nothing
+  WQ w;
+  {
+    const auto in_rsrc = make_rsrc(a.in + sq * a.in_sq_stride + vec * a.in_vec_stride);
+    const uint32_t vin = cl + (uint32_t)ql * 32u * (uint32_t)a.in_shard_stride;  // quarter ql: shard + 32 ql
+    const int q_ld = opaque_s(q);
+#pragma unroll
+    for (int j = 0; j < 32; j++) {
+      const uint32_t so = (uint32_t)(128 * q_ld + q_elem_s(j, 0)) * (uint32_t)a.in_shard_stride;
+      w.lo[j] = __builtin_amdgcn_raw_buffer_load_b32(in_rsrc, vin, so, 0);
+      w.hi[j] = __builtin_amdgcn_raw_buffer_load_b32(in_rsrc, vin + 32u, so, 0);
+    }
+    if (a.copy && active) {  // Q0 placement
+      const auto cp = make_rsrc(a.copy + sq * a.copy_sq_stride + vec * a.copy_vec_stride);
+      const uint32_t vcp = col + (uint32_t)ql * 32u * (uint32_t)a.copy_shard_stride;
+#pragma unroll
+      for (int j = 0; j < 32; j++) {
+        const uint32_t so = (uint32_t)(128 * q_ld + q_elem_s(j, 0)) * (uint32_t)a.copy_shard_stride;
+        __builtin_amdgcn_raw_buffer_store_b32(w.lo[j], cp, vcp, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(w.hi[j], cp, vcp + 32u, so, 0);
+      }
+    }
+  }
+  // Repair fill: which out-half shards are given, read before the transform;
+  // the lane's 32 registers are bits 32 ql .. +31 of the wave's 128 (gw)
+  uint32_t gw = 0;
+  if (a.out_present) {
+    const uint64_t g0 = __builtin_amdgcn_ballot_w64(fill_given(a, sq, vec, 128 * q + lane));
+    const uint64_t g1 = __builtin_amdgcn_ballot_w64(fill_given(a, sq, vec, 128 * q + 64 + lane));
+    gw = ql == 0 ? (uint32_t)g0 : ql == 1 ? (uint32_t)(g0 >> 32) : ql == 2 ? (uint32_t)g1 : (uint32_t)(g1 >> 32);
+  }
+  // ---- IFFT (ifftDITEncoder, skew index IO - 1 + iend) ----
+  wait_dma();
+  layer_s_q<true, 0>(w, ql, lds + q * 64 * kTab16x);
+  layer_s_q<true, 1>(w, ql, lds + IMG1 / 4 + q * 32 * kTab16x);
+  swap_sb_q(w);
+  layer_b_q<true, 2, IO>(w, q);
+  layer_b_q<true, 3, IO>(w, q);
+  layer_b_q<true, 4, IO>(w, q);
+  layer_b_q<true, 5, IO>(w, q);
+  layer_b_q<true, 6, IO>(w, q);
+  __syncthreads();  // every wave's reads of its S-layer images are done
+  xpose_bt_db<3, 4, 0>(w, lds, q, lane);  // rounds A B A B
+  layer_te_q<true, 7, IO>(w);
+  // last IFFT layer (bit 8, skew IO + 255) merged with the first FFT layer
+  // (bit 8, skew FO + 255): registers j, j + 16
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    ifft_fft2_16(w, j, j + 16, MERGED_TAB(1));
+    pin_pair(w, j, j + 16);
+  }
+  // ---- FFT (fftDIT, skew index FO + iend - 1) ----
+  layer_te_q<false, 7, FO>(w);
+  xpose_bt_db<3, 4, 0>(w, lds, q, lane);  // A B A B
+  __syncthreads();  // every wave's reads of B are done: the images come back over it
+  q_pos_tables<FO, IMG1>(lds, q, lane);
+  layer_b_q<false, 6, FO>(w, q);
+  layer_b_q<false, 5, FO>(w, q);
+  layer_b_q<false, 4, FO>(w, q);
+  layer_b_q<false, 3, FO>(w, q);
+  layer_b_q<false, 2, FO>(w, q);
+  swap_sb_q(w);
+  wait_dma();
+  layer_s_q<false, 1>(w, ql, lds + IMG1 / 4 + q * 32 * kTab16x);
+  layer_s_q<false, 0>(w, ql, lds + q * 64 * kTab16x);
+  if (!active) return;
+  // ---- store: compare (prerepairSanityCheck), Repair fill, or plain ----
+  const auto out_rsrc = make_rsrc(a.out + sq * a.out_sq_stride + vec * a.out_vec_stride);
+  const uint32_t vout = col + (uint32_t)ql * 32u * (uint32_t)a.out_shard_stride;
+  const int q_st = opaque_s(q);
+  if (a.mismatch) {
+    uint32_t diff = 0;
+#pragma unroll
+    for (int j = 0; j < 32; j++) {
+      const uint32_t so = (uint32_t)(128 * q_st + q_elem_s(j, 0)) * (uint32_t)a.out_shard_stride;
+      diff |= w.lo[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, vout, so, 0);
+      diff |= w.hi[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, vout + 32u, so, 0);
+    }
+    if (diff) {
+      atomicOr(&a.mismatch[sq], a.mismatch_bit);
+      if (a.mismatch_vec) a.mismatch_vec[sq * a.nvec + vec] = 1;
+    }
+    return;
+  }
+  if (a.out_present) {  // store the missing shards of the out half, compare given ones
+    uint32_t diff = 0;
+#pragma unroll
+    for (int j = 0; j < 32; j++) {
+      const uint32_t so = (uint32_t)(128 * q_st + q_elem_s(j, 0)) * (uint32_t)a.out_shard_stride;
+      if ((gw >> q_elem_s(j, 0)) & 1) {
+        diff |= w.lo[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, vout, so, 0);
+        diff |= w.hi[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, vout + 32u, so, 0);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b32(w.lo[j], out_rsrc, vout, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(w.hi[j], out_rsrc, vout + 32u, so, 0);
+      }
+    }
+    if (diff) a.redo[sv] = 1;
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 32; j++) {
+    const uint32_t so = (uint32_t)(128 * q_st + q_elem_s(j, 0)) * (uint32_t)a.out_shard_stride;
+    __builtin_amdgcn_raw_buffer_store_b32(w.lo[j], out_rsrc, vout, so, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(w.hi[j], out_rsrc, vout + 32u, so, 0);
   }
 }
 
@@ -1572,8 +1737,15 @@ hipError_t launch_leo16_encode(int k, const EncodeArgs& a, hipStream_t s) {
   const long hb = b.nsq * b.nvec * b.nchunk;
   if (hb <= 0) return hipSuccess;
   if (k == 512) {
+#ifndef DAGPU_ENC512_HALF  // (A/B builds: the half-lane k = 512 encoder)
+    b.nchunk = (a.shard_bytes + 127) / 128;  // quarter-lane encoder, 128-B pieces, four workgroups per CU
+    const long qb = b.nsq * b.nvec * b.nchunk;
+    if (a.reverse) hipLaunchKernelGGL((leo16_encode_q_kernel<true>), dim3((unsigned)qb), dim3(256), 0, s, b);
+    else hipLaunchKernelGGL((leo16_encode_q_kernel<false>), dim3((unsigned)qb), dim3(256), 0, s, b);
+#else
     if (a.reverse) hipLaunchKernelGGL((leo16_encode_h_kernel<512, true>), dim3((unsigned)hb), dim3(512), 0, s, b);
     else hipLaunchKernelGGL((leo16_encode_h_kernel<512, false>), dim3((unsigned)hb), dim3(512), 0, s, b);
+#endif
   } else {
     if (a.reverse) hipLaunchKernelGGL((leo16_encode_h_kernel<256, true>), dim3((unsigned)hb), dim3(256), 0, s, b);
     else hipLaunchKernelGGL((leo16_encode_h_kernel<256, false>), dim3((unsigned)hb), dim3(256), 0, s, b);

@@ -182,3 +182,107 @@ def test_quarterlane_decoder_equals_leopard_loops(seed):
     layer_s(R, 1, False)
     layer_s(R, 0, False)
     assert gather(R, e_s) == ref
+
+
+# --- the quarter-lane k = 512 encoder (leo16_encode_q_kernel): m = 512 over 4
+# waves; S and B as the decoder's, T e = ql + 4 (j & 7) + 32 q + 128 (j >> 3)
+# (B <-> T: the 4 x 4 transpose of q with j >> 3, LR = 3)
+NQE = 4
+
+
+def e_te(q, j, ql):
+    return ql + 4 * (j & 7) + 32 * q + 128 * (j >> 3)
+
+
+def xpose_bt_e(R):
+    S = [[None] * 32 for _ in range(NQE)]
+    for q in range(NQE):
+        for jj in range(NQE):
+            for r in range(8):
+                S[jj][(q << 3) | r] = list(R[q][(jj << 3) | r])
+    return S
+
+
+def layer_s_off(R, b, off, inv):
+    d = 1 << b
+    for q, reg in enumerate(R):
+        for j in range(32):
+            if (j >> 3) & d:
+                continue
+            for ql in range(4):
+                e = e_s(q, j, ql)
+                w = [reg[j][ql], reg[j + 8 * d][ql]]
+                bfly(w, 0, 1, off + (e & ~(2 * d - 1)) + d - 1, inv)
+                reg[j][ql], reg[j + 8 * d][ql] = w
+
+
+def layer_b_off(R, b, off, inv):
+    rd, d = 1 << (b - 2), 1 << b
+    for q, reg in enumerate(R):
+        for jb in range(0, 32, 2 * rd):
+            pos = off + 128 * q + 4 * jb + d - 1
+            for j in range(jb, jb + rd):
+                for ql in range(4):
+                    assert off + (e_b(q, j, ql) & ~(2 * d - 1)) + d - 1 == pos
+                    w = [reg[j][ql], reg[j + rd][ql]]
+                    bfly(w, 0, 1, pos, inv)
+                    reg[j][ql], reg[j + rd][ql] = w
+
+
+def layer_te(R, b, off, inv):
+    """bits 7, 8 in T: registers j, j + 8 << (b - 7); position off + 128 (jb >> 3) + d - 1"""
+    rd, d = 8 << (b - 7), 1 << b
+    for q, reg in enumerate(R):
+        for jb in range(0, 32, 2 * rd):
+            pos = off + 128 * (jb >> 3) + d - 1
+            for j in range(jb, jb + rd):
+                for ql in range(4):
+                    assert off + (e_te(q, j, ql) & ~(2 * d - 1)) + d - 1 == pos
+                    w = [reg[j][ql], reg[j + rd][ql]]
+                    bfly(w, 0, 1, pos, inv)
+                    reg[j][ql], reg[j + rd][ql] = w
+
+
+@pytest.mark.parametrize("rev", [False, True])
+def test_quarterlane_encoder_equals_leopard_loops(rev):
+    rng = np.random.default_rng(11 + rev)
+    m = 512
+    io, fo = (0, m) if rev else (m, 0)
+    x = [int(v) for v in rng.integers(0, 65536, m)]
+    ref = list(x)
+    ref_ifft(ref, io)
+    ref_fft(ref, fo)
+    R = [[[x[e_s(q, j, ql)] for ql in range(4)] for j in range(32)] for q in range(NQE)]
+    layer_s_off(R, 0, io, True)
+    layer_s_off(R, 1, io, True)
+    swap_sb(R)
+    for b in range(2, 7):
+        layer_b_off(R, b, io, True)
+    R = xpose_bt_e(R)
+    layer_te(R, 7, io, True)
+    layer_te(R, 8, io, True)  # (merged with the next in the kernel)
+    layer_te(R, 8, fo, False)
+    layer_te(R, 7, fo, False)
+    R = xpose_bt_e(R)
+    for b in range(6, 1, -1):
+        layer_b_off(R, b, fo, False)
+    swap_sb(R)
+    layer_s_off(R, 1, fo, False)
+    layer_s_off(R, 0, fo, False)
+    got = []
+    for e in range(m):
+        q, j, ql = _inv_s(e)
+        got.append(R[q][j][ql])
+    assert got == ref
+
+
+def _inv_s(e):
+    return e >> 7, (e & 3) * 8 + ((e >> 2) & 7), (e >> 5) & 3
+
+
+def test_encoder_layout_bijections():
+    assert {e_te(q, j, ql) for q in range(NQE) for j in range(32) for ql in range(4)} == set(range(512))
+    assert all(e_s(*_inv_s(e)) == e for e in range(512))
+    R = [[[e_b(q, j, ql) for ql in range(4)] for j in range(32)] for q in range(NQE)]
+    T = xpose_bt_e(R)
+    assert all(T[q][j][ql] == e_te(q, j, ql) for q in range(NQE) for j in range(32) for ql in range(4))

@@ -41,5 +41,16 @@ case "$1" in
     bash tools/gpu_ab.sh --rounds 1 "bench:--mode repair --k 2048 --batch 1 --steps 2 --warmup 1" q=lib:celestia-app_amd/libdagpu_q.so base=lib:celestia-app_amd/libdagpu_base.so && \
     bash tools/gpu_ab.sh --rounds 2 "bench:--mode split --split-k 1024 --steps 10 --warmup 2" q=lib:celestia-app_amd/libdagpu_q.so base=lib:celestia-app_amd/libdagpu_base.so
     ;;
+  dec3)  # round 6: quarter-lane k = 512 encoder (four workgroups per CU) vs the half-lane one; counters of the new kernels
+    DAGPU_LIB=celestia-app_amd/libdagpu_qe.so timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_gf16.py tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py tests/test_gpu_split.py > gpurun_out/r06_dec3_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r06_dec3_tests.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 3 repair512 qe=lib:celestia-app_amd/libdagpu_qe.so he=lib:celestia-app_amd/libdagpu_he.so && \
+    bash tools/gpu_ab.sh --rounds 3 repair512q3 qe=lib:celestia-app_amd/libdagpu_qe.so he=lib:celestia-app_amd/libdagpu_he.so base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 3 "bench:--mode split --split-k 512 --steps 30 --warmup 3" qe=lib:celestia-app_amd/libdagpu_qe.so he=lib:celestia-app_amd/libdagpu_he.so base=lib:celestia-app_amd/libdagpu_base.so && \
+    DAGPU_LIB=celestia-app_amd/libdagpu_qe.so bash tools/gpu_pmc_gf16.sh repair512 repair512q3 split512 repair1024 repair2048
+    ;;
+  val1)  # round 6: the whole tree -- every GPU test, the default bench line and its trace, the headline counters
+    bash tools/gpu_final.sh && bash tools/gpu_profile.sh r06 counters
+    ;;
   *) echo "unknown step $1"; exit 2;;
 esac
