@@ -260,7 +260,7 @@ def gf16_kernel_names(k: int):
     (csrc/rs_gf16.hip / rs_gf16_wide.hip launch selection), as rocprofv3 /
     tools/pmc_stress.py name them."""
     if k == 512:  # round 6: the quarter-lane kernels
-        return "leo16_encode_q_kernel<false>", "leo16_decode_q_kernel"
+        return "leo16_encode_q_kernel<false>", "leo16_decode_q_kernel<512>"
     if k == 256:
         return "leo16_encode_h_kernel<256, false>", "leo16_decode_h_kernel<256>"
     ng = {1024: 8, 2048: 8, 4096: 4, 8192: 2}  # slice widths (encoder m = k, decoder n = 2k)

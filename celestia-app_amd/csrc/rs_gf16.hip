@@ -1093,13 +1093,13 @@ __device__ __forceinline__ void layer_b_q(WQ& w, int q) {
 
 // Layer on element bit b in 7..9 in T: registers j, j + 4 * 2^(b-7);
 // compile-time positions 128 (jb >> 2) + d - 1; block start 0 is a zero skew
-template <bool INV, int B>
+template <bool INV, int B, int LR = 2>
 __device__ __forceinline__ void layer_t_q(WQ& w) {
-  constexpr int RD = 4 << (B - 7), D = 1 << B;
+  constexpr int RD = (1 << LR) << (B - 7), D = 1 << B;
 #pragma unroll
   for (int jb = 0; jb < 32; jb += 2 * RD) {
     const bool zero = jb == 0;
-    const int pos = zero ? 0 : opaque_tok(128 * (jb >> 2) + D - 1, w.lo[jb]);
+    const int pos = zero ? 0 : opaque_tok(128 * (jb >> LR) + D - 1, w.lo[jb]);
 #pragma unroll
     for (int j = jb; j < 32; j++) {
       if ((j & ~(2 * RD - 1)) != jb || (j & RD)) continue;
@@ -1120,8 +1120,9 @@ __device__ __forceinline__ void layer_t_q(WQ& w) {
 // ascending register order; wave bits (4-6) and quarter bits (0: lane ^ 16,
 // 1: lane ^ 32) from the originals staged in LDS, 8 registers per round in two
 // alternating 32-KiB buffers (no barrier after a round's reads).
+template <int NQ = 8>
 __device__ __forceinline__ void derivative_tq(WQ& w, uint32_t* lds0, int c, int lane) {
-  constexpr int B = 8, RW = 8 * B * 2 * 64;
+  constexpr int B = 8, RW = NQ * B * 2 * 64;
   const uint32_t m16 = ((lane >> 4) & 1) ? 0u : 0xFFFFFFFFu, m32 = ((lane >> 5) & 1) ? 0u : 0xFFFFFFFFu;
 #pragma unroll
   for (int s0 = 0; s0 < 32; s0 += B) {
@@ -1143,7 +1144,7 @@ __device__ __forceinline__ void derivative_tq(WQ& w, uint32_t* lds0, int c, int 
           ahi ^= w.hi[j | bit];
         }
 #pragma unroll
-      for (int wb = 1; wb < 8; wb <<= 1)
+      for (int wb = 1; wb < NQ; wb <<= 1)
         if ((c & wb) == 0) {
           alo ^= lds[(((c | wb) * B + u) * 2) * 64 + lane];
           ahi ^= lds[(((c | wb) * B + u) * 2 + 1) * 64 + lane];
@@ -1186,14 +1187,19 @@ __device__ __forceinline__ void q_pos_tables(uint32_t* lds, int q, int lane) {
   }
 }
 
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_decode_q_kernel(
+// K = 512 (8 waves, T e = ql + 4 (j & 3) + 16 q + 128 (j >> 2), bits 7-9) and
+// K = 256 (4 waves, T as the encoder's: e = ql + 4 (j & 7) + 32 q + 128 (j >> 3),
+// bits 7-8; four workgroups per CU, the half-lane k = 256 decoder: two)
+template <int K>
+__global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_decode_q_kernel(
     DecodeArgs a) {
-  constexpr int K = 512;
-  // two 32-KiB rounds of the transposes / derivative; the S-layer images
-  // (60 KiB) in the same space before the first transpose and after the last
-  __shared__ __attribute__((aligned(16))) uint32_t lds[16384];
+  constexpr int NQ = K / 64, LR = K == 512 ? 2 : 3, RPR = K == 512 ? 2 : 4, IMG1 = NQ * 5 * 1024;
+  // two rounds of the transposes / derivative (K = 512: 32 KiB each, 256: 16
+  // KiB); the S-layer images (NQ x 7.5 KiB) in the same space before the first
+  // transpose and after the last
+  __shared__ __attribute__((aligned(16))) uint32_t lds[K * 32];
   const uint32_t* img0_base = lds;
-  const uint32_t* img1_base = lds + 40 * 1024 / 4;
+  const uint32_t* img1_base = lds + IMG1 / 4;
   const long blk = blockIdx.x;
   const int piece = (int)(blk % a.nchunk);  // nchunk = 128-B pieces of the shard
   const long v = blk / a.nchunk;
@@ -1202,7 +1208,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   const int lane = threadIdx.x & 63;
   const int ql = lane >> 4;
   const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  q_pos_tables(lds, q, lane);
+  q_pos_tables<0, IMG1>(lds, q, lane);
   const uint32_t col = (uint32_t)piece * 128u + (uint32_t)((lane >> 3) & 1) * 64u + (uint32_t)(lane & 7) * 4u;
   const uint32_t voff = col + (uint32_t)ql * 32u * (uint32_t)a.shard_stride;  // quarter ql: shard + 32 ql
   const auto rsrc = make_rsrc(a.data + sq * a.sq_stride + vec * a.vec_stride);
@@ -1263,18 +1269,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   layer_b_q<true, 5>(w, q);
   layer_b_q<true, 6>(w, q);
   __syncthreads();  // every wave's reads of its S-layer images are done
-  xpose_bt_db<2, 2, 0>(w, lds, q, lane);  // rounds A B A B
-  layer_t_q<true, 7>(w);
-  layer_t_q<true, 8>(w);
-  layer_t_q<true, 9>(w);
-  derivative_tq(w, lds, q, lane);  // A B A B
+  xpose_bt_db<LR, RPR, 0>(w, lds, q, lane);  // rounds A B A B
+  layer_t_q<true, 7, LR>(w);
+  layer_t_q<true, 8, LR>(w);
+  if constexpr (K == 512) layer_t_q<true, 9, LR>(w);
+  derivative_tq<NQ>(w, lds, q, lane);  // A B A B
   // ---- FFT (fftDIT, skew index iend - 1) ----
-  layer_t_q<false, 9>(w);
-  layer_t_q<false, 8>(w);
-  layer_t_q<false, 7>(w);
-  xpose_bt_db<2, 2, 0>(w, lds, q, lane);  // A B A B
+  if constexpr (K == 512) layer_t_q<false, 9, LR>(w);
+  layer_t_q<false, 8, LR>(w);
+  layer_t_q<false, 7, LR>(w);
+  xpose_bt_db<LR, RPR, 0>(w, lds, q, lane);  // A B A B
   __syncthreads();  // every wave's reads of B are done: the images come back over it
-  q_pos_tables(lds, q, lane);
+  q_pos_tables<0, IMG1>(lds, q, lane);
   layer_b_q<false, 6>(w, q);
   layer_b_q<false, 5>(w, q);
   layer_b_q<false, 4>(w, q);
@@ -1781,13 +1787,19 @@ hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mar
     if (a.k == 512) {
 #ifndef DAGPU_DEC512_HALF  // (A/B builds: the half-lane k = 512 decoder)
       b.nchunk = a.shard_bytes / 128;  // quarter-lane decoder, 128-B pieces, two workgroups per CU
-      hipLaunchKernelGGL(leo16_decode_q_kernel, dim3((unsigned)(nv * b.nchunk)), dim3(512), 0, s, b);
+      hipLaunchKernelGGL(leo16_decode_q_kernel<512>, dim3((unsigned)(nv * b.nchunk)), dim3(512), 0, s, b);
 #else
       hipLaunchKernelGGL((leo16_decode_h_kernel<512>), dim3((unsigned)grid), dim3(1024), dec_h_lds_bytes<512>(), s, b);
 #endif
-    }
-    else
+    } else {
+#ifdef DAGPU_DEC256_QUARTER  // (A/B builds: the quarter-lane k = 256 decoder, four workgroups per CU:
+      // 2,533-2,540 vs 2,551-2,562 squares/s for the half-lane one, profiles/gf16_q256_ab_r06.log)
+      b.nchunk = a.shard_bytes / 128;
+      hipLaunchKernelGGL(leo16_decode_q_kernel<256>, dim3((unsigned)(nv * b.nchunk)), dim3(256), 0, s, b);
+#else
       hipLaunchKernelGGL((leo16_decode_h_kernel<256>), dim3((unsigned)grid), dim3(512), dec_h_lds_bytes<256>(), s, b);
+#endif
+    }
   } else {  // shard sizes off the 256-B grid (codec API): the generic LDS decoder
     const long blocks = nv * (a.shard_bytes / 64);
     hipLaunchKernelGGL(leo16_decode_kernel, dim3((unsigned)blocks), dim3(kThreads16),

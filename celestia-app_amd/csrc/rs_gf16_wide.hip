@@ -39,7 +39,15 @@ namespace dagpu {
 namespace {
 
 constexpr uint32_t kMod = 65535u;
+// Threads per workgroup: 512 (8 waves); round 6: the decoders of n >= 4096
+// elements 1,024 (16 waves, so that the one workgroup a CU holds -- its LDS slice
+// takes up to 160 KiB -- has 4 waves per SIMD to hide its LDS and table latency:
+// k = 2048 Repair 18.2 -> 20.2 squares/s; at n = 2048 a wash, and the encoder at
+// 1,024 threads slowed the k = 1024 split square 5.0 -> 6.2 ms;
+// profiles/gf16_wide_ab_r06.log).
 constexpr int kWideThreads = 512;
+template <int NG>
+constexpr int dec_threads() { return NG <= 4 ? 1024 : 512; }
 constexpr int kPtabPos = 2 * kMaxK;  // skew positions used by any transform <= 2 kMaxK
 
 struct WideTabs {
@@ -285,13 +293,13 @@ __device__ __forceinline__ void load_tab_u(const WideTabs& T, int pos, uint32_t 
 // One radix-4 IFFT step (dist, dist4 = 4 dist) over all units.  UNI: the 64
 // units of a wave lie in one block of 4 dist elements (dist * CH >= 64), so
 // their three skew positions are wave-uniform and the tables come by scalar loads.
-template <int NG, int G, bool UNI>
+template <int NG, int G, bool UNI, int TH>
 __device__ __forceinline__ void ifft_step(const Planes<NG>& P, const WideTabs& T, int n, int base, int dist) {
   constexpr int CH = NG / G;
   const int dist4 = dist << 2;
   const int units = (n / 4) * CH;
   uint32_t t[kTabW];
-  for (int u = threadIdx.x; u < units; u += kWideThreads) {
+  for (int u = threadIdx.x; u < units; u += TH) {
     const int quad = u / CH, g0 = (u - quad * CH) * G;
     const int r = (quad / dist) * dist4, i = r + (quad % dist), iend = r + dist;
     const int e[4] = {i, i + dist, i + 2 * dist, i + 3 * dist};
@@ -318,13 +326,13 @@ __device__ __forceinline__ void ifft_step(const Planes<NG>& P, const WideTabs& T
 
 // ifftDITEncoder / ifftDITDecoder over n elements (mtrunc = n), skew index
 // base + iend (encoder: base = IO - 1; decoder: -1)
-template <int NG, int G>
+template <int NG, int G, int TH>
 __device__ void wide_ifft(const Planes<NG>& P, const WideTabs& T, int n, int base) {
   constexpr int CH = NG / G;
   int dist = 1, dist4 = 4;
   while (dist4 <= n) {
-    if (dist * CH >= 64) ifft_step<NG, G, true>(P, T, n, base, dist);
-    else ifft_step<NG, G, false>(P, T, n, base, dist);
+    if (dist * CH >= 64) ifft_step<NG, G, true, TH>(P, T, n, base, dist);
+    else ifft_step<NG, G, false, TH>(P, T, n, base, dist);
     dist = dist4;
     dist4 <<= 2;
   }
@@ -333,7 +341,7 @@ __device__ void wide_ifft(const Planes<NG>& P, const WideTabs& T, int n, int bas
     uint32_t t[kTabW];
     const bool z = zero_skew(base + dist);
     if (!z) load_tab_u(T, base + dist, t);
-    for (int u = threadIdx.x; u < units; u += kWideThreads) {
+    for (int u = threadIdx.x; u < units; u += TH) {
       const int p = u / CH, g0 = (u - p * CH) * G;
       const int e[2] = {p, p + dist};
       Unit<NG, G, 2> x;
@@ -346,13 +354,13 @@ __device__ void wide_ifft(const Planes<NG>& P, const WideTabs& T, int n, int bas
 }
 
 // One radix-4 FFT step (fftDIT, skew index fo + iend - 1); UNI as ifft_step.
-template <int NG, int G, bool UNI>
+template <int NG, int G, bool UNI, int TH>
 __device__ __forceinline__ void fft_step(const Planes<NG>& P, const WideTabs& T, int n, int fo, int dist) {
   constexpr int CH = NG / G;
   const int dist4 = dist << 2;
   const int units = (n / 4) * CH;
   uint32_t t[kTabW];
-  for (int u = threadIdx.x; u < units; u += kWideThreads) {
+  for (int u = threadIdx.x; u < units; u += TH) {
     const int quad = u / CH, g0 = (u - quad * CH) * G;
     const int r = (quad / dist) * dist4, i = r + (quad % dist), iend = r + dist;
     const int e[4] = {i, i + dist, i + 2 * dist, i + 3 * dist};
@@ -378,20 +386,20 @@ __device__ __forceinline__ void fft_step(const Planes<NG>& P, const WideTabs& T,
 }
 
 // fftDIT over n elements (mtrunc = n), skew index fo + iend - 1
-template <int NG, int G>
+template <int NG, int G, int TH>
 __device__ void wide_fft(const Planes<NG>& P, const WideTabs& T, int n, int fo) {
   constexpr int CH = NG / G;
   int dist4 = n, dist = n >> 2;
   while (dist != 0) {
-    if (dist * CH >= 64) fft_step<NG, G, true>(P, T, n, fo, dist);
-    else fft_step<NG, G, false>(P, T, n, fo, dist);
+    if (dist * CH >= 64) fft_step<NG, G, true, TH>(P, T, n, fo, dist);
+    else fft_step<NG, G, false, TH>(P, T, n, fo, dist);
     dist4 = dist;
     dist >>= 2;
   }
   if (dist4 == 2) {
     const int units = (n / 2) * CH;
     uint32_t t[kTabW];
-    for (int u = threadIdx.x; u < units; u += kWideThreads) {
+    for (int u = threadIdx.x; u < units; u += TH) {
       const int p = u / CH, g0 = (u - p * CH) * G;
       const int e[2] = {2 * p, 2 * p + 1};
       const bool z = zero_skew(fo + 2 * p);
@@ -455,8 +463,8 @@ __global__ __launch_bounds__(kWideThreads) void leo16w_encode_kernel(EncodeArgs 
     }
   }
   __syncthreads();
-  wide_ifft<NG, G>(P, T, k, a.reverse ? -1 : k - 1);
-  wide_fft<NG, G>(P, T, k, a.reverse ? k : 0);
+  wide_ifft<NG, G, kWideThreads>(P, T, k, a.reverse ? -1 : k - 1);
+  wide_fft<NG, G, kWideThreads>(P, T, k, a.reverse ? k : 0);
   uint8_t* out = a.out + sq * a.out_sq_stride + vec * a.out_vec_stride + col;
   bool diff = false;
   for (int t = threadIdx.x; t < k * NG; t += kWideThreads) {
@@ -597,7 +605,8 @@ __global__ __launch_bounds__(kFoldThreads) void leo16w_errlocs_kernel(DecodeArgs
 // reading before a barrier and writing after it.
 // ---------------------------------------------------------------------------
 template <int NG, int G>
-__global__ __launch_bounds__(kWideThreads) void leo16w_decode_kernel(DecodeArgs a, WideTabs T) {
+__global__ __launch_bounds__(dec_threads<NG>()) void leo16w_decode_kernel(DecodeArgs a, WideTabs T) {
+  constexpr int TH = dec_threads<NG>();
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   constexpr int CH = NG / G;
   const int k = a.k, n = 2 * k;
@@ -614,7 +623,7 @@ __global__ __launch_bounds__(kWideThreads) void leo16w_decode_kernel(DecodeArgs 
   // k = 256 / 512 (DAGPU_GF16_WIDE A/B) has the register kernels' tables there
   const uint8_t* pbase = k >= 1024 ? (const uint8_t*)err + rs_err_tab_off(k) : nullptr;
   // one thread per element: its table once, then its NG dword pairs
-  for (int i = threadIdx.x; i < n; i += kWideThreads) {
+  for (int i = threadIdx.x; i < n; i += TH) {
     const long shard = i < k ? k + i : i - k;
     if (pres[shard * a.p_shard_stride]) {
       const uint32_t* src = (const uint32_t*)(base + shard * a.shard_stride);
@@ -640,9 +649,9 @@ __global__ __launch_bounds__(kWideThreads) void leo16w_decode_kernel(DecodeArgs 
     }
   }
   __syncthreads();
-  wide_ifft<NG, G>(P, T, n, -1);
+  wide_ifft<NG, G, TH>(P, T, n, -1);
   {  // formal derivative, ascending chunks of X elements
-    constexpr int X = kWideThreads / CH;
+    constexpr int X = TH / CH;
     for (int x0 = 0; x0 < n; x0 += X) {
       const int u = threadIdx.x;
       const int x = x0 + u / CH, g0 = (u % CH) * G;
@@ -674,8 +683,8 @@ __global__ __launch_bounds__(kWideThreads) void leo16w_decode_kernel(DecodeArgs 
       __syncthreads();
     }
   }
-  wide_fft<NG, G>(P, T, n, 0);
-  for (int i = threadIdx.x; i < n; i += kWideThreads) {
+  wide_fft<NG, G, TH>(P, T, n, 0);
+  for (int i = threadIdx.x; i < n; i += TH) {
     const long shard = i < k ? k + i : i - k;
     if (pres[shard * a.p_shard_stride]) continue;
     uint32_t lo[NG], hi[NG];
@@ -811,7 +820,7 @@ hipError_t launch_dec(const DecodeArgs& a, const WideTabs& T, hipStream_t s) {
   if (e != hipSuccess) return e;
   const long blocks = a.nsq * a.nvec * (a.shard_bytes / 64) * (8 / NG);
   if (blocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL((leo16w_decode_kernel<NG, G>), dim3((unsigned)blocks), dim3(kWideThreads), lds, s, a, T);
+  hipLaunchKernelGGL((leo16w_decode_kernel<NG, G>), dim3((unsigned)blocks), dim3(dec_threads<NG>()), lds, s, a, T);
   return hipGetLastError();
 }
 

@@ -286,3 +286,57 @@ def test_encoder_layout_bijections():
     R = [[[e_b(q, j, ql) for ql in range(4)] for j in range(32)] for q in range(NQE)]
     T = xpose_bt_e(R)
     assert all(T[q][j][ql] == e_te(q, j, ql) for q in range(NQE) for j in range(32) for ql in range(4))
+
+
+# --- k = 256 (n = 512) through the same decoder template: 4 waves, T as the
+# encoder's (LR = 3: e = ql + 4 (j & 7) + 32 q + 128 (j >> 3)), layers on bits 7-8
+def derivative_te(R):
+    orig = [[list(x) for x in reg] for reg in R]
+    for c, reg in enumerate(R):
+        for j in range(32):
+            for ql in range(4):
+                acc = orig[c][j][ql]
+                for bit in (1, 2, 4, 8, 16):
+                    if not j & bit:
+                        acc ^= orig[c][j | bit][ql]
+                for wb in (1, 2):
+                    if not c & wb:
+                        acc ^= orig[c | wb][j][ql]
+                for qb in (1, 2):
+                    if not ql & qb:
+                        acc ^= orig[c][j][ql | qb]
+                reg[j][ql] = acc
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_quarterlane_decoder_k256_equals_leopard_loops(seed):
+    rng = np.random.default_rng(seed)
+    n = 512
+    x = [int(v) for v in rng.integers(0, 65536, n)]
+    ref = list(x)
+    ref_ifft(ref, 0)
+    ref_derivative(ref)
+    ref_fft(ref, 0)
+    R = [[[x[e_s(q, j, ql)] for ql in range(4)] for j in range(32)] for q in range(NQE)]
+    layer_s_off(R, 0, 0, True)
+    layer_s_off(R, 1, 0, True)
+    swap_sb(R)
+    for b in range(2, 7):
+        layer_b_off(R, b, 0, True)
+    R = xpose_bt_e(R)
+    layer_te(R, 7, 0, True)
+    layer_te(R, 8, 0, True)
+    derivative_te(R)
+    layer_te(R, 8, 0, False)
+    layer_te(R, 7, 0, False)
+    R = xpose_bt_e(R)
+    for b in range(6, 1, -1):
+        layer_b_off(R, b, 0, False)
+    swap_sb(R)
+    layer_s_off(R, 1, 0, False)
+    layer_s_off(R, 0, 0, False)
+    got = []
+    for e in range(n):
+        q, j, ql = _inv_s(e)
+        got.append(R[q][j][ql])
+    assert got == ref

@@ -52,5 +52,14 @@ case "$1" in
   val1)  # round 6: the whole tree -- every GPU test, the default bench line and its trace, the headline counters
     bash tools/gpu_final.sh && bash tools/gpu_profile.sh r06 counters
     ;;
+  val2)  # round 6: k = 256 quarter-lane decoder and 1,024-thread wide kernels (A/B), then the whole tree
+    DAGPU_LIB=celestia-app_amd/libdagpu.so timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_gf16.py > gpurun_out/r06_val2_gf16.log 2>&1
+    rc=$?; echo "gf16 tests rc=$rc"; tail -2 gpurun_out/r06_val2_gf16.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 256 --batch 8 --steps 10 --warmup 2" q256= h256=lib:celestia-app_amd/libdagpu_h256.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 1024 --batch 1 --steps 3 --warmup 1" w1024= w512=lib:celestia-app_amd/libdagpu_w512.so && \
+    bash tools/gpu_ab.sh --rounds 1 "bench:--mode repair --k 2048 --batch 1 --steps 2 --warmup 1" w1024= w512=lib:celestia-app_amd/libdagpu_w512.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode split --split-k 1024 --steps 10 --warmup 2" w1024= w512=lib:celestia-app_amd/libdagpu_w512.so && \
+    bash tools/gpu_final.sh
+    ;;
   *) echo "unknown step $1"; exit 2;;
 esac
