@@ -1134,6 +1134,29 @@ hipError_t read_small(void* dst, const void* src, size_t bytes, Mailbox& mb, hip
   return e;
 }
 
+// The round counters a vec_count_round launch left in the mailbox: spin on its
+// sequence word (kernels queued behind that launch keep the stream busy, so
+// the stream itself is not waited for); the stream is polled now and then, for
+// errors and for a word that never arrives (then the counters are copied).
+hipError_t wait_round_counters(int32_t* cnt, const RoundCounters& rc, Mailbox& mb, hipStream_t s) {
+  const volatile int32_t* word = rc.host + kCtrRead;
+  for (unsigned spin = 0;; spin++) {
+    if (*word == rc.seq) {
+      __atomic_thread_fence(__ATOMIC_ACQUIRE);
+      memcpy(cnt, (const void*)rc.host, kCtrRead * sizeof(int32_t));
+      return hipSuccess;
+    }
+    if ((spin & 1023) == 1023) {
+      const hipError_t e = hipStreamQuery(s);
+      if (e == hipSuccess && *word != rc.seq) return read_small(cnt, rc.ctr, kCtrRead * sizeof(int32_t), mb, s);
+      if (e != hipSuccess && e != hipErrorNotReady) return e;
+    }
+    __builtin_ia32_pause();
+  }
+}
+
+std::atomic<int32_t> g_round_seq{1};
+
 // rsmt2d Repair for n same-k squares resident on the device (see repair.hip).
 // d_byz (optional, n * 4 int32): failing axis per square; asking for it makes
 // the call resolve crossword failures in rsmt2d's order (exact_repair).
@@ -1148,8 +1171,7 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
   HIP_TRY(ctx, hipMemcpyAsync(r.p0, d_present, n * w * w, hipMemcpyDeviceToDevice, s));
   HIP_TRY(ctx, hipMemsetAsync(r.bits, 0, n * sizeof(int32_t), s));
   HIP_TRY(ctx, hipMemsetAsync(r.parity_bad, 0, n * 2 * w * sizeof(int32_t), s));
-  HIP_TRY(ctx, hipMemsetAsync(r.counters + 5, 0, 2 * sizeof(int32_t), s));  // [5] complete axes, [6] deferred squares
-  HIP_TRY(ctx, hipMemsetAsync(r.counters + 8, 0, 3 * sizeof(int32_t), s));  // [8..10] planned fills / decodes
+  HIP_TRY(ctx, hipMemsetAsync(r.counters, 0, kCtrSlots * sizeof(int32_t), s));  // kernels.hpp kCtr*
   int64_t rounds_run = 0, deferred_run = 0;
   HIP_TRY(ctx, launch_axis_complete(d_present, (int)k, (long)n, r.complete_before, s, r.counters + 5));
   // prerepairSanityCheck: complete axes must satisfy parity == Encode(data).
@@ -1206,21 +1228,37 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
   const int max_rounds = 4 * (int)w + 4;
   Mailbox mb_own(mb_in ? nullptr : ctx);
   Mailbox& mb = mb_in ? *mb_in : mb_own;
+  // Per round: one launch counts both axes and leaves the counters in the
+  // mailbox (RoundCounters), the host picks the axis, and the round's last
+  // launch (launch_rs_mark_round) clears the next round's counts: no memsets
+  // or copies between the kernels of a round.
+  RoundCounters rcnt{r.counters, mb.p ? (int32_t*)mb.p : nullptr, 0};
   for (int pass = 0; pass < 2; pass++) {
     long deferred_total = 0;
     int last_ax = -1;
-    HIP_TRY(ctx, hipMemsetAsync(r.counters, 0, 4 * sizeof(int32_t), s));  // [2] is read every round
+    if (pass > 0) {  // (the repair's first memset covers pass 0)
+      HIP_TRY(ctx, hipMemsetAsync(r.counters, 0, (kCtrPairsRev + 1) * sizeof(int32_t), s));
+      HIP_TRY(ctx, hipMemsetAsync(r.counters + kCtrDeferSquares, 0, 2 * sizeof(int32_t), s));
+    }
     for (int round = 0; round < max_rounds; round++) {
       DecodeArgs dr = axis_decode_args(k, n, d_eds, d_present, 0, r);
       DecodeArgs dc = axis_decode_args(k, n, d_eds, d_present, 1, r);
       // decodable vectors and counts of both axes (no locators yet)
       dr.vec_counts = r.counts[0];
       dc.vec_counts = r.counts[1];
-      HIP_TRY(ctx, hipMemsetAsync(r.counters, 0, 2 * sizeof(int32_t), s));
-      HIP_TRY(ctx, launch_vec_count(dr, s));
-      HIP_TRY(ctx, launch_vec_count(dc, s));
-      int32_t cnt[11] = {};
-      HIP_TRY(ctx, read_small(cnt, r.counters, sizeof cnt, mb, s));
+      rcnt.seq = g_round_seq.fetch_add(1) & 0x7fffffff;
+      HIP_TRY(ctx, launch_vec_count_round(dr, dc, rcnt, s));
+      // Few vectors (a launch is mostly latency): both axes' candidate locator
+      // heads while the host reads the counts; else the chosen axis' after it.
+      const bool early_heads = (long)n * w <= 8192;
+      if (early_heads) HIP_TRY(ctx, launch_errloc_heads2(dr, &dc, s));
+      int32_t cnt[kCtrRead] = {};
+      if (rcnt.host) {
+        HIP_TRY(ctx, wait_round_counters(cnt, rcnt, mb, s));
+      } else {
+        HIP_TRY(ctx, read_small(cnt, r.counters, sizeof cnt, mb, s));
+      }
+      cnt[kCtrDeferred] = cnt[kCtrDeferredPrev];  // the previous round's plan
       {  // schedule totals so far (diagnostics): plans of the earlier rounds are complete;
          // a started Repair writes its slot's copy (published at its join)
         std::unique_lock<std::mutex> g(ctx->prof_mu, std::defer_lock);
@@ -1246,7 +1284,6 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
       last_ax = ax;
       DecodeArgs& d = ax == 0 ? dr : dc;
       if (shortcut) {
-        HIP_TRY(ctx, hipMemsetAsync(r.counters + 2, 0, 3 * sizeof(int32_t), s));
         const long w_ = w;
         EncodeArgs e{};
         e.in = d_eds;
@@ -1307,17 +1344,17 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
       }
       // locators of the vectors left to the decoder (fill redos included)
       d.locators_only = 1;
-      HIP_TRY(ctx, launch_rs_errlocs(d, s));
+      if (!early_heads) HIP_TRY(ctx, launch_errloc_heads2(d, nullptr, s));
+      HIP_TRY(ctx, launch_rs_errlocs_only(d, s));
       {
         ProfScope p(ctx, 5, s);
         HIP_TRY(ctx, launch_rs_decode_only(d, s, false));
       }
-      HIP_TRY(ctx, launch_rs_mark_present(d, d.flags, s));
-      if (shortcut) HIP_TRY(ctx, launch_rs_mark_present(d, r.fill, s, r.known + (long)ax * n * w));
+      HIP_TRY(ctx, launch_rs_mark_round(d, shortcut ? r.fill : nullptr,
+                                        shortcut ? r.known + (long)ax * n * w : nullptr, r.counters, s));
     }
     if (!shortcut || deferred_total == 0) break;
     // deferred vectors whose codeword property is not implied: compare-mode encodes
-    HIP_TRY(ctx, hipMemsetAsync(r.counters + 6, 0, sizeof(int32_t), s));
     HIP_TRY(ctx, launch_repair_defer_check(r.deferred, r.known, (int)k, (long)n, r.check, s, r.counters + 6));
     int32_t left = 0;  // squares whose deferred axes are not proven codewords
     HIP_TRY(ctx, read_small(&left, r.counters + 6, sizeof left, mb, s));

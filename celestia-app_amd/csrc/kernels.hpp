@@ -140,6 +140,39 @@ __device__ __forceinline__ bool vec_selected(const DecodeArgs& a, long v) {
 
 // vector whose error locators vector v uses
 __device__ __forceinline__ long err_vec(const DecodeArgs& a, long v) { return a.err_head ? a.err_head[v] : v; }
+// Round 6: the flag-by-flag check of a candidate head (errloc_heads_kernel:
+// the first vector of the square with an equal key) runs inside the locator
+// kernels.  Returns v's head: the candidate when the two vectors' presence
+// flags agree one by one, else v itself (a key collision; err_head[v] is
+// rewritten, and no other vector has v as its candidate).  Block-wide: every
+// thread of the block calls it for the same v.
+__device__ __forceinline__ bool err_flags_differ(const DecodeArgs& a, long v, long hv, int first, int step) {
+  const long sq = v / a.nvec;
+  const uint8_t* pv = a.present + sq * a.p_sq_stride + (v - sq * a.nvec) * a.p_vec_stride;
+  const uint8_t* pu = a.present + sq * a.p_sq_stride + (hv - sq * a.nvec) * a.p_vec_stride;
+  bool diff = false;
+  for (int i = first; i < 2 * a.k; i += step)
+    diff |= (pv[(long)i * a.p_shard_stride] != 0) != (pu[(long)i * a.p_shard_stride] != 0);
+  return diff;
+}
+__device__ __forceinline__ long err_head_checked_block(const DecodeArgs& a, long v) {
+  if (!a.err_head) return v;
+  const long hv = a.err_head[v];
+  if (hv == v) return v;  // uniform
+  const bool diff = err_flags_differ(a, v, hv, threadIdx.x, blockDim.x);
+  if (!__syncthreads_or(diff)) return hv;
+  if (threadIdx.x == 0) a.err_head[v] = (int32_t)v;
+  return v;
+}
+// the same for one wave per vector
+__device__ __forceinline__ long err_head_checked_wave(const DecodeArgs& a, long v, int lane) {
+  if (!a.err_head) return v;
+  const long hv = a.err_head[v];
+  if (hv == v) return v;  // uniform per wave
+  if (!__any(err_flags_differ(a, v, hv, lane, 64))) return hv;
+  if (lane == 0) a.err_head[v] = (int32_t)v;
+  return v;
+}
 // does vector v (decodable) compute the locators of its head hv?
 __device__ __forceinline__ bool err_computes(const DecodeArgs& a, long v, long hv) {
   return hv == v || (a.locators_only && a.flags[hv] == 0);
@@ -169,6 +202,11 @@ hipError_t launch_rs_prepare(int k);
 hipError_t leo16w_prepare();
 hipError_t launch_rs_encode(int k, const EncodeArgs& a, hipStream_t s);
 hipError_t launch_rs_errlocs(const DecodeArgs& a, hipStream_t s);
+// the two halves of launch_rs_errlocs: candidate heads (of a, and of a1 when
+// given, in the same launches) and the locators (whose kernels check the
+// candidates flag by flag)
+hipError_t launch_errloc_heads2(const DecodeArgs& a, const DecodeArgs* a1, hipStream_t s);
+hipError_t launch_rs_errlocs_only(const DecodeArgs& a, hipStream_t s);
 hipError_t launch_rs_decode_only(const DecodeArgs& a, hipStream_t s, bool mark_present);
 hipError_t launch_rs_decode(const DecodeArgs& a, hipStream_t s, bool mark_present);
 
@@ -230,10 +268,36 @@ hipError_t launch_repair_defer_check(int32_t* deferred, const int32_t* known, in
 // vector; flags[v], vec_counts[v] (when set) and *ndecodable as the locator pass
 // would leave them.
 hipError_t launch_vec_count(const DecodeArgs& a, hipStream_t s);
+// Repair round counters (int32 slots of the 64-slot counters array):
+// decodable rows / columns of the round (vec_count), deferrals of the round's
+// plan, its fill pair counts, complete axes before the repair, squares left for
+// the deferral check, the previous round's deferrals (moved there by the next
+// round's count launch, so the host reads it with the round's counts), the
+// plan's totals (3 slots), the count launch's last-block ticket.  The host
+// reads slots [0, kCtrRead).
+constexpr int kCtrRowsDec = 0, kCtrColsDec = 1, kCtrDeferred = 2, kCtrPairs = 3, kCtrPairsRev = 4,
+              kCtrComplete = 5, kCtrDeferSquares = 6, kCtrDeferredPrev = 7, kCtrPlan = 8, kCtrRead = 11,
+              kCtrTicket = 12, kCtrSlots = 64;
+struct RoundCounters {
+  int32_t* ctr;   // device counters (kCtrSlots)
+  int32_t* host;  // optional: page-locked host copy of slots [0, kCtrRead), written by the last block,
+                  // then host[kCtrRead] = seq (the host spins on it, not on the stream)
+  int32_t seq;
+};
+// Both axes' vec_count of a Repair round in one launch plus the counter
+// bookkeeping above.  Slots kCtrRowsDec / kCtrColsDec must be 0 on entry
+// (the previous round's launch_rs_mark_round clears them).
+hipError_t launch_vec_count_round(const DecodeArgs& a0, const DecodeArgs& a1, const RoundCounters& rc,
+                                  hipStream_t s);
 // presence += vectors with flags[v] != 0 (axis given by the args); with
 // `known` ([sq][idx] of that axis), known[v] = 0 where a.flags[v] is set too
 hipError_t launch_rs_mark_present(const DecodeArgs& a, const int32_t* flags, hipStream_t s,
                                   int32_t* known = nullptr);
+// The end of a Repair round in one launch: presence += vectors flagged in
+// a.flags (decoded) or fill (optional, filled); known[v] = 0 where both are
+// set; zero2[0..1] (optional) := 0 for the next round's counts.
+hipError_t launch_rs_mark_round(const DecodeArgs& a, const int32_t* fill, int32_t* known, int32_t* zero2,
+                                hipStream_t s);
 // (optional) pre_fail[sq] = 1 where the pre-repair check failed
 hipError_t launch_finalize_repair(const int32_t* bits, const int32_t* complete_before, const int32_t* root_bad,
                                   const int32_t* parity_bad, int k, long nsq, int32_t* status, int32_t* byz,

@@ -287,16 +287,15 @@ __device__ __forceinline__ void vec_count_finish(const DecodeArgs& a, long v, in
 // 16-flag loads each lie inside one half (k >= 16, aligned), one row per wave
 // otherwise (a wave per row spent most of its time launching and reducing:
 // 35 us for 256 k = 128 squares).
-__global__ __launch_bounds__(1024) void vec_count_rows_kernel(DecodeArgs a) {
-  __shared__ int blk_cnt;
-  if (threadIdx.x == 0) blk_cnt = 0;
+__device__ __forceinline__ void vec_count_rows_block(const DecodeArgs& a, long bid, int* blk_cnt) {
+  if (threadIdx.x == 0) *blk_cnt = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int k = a.k, n = 2 * k;
   const long nv = a.nsq * a.nvec;
   if (k >= 16 && ((uintptr_t)a.present & 15) == 0 && (a.p_vec_stride & 15) == 0 && (a.p_sq_stride & 15) == 0) {
     // a 16-flag load straddling index k would count parity flags as data: k >= 16
-    const long v = ((long)blockIdx.x * 16 + wave) * 4 + (lane >> 4);
+    const long v = (bid * 16 + wave) * 4 + (lane >> 4);
     const int sl = lane & 15;
     int sys = 0, tot = 0;
     if (v < nv) {
@@ -314,9 +313,9 @@ __global__ __launch_bounds__(1024) void vec_count_rows_kernel(DecodeArgs a) {
       sys += __shfl_xor(sys, off);
       tot += __shfl_xor(tot, off);
     }
-    if (sl == 0 && v < nv) vec_count_finish(a, v, sys, tot, &blk_cnt);
+    if (sl == 0 && v < nv) vec_count_finish(a, v, sys, tot, blk_cnt);
   } else {
-    const long v = (long)blockIdx.x * 16 + wave;  // wave-uniform
+    const long v = bid * 16 + wave;  // wave-uniform
     if (v < nv) {
       const long sq = v / a.nvec;
       const uint8_t* pres = a.present + sq * a.p_sq_stride + (v - sq * a.nvec) * a.p_vec_stride;
@@ -331,22 +330,21 @@ __global__ __launch_bounds__(1024) void vec_count_rows_kernel(DecodeArgs a) {
         sys += __shfl_xor(sys, off);
         tot += __shfl_xor(tot, off);
       }
-      if (lane == 0) vec_count_finish(a, v, sys, tot, &blk_cnt);
+      if (lane == 0) vec_count_finish(a, v, sys, tot, blk_cnt);
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0 && blk_cnt && a.ndecodable) atomicAdd(a.ndecodable, blk_cnt);
+  if (threadIdx.x == 0 && *blk_cnt && a.ndecodable) atomicAdd(a.ndecodable, *blk_cnt);
 }
 
-__global__ __launch_bounds__(1024) void vec_count_cols_kernel(DecodeArgs a) {
-  __shared__ int blk_cnt;
-  __shared__ int acc_sys[64], acc_tot[64];
+__device__ __forceinline__ void vec_count_cols_block(const DecodeArgs& a, long bid, int* blk_cnt, int* acc_sys,
+                                                     int* acc_tot) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long nb = (a.nvec + 63) / 64;
-  const long sq = blockIdx.x / nb;
-  const long vec = (blockIdx.x - sq * nb) * 64 + lane;
+  const long sq = bid / nb;
+  const long vec = (bid - sq * nb) * 64 + lane;
   if (threadIdx.x < 64) acc_sys[threadIdx.x] = acc_tot[threadIdx.x] = 0;
-  if (threadIdx.x == 0) blk_cnt = 0;
+  if (threadIdx.x == 0) *blk_cnt = 0;
   __syncthreads();
   const int k = a.k, n = 2 * k;
   if (vec < a.nvec) {
@@ -362,25 +360,80 @@ __global__ __launch_bounds__(1024) void vec_count_cols_kernel(DecodeArgs a) {
     if (tot) atomicAdd(&acc_tot[lane], tot);
   }
   __syncthreads();
-  if (wave == 0 && vec < a.nvec) vec_count_finish(a, sq * a.nvec + vec, acc_sys[lane], acc_tot[lane], &blk_cnt);
+  if (wave == 0 && vec < a.nvec) vec_count_finish(a, sq * a.nvec + vec, acc_sys[lane], acc_tot[lane], blk_cnt);
   __syncthreads();
-  if (threadIdx.x == 0 && blk_cnt && a.ndecodable) atomicAdd(a.ndecodable, blk_cnt);
+  if (threadIdx.x == 0 && *blk_cnt && a.ndecodable) atomicAdd(a.ndecodable, *blk_cnt);
 }
 
-// the 4-rows-per-wave layout of vec_count_rows_kernel (same condition as the kernel's)
+// the 4-rows-per-wave layout of vec_count_rows_block (same condition as the block's)
 static bool vec_rows_packed(const DecodeArgs& a) {
   return a.k >= 16 && ((uintptr_t)a.present & 15) == 0 && (a.p_vec_stride & 15) == 0 && (a.p_sq_stride & 15) == 0;
 }
+static long vec_count_blocks(const DecodeArgs& a) {
+  const long nv = a.nsq * a.nvec;
+  if (nv <= 0) return 0;
+  if (a.p_shard_stride == 1) return vec_rows_packed(a) ? (nv + 63) / 64 : (nv + 15) / 16;
+  return a.nsq * ((a.nvec + 63) / 64);
+}
+
+__device__ __forceinline__ void vec_count_block(const DecodeArgs& a, long bid, int* blk_cnt, int* acc_sys,
+                                                int* acc_tot) {
+  if (a.p_shard_stride == 1) vec_count_rows_block(a, bid, blk_cnt);
+  else vec_count_cols_block(a, bid, blk_cnt, acc_sys, acc_tot);
+}
+
+__global__ __launch_bounds__(1024) void vec_count_kernel(DecodeArgs a) {
+  __shared__ int blk_cnt;
+  __shared__ int acc_sys[64], acc_tot[64];
+  vec_count_block(a, blockIdx.x, &blk_cnt, acc_sys, acc_tot);
+}
 
 hipError_t launch_vec_count(const DecodeArgs& a, hipStream_t s) {
-  const long nv = a.nsq * a.nvec;
-  if (nv <= 0) return hipSuccess;
-  if (a.p_shard_stride == 1)
-    hipLaunchKernelGGL(vec_count_rows_kernel,
-                       dim3((unsigned)(vec_rows_packed(a) ? (nv + 63) / 64 : (nv + 15) / 16)), dim3(1024), 0, s, a);
-  else
-    hipLaunchKernelGGL(vec_count_cols_kernel, dim3((unsigned)(a.nsq * ((a.nvec + 63) / 64))), dim3(1024), 0, s,
-                       a);
+  const long nb = vec_count_blocks(a);
+  if (nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(vec_count_kernel, dim3((unsigned)nb), dim3(1024), 0, s, a);
+  return hipGetLastError();
+}
+
+// Both axes of a Repair round in one launch (blocks [0, nb0) count axis a0,
+// the rest a1), plus the round's counter bookkeeping (see RoundCounters):
+// block 0 moves the previous plan's deferral count to its read slot and clears
+// the plan's counters, and the last block to finish copies the counters to the
+// host mailbox, so the host's read needs no copy of its own.
+__global__ __launch_bounds__(1024) void vec_count_round_kernel(DecodeArgs a0, DecodeArgs a1, long nb0,
+                                                               RoundCounters rc) {
+  __shared__ int blk_cnt;
+  __shared__ int acc_sys[64], acc_tot[64];
+  __shared__ int last_s;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    atomicExch(rc.ctr + kCtrDeferredPrev, atomicExch(rc.ctr + kCtrDeferred, 0));
+    atomicExch(rc.ctr + kCtrPairs, 0);
+    atomicExch(rc.ctr + kCtrPairsRev, 0);
+  }
+  if ((long)blockIdx.x < nb0) vec_count_block(a0, blockIdx.x, &blk_cnt, acc_sys, acc_tot);
+  else vec_count_block(a1, blockIdx.x - nb0, &blk_cnt, acc_sys, acc_tot);
+  if (!rc.host) return;  // uniform
+  if (threadIdx.x == 0) {
+    // This thread's counter atomics are performed (their completion waited
+    // for) before its ticket; no fence: an agent-scope fence here writes back
+    // and invalidates the XCD's L2 in every block (2x the launch's time at
+    // 2,048 blocks).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last_s = atomicAdd(rc.ctr + kCtrTicket, 1) == (int)gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last_s || threadIdx.x != 0) return;
+  for (int i = 0; i < kCtrRead; i++) rc.host[i] = atomicAdd(rc.ctr + i, 0);
+  atomicExch(rc.ctr + kCtrTicket, 0);
+  __threadfence_system();  // the counters before the sequence number
+  ((volatile int32_t*)rc.host)[kCtrRead] = rc.seq;
+}
+
+hipError_t launch_vec_count_round(const DecodeArgs& a0, const DecodeArgs& a1, const RoundCounters& rc,
+                                  hipStream_t s) {
+  const long nb0 = vec_count_blocks(a0), nb1 = vec_count_blocks(a1);
+  if (nb0 + nb1 <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(vec_count_round_kernel, dim3((unsigned)(nb0 + nb1)), dim3(1024), 0, s, a0, a1, nb0, rc);
   return hipGetLastError();
 }
 
@@ -525,24 +578,31 @@ __global__ __launch_bounds__(256) void mark_flagged_kernel(DecodeArgs a, const i
 // The same over the whole presence map of square-major [sq][r][c] bytes, one
 // dword (4 columns) per thread: a row axis marks whole dwords of flagged rows,
 // a column axis ORs in the bytes of flagged columns; threads gid < nsq * w
-// also do the known[] update of vector gid.
-__global__ __launch_bounds__(256) void mark_flagged_map_kernel(DecodeArgs a, const int32_t* flags, int32_t* known,
-                                                               int rows) {
+// also do the known[] update of vector gid.  A vector is flagged in flags or
+// (optional) flags2; the known[] update follows flags2 when it is given.
+// zero2 (optional): two counters cleared for the next Repair round.
+__global__ __launch_bounds__(256) void mark_flagged_map_kernel(DecodeArgs a, const int32_t* flags,
+                                                               const int32_t* flags2, int32_t* known, int rows,
+                                                               int32_t* zero2) {
   const int w = 2 * a.k, w4 = w / 4;
   const long gid = (long)blockIdx.x * 256 + threadIdx.x;
   const long nv = a.nsq * w;
-  if (known && gid < nv && flags[gid] && a.flags[gid]) known[gid] = 0;
+  if (zero2 && gid < 2) zero2[gid] = 0;
+  const int32_t* kf = flags2 ? flags2 : flags;
+  if (known && gid < nv && kf[gid] && a.flags[gid]) known[gid] = 0;
   if (gid >= nv * w4) return;
   const long sq = gid / ((long)w * w4);
   const long rem = gid - sq * (long)w * w4;
   const int r = (int)(rem / w4), c = 4 * (int)(rem - (long)r * w4);
   uint32_t* p = (uint32_t*)(a.present + sq * a.p_sq_stride + (long)r * w + c);
   const int32_t* f = flags + sq * w;
+  const int32_t* f2 = flags2 ? flags2 + sq * w : nullptr;
+  auto flagged = [&](int i) -> bool { return f[i] || (f2 && f2[i]); };
   if (rows) {
-    if (f[r]) *p = 0x01010101u;
+    if (flagged(r)) *p = 0x01010101u;
   } else {
-    const uint32_t set = (f[c] ? 0x1u : 0u) | (f[c + 1] ? 0x100u : 0u) | (f[c + 2] ? 0x10000u : 0u) |
-                         (f[c + 3] ? 0x1000000u : 0u);
+    const uint32_t set = (flagged(c) ? 0x1u : 0u) | (flagged(c + 1) ? 0x100u : 0u) |
+                         (flagged(c + 2) ? 0x10000u : 0u) | (flagged(c + 3) ? 0x1000000u : 0u);
     if (set) {
       const uint32_t x = *p;
       // a flagged byte becomes exactly 1 (the decoders test presence != 0)
@@ -555,20 +615,43 @@ __global__ __launch_bounds__(256) void mark_flagged_map_kernel(DecodeArgs a, con
   }
 }
 
+static bool mark_map_ok(const DecodeArgs& a, bool& rows) {
+  const long w = 2L * a.k;
+  rows = a.p_vec_stride == w && a.p_shard_stride == 1;
+  const bool cols = a.p_vec_stride == 1 && a.p_shard_stride == w;
+  return a.nvec == w && w % 4 == 0 && a.p_sq_stride == w * w && (rows || cols) && ((uintptr_t)a.present & 3) == 0;
+}
+
 hipError_t launch_rs_mark_present(const DecodeArgs& a, const int32_t* flags, hipStream_t s, int32_t* known) {
   const long nv = a.nsq * a.nvec;
   if (nv <= 0) return hipSuccess;
-  const long w = 2L * a.k;
-  const bool rows = a.p_vec_stride == w && a.p_shard_stride == 1;
-  const bool cols = a.p_vec_stride == 1 && a.p_shard_stride == w;
-  if (a.nvec == w && w % 4 == 0 && a.p_sq_stride == w * w && (rows || cols) && ((uintptr_t)a.present & 3) == 0) {
+  bool rows = false;
+  if (mark_map_ok(a, rows)) {
+    const long w = 2L * a.k;
     const long threads = a.nsq * w * (w / 4);
     hipLaunchKernelGGL(mark_flagged_map_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, a, flags,
-                       known, rows ? 1 : 0);
+                       (const int32_t*)nullptr, known, rows ? 1 : 0, (int32_t*)nullptr);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(mark_flagged_kernel, dim3((unsigned)nv), dim3(256), 0, s, a, flags, known);
   return hipGetLastError();
+}
+
+hipError_t launch_rs_mark_round(const DecodeArgs& a, const int32_t* fill, int32_t* known, int32_t* zero2,
+                                hipStream_t s) {
+  const long nv = a.nsq * a.nvec;
+  bool rows = false;
+  if (nv > 0 && mark_map_ok(a, rows)) {
+    const long w = 2L * a.k;
+    const long threads = a.nsq * w * (w / 4);
+    hipLaunchKernelGGL(mark_flagged_map_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, a, a.flags,
+                       fill, known, rows ? 1 : 0, zero2);
+    return hipGetLastError();
+  }
+  hipError_t e = launch_rs_mark_present(a, a.flags, s, nullptr);
+  if (e == hipSuccess && fill) e = launch_rs_mark_present(a, fill, s, known);
+  if (e == hipSuccess && zero2) e = hipMemsetAsync(zero2, 0, 2 * sizeof(int32_t), s);
+  return e;
 }
 
 }  // namespace dagpu

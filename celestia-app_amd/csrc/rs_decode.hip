@@ -80,7 +80,9 @@ __global__ __launch_bounds__(64 * kErrVecs) void leo8_errlocs_kernel(DecodeArgs 
   __syncthreads();
   const long v = (long)blockIdx.x * kErrVecs + wave;  // flattened (square, vector)
   // locators_only: flagged vectors that compute their head's locators (uniform per wave)
-  const bool skip = v >= a.nsq * a.nvec || (a.locators_only && (!a.flags[v] || !err_computes(a, v, err_vec(a, v))));
+  bool skip = v >= a.nsq * a.nvec || (a.locators_only && !a.flags[v]);
+  const long hv = skip ? v : err_head_checked_wave(a, v, lane);
+  skip = skip || (a.locators_only && !err_computes(a, v, hv));
   if (!skip) {
     uint32_t* e = e_all[wave];
     const long sq = v / a.nvec, vec = v % a.nvec;
@@ -107,7 +109,6 @@ __global__ __launch_bounds__(64 * kErrVecs) void leo8_errlocs_kernel(DecodeArgs 
     }
     // uniform per wave; a vector sharing an earlier vector's erasure pattern
     // uses that vector's locators
-    const long hv = err_vec(a, v);
     if (decode && err_computes(a, v, hv)) {
       wave_sync();
       fwht256_wave(e, n, lane);

@@ -209,7 +209,9 @@ __global__ __launch_bounds__(kFoldThreads) void leo16_errlocs_fold_kernel(Decode
   const long sq = v / a.nvec, vec = v % a.nvec;
   constexpr int k = N / 2;
   const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
-  if (a.locators_only && (!a.flags[v] || !err_computes(a, v, err_vec(a, v)))) return;  // uniform
+  if (a.locators_only && !a.flags[v]) return;  // uniform
+  const long hv = err_head_checked_block(a, v);
+  if (a.locators_only && !err_computes(a, v, hv)) return;  // uniform
   if (threadIdx.x == 0) cnt_s = 0;
   __syncthreads();
   int cnt = 0;
@@ -234,7 +236,6 @@ __global__ __launch_bounds__(kFoldThreads) void leo16_errlocs_fold_kernel(Decode
     }
   }
   if (!decode) return;  // uniform
-  const long hv = err_vec(a, v);
   if (!err_computes(a, v, hv)) return;  // shares an earlier vector's locators
   fwht_n<N>(e);
   const uint16_t* wf = g_wfold16[N == 1024];
@@ -1838,9 +1839,9 @@ __device__ __forceinline__ uint32_t key_mix(uint64_t m, int g) {
   return (uint32_t)x;
 }
 
-__global__ __launch_bounds__(1024) void errloc_key_rows_kernel(DecodeArgs a) {
+__device__ __forceinline__ void errloc_key_rows_block(const DecodeArgs& a, long bid) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const long gv = (long)blockIdx.x * 16 + wave;  // wave-uniform
+  const long gv = bid * 16 + wave;  // wave-uniform
   if (gv >= a.nsq * a.nvec) return;
   const long sq = gv / a.nvec;
   const long v = gv - sq * a.nvec;
@@ -1855,12 +1856,11 @@ __global__ __launch_bounds__(1024) void errloc_key_rows_kernel(DecodeArgs a) {
   if (lane == 0) a.err_key[gv] = (int32_t)key;
 }
 
-__global__ __launch_bounds__(1024) void errloc_key_cols_kernel(DecodeArgs a) {
-  __shared__ uint32_t acc[64];
+__device__ __forceinline__ void errloc_key_cols_block(const DecodeArgs& a, long bid, uint32_t* acc) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long nb = (a.nvec + 63) / 64;
-  const long sq = blockIdx.x / nb;
-  const long v = (blockIdx.x - sq * nb) * 64 + lane;
+  const long sq = bid / nb;
+  const long v = (bid - sq * nb) * 64 + lane;
   const int n = 2 * a.k;
   if (threadIdx.x < 64) acc[threadIdx.x] = 0;
   __syncthreads();
@@ -1879,12 +1879,28 @@ __global__ __launch_bounds__(1024) void errloc_key_cols_kernel(DecodeArgs a) {
   if (wave == 0 && v < a.nvec) a.err_key[sq * a.nvec + v] = (int32_t)acc[lane];
 }
 
+static long errloc_key_blocks(const DecodeArgs& a) {
+  return a.p_shard_stride == 1 ? (a.nsq * a.nvec + 15) / 16 : a.nsq * ((a.nvec + 63) / 64);
+}
+
+// keys of a0 (blocks < nb0), then of a1 (one launch for both axes of a Repair round)
+__global__ __launch_bounds__(1024) void errloc_key_kernel(DecodeArgs a0, DecodeArgs a1, long nb0) {
+  __shared__ uint32_t acc[64];
+  const bool second = (long)blockIdx.x >= nb0;
+  const DecodeArgs& a = second ? a1 : a0;
+  const long bid = second ? (long)blockIdx.x - nb0 : (long)blockIdx.x;
+  if (a.p_shard_stride == 1) errloc_key_rows_block(a, bid);
+  else errloc_key_cols_block(a, bid, acc);
+}
+
 // One workgroup per square (nvec <= kMaxHeadVec): keys in LDS, candidate head =
-// the first vector with an equal key.
+// the first vector with an equal key; squares of a0 (blocks < a0.nsq), then of a1.
 constexpr int kMaxHeadVec = 2 * kMaxK;
-__global__ __launch_bounds__(1024) void errloc_heads_kernel(DecodeArgs a) {
+__global__ __launch_bounds__(1024) void errloc_heads_kernel(DecodeArgs a0, DecodeArgs a1) {
   extern __shared__ int32_t key[];  // nvec
-  const long sq = blockIdx.x;
+  const bool second = (long)blockIdx.x >= a0.nsq;
+  const DecodeArgs& a = second ? a1 : a0;
+  const long sq = second ? (long)blockIdx.x - a0.nsq : (long)blockIdx.x;
   const int nvec = (int)a.nvec;
   const long v0 = sq * a.nvec;
   for (int t = threadIdx.x; t < nvec; t += 1024) key[t] = a.err_key[v0 + t];
@@ -1897,66 +1913,27 @@ __global__ __launch_bounds__(1024) void errloc_heads_kernel(DecodeArgs a) {
   }
 }
 
-// Candidate heads checked flag by flag (a key collision falls back to the
-// vector itself); the same two layouts as the key kernels.
-__global__ __launch_bounds__(1024) void errloc_verify_rows_kernel(DecodeArgs a) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const long gv = (long)blockIdx.x * 16 + wave;  // wave-uniform
-  if (gv >= a.nsq * a.nvec) return;
-  const long hv = a.err_head[gv];
-  if (hv == gv) return;
-  const long sq = gv / a.nvec;
-  const uint8_t* pv = a.present + sq * a.p_sq_stride + (gv - sq * a.nvec) * a.p_vec_stride;
-  const uint8_t* pu = a.present + sq * a.p_sq_stride + (hv - sq * a.nvec) * a.p_vec_stride;
-  bool diff = false;
-  for (int i = lane; i < 2 * a.k; i += 64) diff |= (pv[i] != 0) != (pu[i] != 0);
-  if (__builtin_amdgcn_ballot_w64(diff) != 0 && lane == 0) a.err_head[gv] = (int32_t)gv;
-}
-
-__global__ __launch_bounds__(1024) void errloc_verify_cols_kernel(DecodeArgs a) {
-  __shared__ int32_t bad[64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const long nb = (a.nvec + 63) / 64;
-  const long sq = blockIdx.x / nb;
-  const long v = (blockIdx.x - sq * nb) * 64 + lane;
-  if (threadIdx.x < 64) bad[threadIdx.x] = 0;
-  __syncthreads();
-  const long gv = sq * a.nvec + v;
-  const long hv = v < a.nvec ? a.err_head[gv] : gv;
-  if (v < a.nvec && hv != gv) {
-    const uint8_t* pv = a.present + sq * a.p_sq_stride + v * a.p_vec_stride;
-    const uint8_t* pu = a.present + sq * a.p_sq_stride + (hv - sq * a.nvec) * a.p_vec_stride;
-    bool diff = false;
-    for (int i = wave; i < 2 * a.k; i += 16)
-      diff |= (pv[(long)i * a.p_shard_stride] != 0) != (pu[(long)i * a.p_shard_stride] != 0);
-    if (diff) bad[lane] = 1;  // every writer stores the same value
-  }
-  __syncthreads();
-  if (wave == 0 && v < a.nvec && bad[lane]) a.err_head[gv] = (int32_t)gv;
-}
-
-hipError_t launch_errloc_heads(const DecodeArgs& a, hipStream_t s) {
+// Candidate heads of a (and of a1 when given, e.g. both axes of a Repair round
+// ahead of the axis choice); the flag-by-flag check of each candidate is the
+// locator kernels' err_head_checked_*.
+hipError_t launch_errloc_heads2(const DecodeArgs& a, const DecodeArgs* a1, hipStream_t s) {
   if (!a.err_key || !a.err_head) return hipSuccess;
+  if (a1 && (!a1->err_key || !a1->err_head || a1->nsq <= 0 || a1->nvec <= 0)) return hipErrorInvalidValue;
   const long nv = a.nsq * a.nvec;
   if (nv <= 0) return hipSuccess;
-  if (a.nvec > kMaxHeadVec) return hipErrorInvalidValue;
-  if (a.p_shard_stride == 1)
-    hipLaunchKernelGGL(errloc_key_rows_kernel, dim3((unsigned)((nv + 15) / 16)), dim3(1024), 0, s, a);
-  else
-    hipLaunchKernelGGL(errloc_key_cols_kernel, dim3((unsigned)(a.nsq * ((a.nvec + 63) / 64))), dim3(1024), 0,
-                       s, a);
+  if (a.nvec > kMaxHeadVec || (a1 && a1->nvec > kMaxHeadVec)) return hipErrorInvalidValue;
+  const DecodeArgs& b = a1 ? *a1 : a;
+  const long nb0 = errloc_key_blocks(a), nb1 = a1 ? errloc_key_blocks(b) : 0;
+  hipLaunchKernelGGL(errloc_key_kernel, dim3((unsigned)(nb0 + nb1)), dim3(1024), 0, s, a, b, nb0);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(errloc_heads_kernel, dim3((unsigned)a.nsq), dim3(1024), (size_t)a.nvec * 4, s, a);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  if (a.p_shard_stride == 1)
-    hipLaunchKernelGGL(errloc_verify_rows_kernel, dim3((unsigned)((nv + 15) / 16)), dim3(1024), 0, s, a);
-  else
-    hipLaunchKernelGGL(errloc_verify_cols_kernel, dim3((unsigned)(a.nsq * ((a.nvec + 63) / 64))), dim3(1024), 0,
-                       s, a);
+  const long nvec = a1 && b.nvec > a.nvec ? b.nvec : a.nvec;
+  hipLaunchKernelGGL(errloc_heads_kernel, dim3((unsigned)(a.nsq + (a1 ? b.nsq : 0))), dim3(1024),
+                     (size_t)nvec * 4, s, a, b);
   return hipGetLastError();
 }
+
+hipError_t launch_errloc_heads(const DecodeArgs& a, hipStream_t s) { return launch_errloc_heads2(a, nullptr, s); }
 
 hipError_t launch_rs_prepare(int k) {
   if (k <= 128) return hipSuccess;  // GF(2^8): constexpr tables
@@ -1969,10 +1946,13 @@ hipError_t launch_rs_prepare(int k) {
 hipError_t launch_rs_encode(int k, const EncodeArgs& a, hipStream_t s) {
   return k <= 128 ? launch_leo8_encode(k, a, s) : launch_leo16_encode(k, a, s);
 }
+hipError_t launch_rs_errlocs_only(const DecodeArgs& a, hipStream_t s) {
+  return a.k <= 128 ? launch_leo8_errlocs(a, s) : launch_leo16_errlocs(a, s);
+}
 hipError_t launch_rs_errlocs(const DecodeArgs& a, hipStream_t s) {
   hipError_t e = launch_errloc_heads(a, s);
   if (e != hipSuccess) return e;
-  return a.k <= 128 ? launch_leo8_errlocs(a, s) : launch_leo16_errlocs(a, s);
+  return launch_rs_errlocs_only(a, s);
 }
 hipError_t launch_rs_decode_only(const DecodeArgs& a, hipStream_t s, bool mark_present) {
   return a.k <= 128 ? launch_leo8_decode_only(a, s, mark_present)

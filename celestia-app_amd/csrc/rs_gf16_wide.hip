@@ -537,7 +537,9 @@ __global__ __launch_bounds__(kFoldThreads) void leo16w_errlocs_kernel(DecodeArgs
   const long sq = v / a.nvec, vec = v % a.nvec;
   const int k = a.k, n = 2 * k;
   const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
-  if (a.locators_only && (!a.flags[v] || !err_computes(a, v, err_vec(a, v)))) return;  // uniform
+  if (a.locators_only && !a.flags[v]) return;  // uniform
+  const long hv = err_head_checked_block(a, v);
+  if (a.locators_only && !err_computes(a, v, hv)) return;  // uniform
   if (threadIdx.x == 0) cnt_s = 0;
   __syncthreads();
   int cnt = 0;
@@ -562,7 +564,6 @@ __global__ __launch_bounds__(kFoldThreads) void leo16w_errlocs_kernel(DecodeArgs
     }
   }
   if (!decode) return;  // uniform
-  const long hv = err_vec(a, v);
   if (!err_computes(a, v, hv)) return;  // shares an earlier vector's locators
   fwht_rt(e, n);
   const uint16_t* wf = T.wfold + wf_off;
