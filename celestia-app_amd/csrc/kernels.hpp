@@ -26,7 +26,7 @@ constexpr int kMaxK = 8192;
 // at k >= 1024 the n x 32-B basis products (1 << b) * that factor, b < 16, from
 // which a wide decoder workgroup builds an element's table without gathers.
 constexpr long rs_err_tab_off(int k) { return 4L * k; }
-constexpr long rs_err_elem_bytes(int k) { return k <= 512 ? 80 : 32; }
+constexpr long rs_err_elem_bytes(int k) { return k <= 1024 ? 80 : 32; }
 constexpr long rs_err_bytes(int k) { return k <= 128 ? 256 : 4L * k + 2L * k * rs_err_elem_bytes(k); }
 
 // Per-square status bits written by the kernels (0 = OK).

@@ -40,7 +40,7 @@ __device__ uint16_t g_exp16[65536];
 __device__ uint16_t g_skew16[65536];
 // Folded Walsh weights for the n-point error-locator transform (n = 2k =
 // 512, 1024): g_wfold16[n == 1024][r] = sum_q walsh[q*n + r] mod 65535.
-__device__ uint16_t g_wfold16[2][1024];
+__device__ uint16_t g_wfold16[3][2048];
 
 __device__ __forceinline__ uint32_t mul16(uint32_t a, uint32_t lm) {
   if (a == 0) return 0;
@@ -238,7 +238,7 @@ __global__ __launch_bounds__(kFoldThreads) void leo16_errlocs_fold_kernel(Decode
   if (!decode) return;  // uniform
   if (!err_computes(a, v, hv)) return;  // shares an earlier vector's locators
   fwht_n<N>(e);
-  const uint16_t* wf = g_wfold16[N == 1024];
+  const uint16_t* wf = g_wfold16[N == 512 ? 0 : N == 1024 ? 1 : 2];
   for (int i = threadIdx.x; i < N; i += kFoldThreads) e[i] = (e[i] * (uint32_t)wf[i]) % kMod16;
   __syncthreads();
   fwht_n<N>(e);
@@ -348,7 +348,7 @@ __device__ __forceinline__ int opaque_s(int x) {
 // Positions < 2m = 1024 cover every encoder skew index (IFFT m-1+iend+2d <
 // 2m, FFT iend-1 < m) and every k = 512 decoder one (iend - 1 < n).
 // __constant__ so that the wave-uniform table reads become scalar loads.
-constexpr int kTabPos = 1024;
+constexpr int kTabPos = 2048;  // skew positions of the register kernels (n <= 2048)
 
 // 3/3/2 split (round 5): each byte of y in groups of 3, 3 and 2 bits, so a
 // symbol takes 6 lookups per output byte instead of 8.  A 3-bit group indexes
@@ -1194,7 +1194,8 @@ __device__ __forceinline__ void q_pos_tables(uint32_t* lds, int q, int lane) {
 template <int K>
 __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_decode_q_kernel(
     DecodeArgs a) {
-  constexpr int NQ = K / 64, LR = K == 512 ? 2 : 3, RPR = K == 512 ? 2 : 4, IMG1 = NQ * 5 * 1024;
+  constexpr int NQ = K / 64, LR = K == 1024 ? 1 : K == 512 ? 2 : 3, RPR = K == 1024 ? 1 : K == 512 ? 2 : 4,
+                IMG1 = NQ * 5 * 1024;
   // two rounds of the transposes / derivative (K = 512: 32 KiB each, 256: 16
   // KiB); the S-layer images (NQ x 7.5 KiB) in the same space before the first
   // transpose and after the last
@@ -1273,10 +1274,12 @@ __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
   xpose_bt_db<LR, RPR, 0>(w, lds, q, lane);  // rounds A B A B
   layer_t_q<true, 7, LR>(w);
   layer_t_q<true, 8, LR>(w);
-  if constexpr (K == 512) layer_t_q<true, 9, LR>(w);
+  if constexpr (K >= 512) layer_t_q<true, 9, LR>(w);
+  if constexpr (K >= 1024) layer_t_q<true, 10, LR>(w);
   derivative_tq<NQ>(w, lds, q, lane);  // A B A B
   // ---- FFT (fftDIT, skew index iend - 1) ----
-  if constexpr (K == 512) layer_t_q<false, 9, LR>(w);
+  if constexpr (K >= 1024) layer_t_q<false, 10, LR>(w);
+  if constexpr (K >= 512) layer_t_q<false, 9, LR>(w);
   layer_t_q<false, 8, LR>(w);
   layer_t_q<false, 7, LR>(w);
   xpose_bt_db<LR, RPR, 0>(w, lds, q, lane);  // A B A B
@@ -1660,13 +1663,13 @@ hipError_t ensure_tables() {
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_exp16), t.exp.data(), 65536 * 2)) != hipSuccess) return e;
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_skew16), t.skew.data(), 65536 * 2)) != hipSuccess) return e;
   {
-    std::vector<uint16_t> wf(2 * 1024, 0);
-    for (int f = 0; f < 2; f++) {
-      const int n = f ? 1024 : 512;
+    std::vector<uint16_t> wf(3 * 2048, 0);
+    for (int f = 0; f < 3; f++) {
+      const int n = 512 << f;
       for (int r = 0; r < n; r++) {
         uint64_t acc = 0;
         for (int q = 0; q < 65536 / n; q++) acc += t.walsh[(size_t)q * n + r];
-        wf[(size_t)f * 1024 + r] = (uint16_t)(acc % kMod16);
+        wf[(size_t)f * 2048 + r] = (uint16_t)(acc % kMod16);
       }
     }
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_wfold16), wf.data(), wf.size() * 2)) != hipSuccess) return e;
@@ -1725,11 +1728,11 @@ bool gf16_k_ok(int k) { return k >= 256 && k <= 512 && (k & (k - 1)) == 0; }
 
 // Wide squares (k > 512) and DAGPU_GF16_WIDE=1 (A/B of the wide kernels at
 // k = 256 / 512): the LDS-slice kernels of rs_gf16_wide.hip.
-static bool use_wide(int k) {
-  if (k > 512) return true;
+static bool wide_forced() {
   const char* e = sw(SW_GF16_WIDE);
   return e && e[0] == '1';
 }
+static bool use_wide(int k) { return k > 512 || wide_forced(); }
 
 // k = 256 / 512 encoders: the half-lane kernels, one workgroup per 256-B piece
 // of a vector's shards (a last partial piece: inactive lanes store nothing)
@@ -1761,20 +1764,35 @@ hipError_t launch_leo16_encode(int k, const EncodeArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_leo16_errlocs(const DecodeArgs& a, hipStream_t s) {
-  if (a.k > 512) return launch_leo16w_errlocs(a, s);
-  if (!gf16_k_ok(a.k)) return hipErrorInvalidValue;
+  if (a.k > 1024) return launch_leo16w_errlocs(a, s);
+  if (!gf16_k_ok(a.k) && a.k != 1024) return hipErrorInvalidValue;
   hipError_t e = ensure_tables();
   if (e != hipSuccess) return e;
   const long nv = a.nsq * a.nvec;
   if (nv <= 0) return hipSuccess;
   if (a.k == 256)
     hipLaunchKernelGGL(leo16_errlocs_fold_kernel<512>, dim3((unsigned)nv), dim3(kFoldThreads), 0, s, a);
-  else
+  else if (a.k == 512)
     hipLaunchKernelGGL(leo16_errlocs_fold_kernel<1024>, dim3((unsigned)nv), dim3(kFoldThreads), 0, s, a);
+  else  // k = 1024: the quarter-lane decoder's 80-B tables (the wide decoder reads the locators)
+    hipLaunchKernelGGL(leo16_errlocs_fold_kernel<2048>, dim3((unsigned)nv), dim3(kFoldThreads), 0, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_leo16_decode_only(const DecodeArgs& a, hipStream_t s, bool mark_present) {
+  if (a.k == 1024 && a.shard_bytes % 128 == 0 && !wide_forced()) {
+    // k = 1024: the quarter-lane decoder, 16 waves (one workgroup per CU), 128-B pieces
+    hipError_t e = ensure_tables();
+    if (e != hipSuccess) return e;
+    const long nv = a.nsq * a.nvec;
+    if (nv <= 0) return hipSuccess;
+    DecodeArgs b = a;
+    b.nchunk = a.shard_bytes / 128;
+    hipLaunchKernelGGL(leo16_decode_q_kernel<1024>, dim3((unsigned)(nv * b.nchunk)), dim3(1024), 0, s, b);
+    if ((e = hipGetLastError()) != hipSuccess || !mark_present) return e;
+    hipLaunchKernelGGL(mark_present16_kernel, dim3((unsigned)nv), dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
   if (use_wide(a.k)) return launch_leo16w_decode_only(a, s, mark_present);
   if (!gf16_k_ok(a.k) || a.shard_bytes % 64) return hipErrorInvalidValue;
   hipError_t e = ensure_tables();

@@ -577,7 +577,7 @@ __global__ __launch_bounds__(kFoldThreads) void leo16w_errlocs_kernel(DecodeArgs
   // one -- once per erasure pattern, so the decoder's workgroups (one per
   // column slice) build their tables from two coalesced 16-B loads instead of
   // 16 random exp gathers per element each.
-  if (a.k >= 1024) {
+  if (rs_err_elem_bytes(a.k) == 32) {  // (k = 1024: leo16_errlocs_fold_kernel<2048> writes 80-B tables)
     uint4* pbo = (uint4*)(a.err + hv * (long)rs_err_bytes(k) + rs_err_tab_off(k));
     for (int i = threadIdx.x, r = 0; i < n; i += kFoldThreads, r++) {
       const uint32_t lm0 = e[i] & 0xFFFFu;
@@ -620,9 +620,10 @@ __global__ __launch_bounds__(dec_threads<NG>()) void leo16w_decode_kernel(Decode
   uint8_t* base = a.data + sq * a.sq_stride + vec * a.vec_stride + col;
   const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
   const uint16_t* err = (const uint16_t*)(a.err + err_vec(a, v) * (long)rs_err_bytes(k));
-  // k >= 1024: the basis products leo16w_errlocs_kernel stored per element;
-  // k = 256 / 512 (DAGPU_GF16_WIDE A/B) has the register kernels' tables there
-  const uint8_t* pbase = k >= 1024 ? (const uint8_t*)err + rs_err_tab_off(k) : nullptr;
+  // k >= 2048: the basis products leo16w_errlocs_kernel stored per element;
+  // k <= 1024 has the register kernels' 80-B tables there (this kernel then
+  // reads the locators: DAGPU_GF16_WIDE A/B, shards off the 128-B grid)
+  const uint8_t* pbase = rs_err_elem_bytes(k) == 32 ? (const uint8_t*)err + rs_err_tab_off(k) : nullptr;
   // one thread per element: its table once, then its NG dword pairs
   for (int i = threadIdx.x; i < n; i += TH) {
     const long shard = i < k ? k + i : i - k;

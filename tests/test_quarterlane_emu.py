@@ -340,3 +340,95 @@ def test_quarterlane_decoder_k256_equals_leopard_loops(seed):
         q, j, ql = _inv_s(e)
         got.append(R[q][j][ql])
     assert got == ref
+
+
+# --- k = 1024 (n = 2048) through the same decoder template: 16 waves (1,024
+# threads, one workgroup per CU), T e = ql + 4 (j & 1) + 8 q + 128 (j >> 1)
+# (B <-> T: the 16 x 16 transpose of q with j >> 1, LR = 1), layers on bits 7-10
+NQ1K = 16
+
+
+def e_t1k(q, j, ql):
+    return ql + 4 * (j & 1) + 8 * q + 128 * (j >> 1)
+
+
+def xpose_bt_1k(R):
+    S = [[None] * 32 for _ in range(NQ1K)]
+    for q in range(NQ1K):
+        for jj in range(NQ1K):
+            for r in range(2):
+                S[jj][(q << 1) | r] = list(R[q][(jj << 1) | r])
+    return S
+
+
+def layer_t1k(R, b, inv):
+    """bits 7-10 in T: registers j, j + 2 << (b - 7); position 128 (jb >> 1) + d - 1"""
+    rd, d = 2 << (b - 7), 1 << b
+    for q, reg in enumerate(R):
+        for jb in range(0, 32, 2 * rd):
+            pos = 128 * (jb >> 1) + d - 1
+            for j in range(jb, jb + rd):
+                for ql in range(4):
+                    assert (e_t1k(q, j, ql) & ~(2 * d - 1)) + d - 1 == pos
+                    w = [reg[j][ql], reg[j + rd][ql]]
+                    bfly(w, 0, 1, pos, inv)
+                    reg[j][ql], reg[j + rd][ql] = w
+
+
+def derivative_t1k(R):
+    orig = [[list(x) for x in reg] for reg in R]
+    for c, reg in enumerate(R):
+        for j in range(32):
+            for ql in range(4):
+                acc = orig[c][j][ql]
+                for bit in (1, 2, 4, 8, 16):
+                    if not j & bit:
+                        acc ^= orig[c][j | bit][ql]
+                for wb in (1, 2, 4, 8):
+                    if not c & wb:
+                        acc ^= orig[c | wb][j][ql]
+                for qb in (1, 2):
+                    if not ql & qb:
+                        acc ^= orig[c][j][ql | qb]
+                reg[j][ql] = acc
+
+
+def test_k1024_layout_bijections():
+    assert {e_t1k(q, j, ql) for q in range(NQ1K) for j in range(32) for ql in range(4)} == set(range(2048))
+    assert {e_s(q, j, ql) for q in range(NQ1K) for j in range(32) for ql in range(4)} == set(range(2048))
+    R = [[[e_b(q, j, ql) for ql in range(4)] for j in range(32)] for q in range(NQ1K)]
+    T = xpose_bt_1k(R)
+    assert all(T[q][j][ql] == e_t1k(q, j, ql) for q in range(NQ1K) for j in range(32) for ql in range(4))
+
+
+def test_quarterlane_decoder_k1024_equals_leopard_loops():
+    rng = np.random.default_rng(21)
+    n = 2048
+    x = [int(v) for v in rng.integers(0, 65536, n)]
+    ref = list(x)
+    ref_ifft(ref, 0)
+    ref_derivative(ref)
+    ref_fft(ref, 0)
+    R = [[[x[e_s(q, j, ql)] for ql in range(4)] for j in range(32)] for q in range(NQ1K)]
+    layer_s_off(R, 0, 0, True)
+    layer_s_off(R, 1, 0, True)
+    swap_sb(R)
+    for b in range(2, 7):
+        layer_b_off(R, b, 0, True)
+    R = xpose_bt_1k(R)
+    for b in (7, 8, 9, 10):
+        layer_t1k(R, b, True)
+    derivative_t1k(R)
+    for b in (10, 9, 8, 7):
+        layer_t1k(R, b, False)
+    R = xpose_bt_1k(R)
+    for b in range(6, 1, -1):
+        layer_b_off(R, b, 0, False)
+    swap_sb(R)
+    layer_s_off(R, 1, 0, False)
+    layer_s_off(R, 0, 0, False)
+    got = []
+    for e in range(n):
+        q, j, ql = _inv_s(e)
+        got.append(R[q][j][ql])
+    assert got == ref

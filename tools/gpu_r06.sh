@@ -11,6 +11,15 @@ case "$1" in
     timeout -k 10 600 python -u bench.py > gpurun_out/r06_clean_bench.log 2>&1 || { echo "bench failed"; tail -5 gpurun_out/r06_clean_bench.log; exit 1; }
     tail -c 600 gpurun_out/r06_clean_bench.log
     ;;
+  q1k)  # round 6: quarter-lane k = 1024 decoder (16 waves, one workgroup per CU) vs the wide one
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_wide.py -k "not k8192 and not k4096" > gpurun_out/r06_q1k_wide.log 2>&1
+    rc=$?; echo "wide tests rc=$rc"; tail -3 gpurun_out/r06_q1k_wide.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_gf16.py tests/test_gpu_repair_fill.py > gpurun_out/r06_q1k_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r06_q1k_tests.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 1024 --batch 1 --steps 3 --warmup 1" new= wide=DAGPU_GF16_WIDE=1 base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 1 "bench:--mode repair --k 1024 --batch 2 --steps 3 --warmup 1" new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 1 "bench:--mode repair --k 512 --batch 2 --steps 5 --warmup 1" new= base=lib:celestia-app_amd/libdagpu_base.so
+    ;;
   ctl)  # round 6: Repair round control -- fused count/mark launches, mailbox counters, early candidate heads
     timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py tests/test_gpu_repair_async.py tests/test_gpu_parity.py tests/test_gpu_gf16.py tests/test_gpu_c_client.py > gpurun_out/r06_ctl_tests.log 2>&1
     rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r06_ctl_tests.log; [ $rc -eq 0 ] || exit $rc
