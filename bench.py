@@ -260,7 +260,7 @@ def gf16_kernel_names(k: int):
     (csrc/rs_gf16.hip / rs_gf16_wide.hip launch selection), as rocprofv3 /
     tools/pmc_stress.py name them."""
     if k == 512:  # round 6: the quarter-lane kernels
-        return "leo16_encode_q_kernel<false>", "leo16_decode_q_kernel<512>"
+        return "leo16_encode_q_kernel<512, false>", "leo16_decode_q_kernel<512>"
     if k == 256:
         return "leo16_encode_h_kernel<256, false>", "leo16_decode_h_kernel<256>"
     ng = {1024: 8, 2048: 8, 4096: 4, 8192: 2}  # slice widths (encoder m = k, decoder n = 2k)
@@ -268,7 +268,10 @@ def gf16_kernel_names(k: int):
     dg = {8: 8, 4: 4, 2: 2, 1: 1}
     e_ng = ng.get(k, 1)
     d_ng = ng.get(2 * k, 1)
-    return (f"leo16w_encode_kernel<{e_ng}, {eg[e_ng]}>", f"leo16w_decode_kernel<{d_ng}, {dg[d_ng]}>")
+    enc = f"leo16w_encode_kernel<{e_ng}, {eg[e_ng]}>"
+    if k == 1024:  # round 6: the quarter-lane kernels (encoder 8 waves, decoder 16)
+        return "leo16_encode_q_kernel<1024, false>", "leo16_decode_q_kernel<1024>"
+    return enc, f"leo16w_decode_kernel<{d_ng}, {dg[d_ng]}>"
 
 
 def stress_roofline(kernel: str, alg_bytes: float, ms: float, launches: int, pmc_name: str, work: str):

@@ -364,7 +364,7 @@ constexpr int kTabPos = 2048;  // skew positions of the register kernels (n <= 2
 //   [10..13] group 3 (bits 8-10), [14..17] group 4 (bits 11-13), [18, 19] group 5 (bits 14-15)
 // entry e of a group at byte e of its pool: product (e << shift) * c.
 __constant__ uint32_t g_ptab16x[kTabPos * kTab16x];
-__constant__ uint32_t g_ptab16x_merged[2 * kTab16x];
+__constant__ uint32_t g_ptab16x_merged[3 * kTab16x];
 
 __device__ __forceinline__ void mul16x_add_t(uint32_t& xlo, uint32_t& xhi, uint32_t ylo, uint32_t yhi,
                                              const uint32_t* t) {
@@ -1339,14 +1339,14 @@ __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
 // first FFT layer (bit 8, registers j, j + 16 in T) are merged as in the other
 // encoders.  Host emulation: tests/test_quarterlane_emu.py.
 // ---------------------------------------------------------------------------
-// bits 7, 8 in T: registers j, j + 8 << (b - 7); position OFF + 128 (jb >> 3) + d - 1
-template <bool INV, int B, int OFF>
+// bits >= 7 in T: registers j, j + (1 << LR) << (b - 7); position OFF + 128 (jb >> LR) + d - 1
+template <bool INV, int B, int OFF, int LR = 3>
 __device__ __forceinline__ void layer_te_q(WQ& w) {
-  constexpr int RD = 8 << (B - 7), D = 1 << B;
+  constexpr int RD = (1 << LR) << (B - 7), D = 1 << B;
 #pragma unroll
   for (int jb = 0; jb < 32; jb += 2 * RD) {
-    const bool zero = OFF + 128 * (jb >> 3) == 0;
-    const int pos = zero ? 0 : opaque_tok(OFF + 128 * (jb >> 3) + D - 1, w.lo[jb]);
+    const bool zero = OFF + 128 * (jb >> LR) == 0;
+    const int pos = zero ? 0 : opaque_tok(OFF + 128 * (jb >> LR) + D - 1, w.lo[jb]);
 #pragma unroll
     for (int j = jb; j < jb + RD; j++) {
       if (zero) {
@@ -1362,15 +1362,19 @@ __device__ __forceinline__ void layer_te_q(WQ& w) {
   }
 }
 
-template <bool REV>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_encode_q_kernel(
+// M = 1024 (k = 1024, round 6): 8 waves (512 threads), T as the k = 512
+// decoder's (LR = 2: e = ql + 4 (j & 3) + 16 q + 128 (j >> 2)), layers on bits
+// 7, 8 and the merged bit 9; 64 KiB of LDS, two workgroups per CU.
+template <int M, bool REV>
+__global__ __launch_bounds__(M / 2) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_encode_q_kernel(
     EncodeArgs a) {
-  constexpr int M = 512, IO = REV ? 0 : M, FO = REV ? M : 0;
-  // two 16-KiB transpose rounds (xpose_bt_db, LR = 3, RPR = 4); the S-layer
-  // images (30 KiB: bit 0 at q x 5 KiB, bit 1 at 20 KiB + q x 2.5 KiB) in the
-  // same space before the first transpose and after the last
-  __shared__ __attribute__((aligned(16))) uint32_t lds[8192];
-  constexpr int IMG1 = 20 * 1024;
+  constexpr int IO = REV ? 0 : M, FO = REV ? M : 0;
+  constexpr int NQ = M / 128, LR = M == 1024 ? 2 : 3, RPR = M == 1024 ? 2 : 4;
+  // two transpose rounds (xpose_bt_db; M = 512: 16 KiB each, 1024: 32 KiB); the
+  // S-layer images (NQ x 7.5 KiB: bit 0 at q x 5 KiB, bit 1 at IMG1 + q x 2.5
+  // KiB) in the same space before the first transpose and after the last
+  __shared__ __attribute__((aligned(16))) uint32_t lds[M == 1024 ? 16384 : 8192];
+  constexpr int IMG1 = NQ * 5 * 1024;
   const long blk = blockIdx.x;
   const int piece = (int)(blk % a.nchunk);  // nchunk = 128-B pieces of the shard
   const long sv = blk / a.nchunk;
@@ -1425,18 +1429,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   layer_b_q<true, 5, IO>(w, q);
   layer_b_q<true, 6, IO>(w, q);
   __syncthreads();  // every wave's reads of its S-layer images are done
-  xpose_bt_db<3, 4, 0>(w, lds, q, lane);  // rounds A B A B
-  layer_te_q<true, 7, IO>(w);
-  // last IFFT layer (bit 8, skew IO + 255) merged with the first FFT layer
-  // (bit 8, skew FO + 255): registers j, j + 16
+  xpose_bt_db<LR, RPR, 0>(w, lds, q, lane);  // rounds A B A B
+  layer_te_q<true, 7, IO, LR>(w);
+  if constexpr (M == 1024) layer_te_q<true, 8, IO, LR>(w);
+  // last IFFT layer (top bit, skew IO + M/2 - 1) merged with the first FFT
+  // layer (top bit, skew FO + M/2 - 1): registers j, j + 16
 #pragma unroll
   for (int j = 0; j < 16; j++) {
-    ifft_fft2_16(w, j, j + 16, MERGED_TAB(1));
+    ifft_fft2_16(w, j, j + 16, MERGED_TAB(M == 1024 ? 2 : 1));
     pin_pair(w, j, j + 16);
   }
   // ---- FFT (fftDIT, skew index FO + iend - 1) ----
-  layer_te_q<false, 7, FO>(w);
-  xpose_bt_db<3, 4, 0>(w, lds, q, lane);  // A B A B
+  if constexpr (M == 1024) layer_te_q<false, 8, FO, LR>(w);
+  layer_te_q<false, 7, FO, LR>(w);
+  xpose_bt_db<LR, RPR, 0>(w, lds, q, lane);  // A B A B
   __syncthreads();  // every wave's reads of B are done: the images come back over it
   q_pos_tables<FO, IMG1>(lds, q, lane);
   layer_b_q<false, 6, FO>(w, q);
@@ -1677,7 +1683,7 @@ hipError_t ensure_tables() {
   {
     // merged encoder tables: the element exp(skew[p]) ^ exp(skew[q]) (skew kMod16 = element 0)
     auto elem = [&](int pos) -> unsigned { return t.skew[pos] == kMod16 ? 0u : (unsigned)t.exp[t.skew[pos]]; };
-    const int pairs[2][2] = {{383, 127}, {767, 255}};
+    const int pairs[3][2] = {{383, 127}, {767, 255}, {1535, 511}};  // m = 256, 512, 1024
     // 3/3/2-split tables (mul16x_add_t): per skew position and for the two merged elements
     auto tab332 = [&](unsigned c, uint32_t* out) {  // c = field element (0: zero table)
       for (int i = 0; i < kTab16x; i++) out[i] = 0;
@@ -1701,8 +1707,8 @@ hipError_t ensure_tables() {
     for (int pos = 0; pos < kTabPos; pos++)
       if (t.skew[pos] != kMod16) tab332((unsigned)t.exp[t.skew[pos]], px.data() + (size_t)pos * kTab16x);
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_ptab16x), px.data(), px.size() * 4)) != hipSuccess) return e;
-    std::vector<uint32_t> mx(2 * kTab16x, 0u);
-    for (int m = 0; m < 2; m++) tab332(elem(pairs[m][0]) ^ elem(pairs[m][1]), mx.data() + (size_t)m * kTab16x);
+    std::vector<uint32_t> mx(3 * kTab16x, 0u);
+    for (int m = 0; m < 3; m++) tab332(elem(pairs[m][0]) ^ elem(pairs[m][1]), mx.data() + (size_t)m * kTab16x);
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_ptab16x_merged), mx.data(), mx.size() * 4)) != hipSuccess) return e;
     uint16_t lb[16];
     for (int b = 0; b < 16; b++) lb[b] = (uint16_t)t.log[1u << b];
@@ -1737,6 +1743,19 @@ static bool use_wide(int k) { return k > 512 || wide_forced(); }
 // k = 256 / 512 encoders: the half-lane kernels, one workgroup per 256-B piece
 // of a vector's shards (a last partial piece: inactive lanes store nothing)
 hipError_t launch_leo16_encode(int k, const EncodeArgs& a, hipStream_t s) {
+  if (k == 1024 && a.shard_bytes % 64 == 0 && !wide_forced()) {
+    // k = 1024: the quarter-lane encoder, 8 waves, two workgroups per CU, 128-B pieces
+    if (a.reverse && !a.out_present) return hipErrorInvalidValue;
+    hipError_t e = ensure_tables();
+    if (e != hipSuccess) return e;
+    EncodeArgs b = a;
+    b.nchunk = (a.shard_bytes + 127) / 128;
+    const long qb = b.nsq * b.nvec * b.nchunk;
+    if (qb <= 0) return hipSuccess;
+    if (a.reverse) hipLaunchKernelGGL((leo16_encode_q_kernel<1024, true>), dim3((unsigned)qb), dim3(512), 0, s, b);
+    else hipLaunchKernelGGL((leo16_encode_q_kernel<1024, false>), dim3((unsigned)qb), dim3(512), 0, s, b);
+    return hipGetLastError();
+  }
   if (use_wide(k)) return launch_leo16w_encode(k, a, s);
   if (!gf16_k_ok(k) || a.shard_bytes % 64) return hipErrorInvalidValue;
   if (a.reverse && !a.out_present) return hipErrorInvalidValue;  // reverse transform: Repair fill only
@@ -1750,8 +1769,8 @@ hipError_t launch_leo16_encode(int k, const EncodeArgs& a, hipStream_t s) {
 #ifndef DAGPU_ENC512_HALF  // (A/B builds: the half-lane k = 512 encoder)
     b.nchunk = (a.shard_bytes + 127) / 128;  // quarter-lane encoder, 128-B pieces, four workgroups per CU
     const long qb = b.nsq * b.nvec * b.nchunk;
-    if (a.reverse) hipLaunchKernelGGL((leo16_encode_q_kernel<true>), dim3((unsigned)qb), dim3(256), 0, s, b);
-    else hipLaunchKernelGGL((leo16_encode_q_kernel<false>), dim3((unsigned)qb), dim3(256), 0, s, b);
+    if (a.reverse) hipLaunchKernelGGL((leo16_encode_q_kernel<512, true>), dim3((unsigned)qb), dim3(256), 0, s, b);
+    else hipLaunchKernelGGL((leo16_encode_q_kernel<512, false>), dim3((unsigned)qb), dim3(256), 0, s, b);
 #else
     if (a.reverse) hipLaunchKernelGGL((leo16_encode_h_kernel<512, true>), dim3((unsigned)hb), dim3(512), 0, s, b);
     else hipLaunchKernelGGL((leo16_encode_h_kernel<512, false>), dim3((unsigned)hb), dim3(512), 0, s, b);
