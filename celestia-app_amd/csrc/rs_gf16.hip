@@ -1053,9 +1053,12 @@ __device__ __forceinline__ void lds_tab(const uint32_t* img, uint32_t byte_off, 
 // Layer on element bit b (0 or 1) in S: x = register j, y = j + 8 (b = 0) /
 // j + 16 (b = 1).  Position (e & ~(2d - 1)) + d - 1 per lane; the wave's images:
 // bit 0 at img0 + (e(x) - 128 q) / 2 * 80, bit 1 at img1 + (e(x) - 128 q) / 4 * 80.
-template <bool INV, int B>
+template <bool INV, int B, bool FRESH = false>
 __device__ __forceinline__ void layer_s_q(WQ& w, int ql, const uint32_t* img) {
   constexpr int RD = 8 << B;  // register distance of the pair
+  // FRESH (k = 1024's FFT side): a fresh quarter index, so that the table
+  // offsets are not the IFFT's, held (spilled) across the kernel
+  if constexpr (FRESH) asm volatile("" : "+v"(ql));
 #pragma unroll
   for (int j = 0; j < 32; j++) {
     if ((j >> 3) & (1 << B)) continue;
@@ -1292,8 +1295,8 @@ __global__ __launch_bounds__(K) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
   layer_b_q<false, 2>(w, q);
   swap_sb_q(w);
   wait_dma();
-  layer_s_q<false, 1>(w, ql, img1_base + q * 32 * kTab16x);
-  layer_s_q<false, 0>(w, ql, img0_base + q * 64 * kTab16x);
+  layer_s_q<false, 1, K == 1024>(w, ql, img1_base + q * 32 * kTab16x);
+  layer_s_q<false, 0, K == 1024>(w, ql, img0_base + q * 64 * kTab16x);
   // erased shards = work * (65535 - errLocs): the stored table of a missing
   // element; a register whose four elements are all given is skipped (uniform)
   const int q_e = opaque_s(q);

@@ -11,6 +11,15 @@ case "$1" in
     timeout -k 10 600 python -u bench.py > gpurun_out/r06_clean_bench.log 2>&1 || { echo "bench failed"; tail -5 gpurun_out/r06_clean_bench.log; exit 1; }
     tail -c 600 gpurun_out/r06_clean_bench.log
     ;;
+  q1kc)  # round 6: k = 1024 decoder without the S-layer offset spill; counters of the k >= 1024 kernels
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_wide.py -k "not k8192 and not k4096" > gpurun_out/r06_q1kc_wide.log 2>&1
+    rc=$?; echo "wide tests rc=$rc"; tail -3 gpurun_out/r06_q1kc_wide.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_gf16.py tests/test_gpu_repair_fill.py > gpurun_out/r06_q1kc_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r06_q1kc_tests.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 1024 --batch 1 --steps 3 --warmup 1" new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 1 repair512 new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_pmc_gf16.sh repair1024 split1024 repair2048
+    ;;
   q1ke)  # round 6: quarter-lane k = 1024 encoder (8 waves, two workgroups per CU) + decoder vs HEAD (quarter decoder, wide encoder)
     timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_wide.py -k "not k8192 and not k4096" > gpurun_out/r06_q1ke_wide.log 2>&1
     rc=$?; echo "wide tests rc=$rc"; tail -3 gpurun_out/r06_q1ke_wide.log; [ $rc -eq 0 ] || exit $rc
