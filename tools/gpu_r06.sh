@@ -11,6 +11,14 @@ case "$1" in
     timeout -k 10 600 python -u bench.py > gpurun_out/r06_clean_bench.log 2>&1 || { echo "bench failed"; tail -5 gpurun_out/r06_clean_bench.log; exit 1; }
     tail -c 600 gpurun_out/r06_clean_bench.log
     ;;
+  tail)  # round 6: fused NMT tree tail (few squares in flight) vs one launch per level
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_split.py tests/test_gpu_repair_fill.py tests/test_gpu_square.py tests/test_gpu_proof.py > gpurun_out/r06_tail_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r06_tail_tests.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 3 "bench:--mode split --split-k 512 --steps 30 --warmup 3" new= off=DAGPU_NMT_TAIL=0 base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 2 repair512 new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 1 headline new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    timeout -k 10 300 python -u tools/single_square.py 3 DAGPU_NMT_TAIL=auto,0 > gpurun_out/r06_tail_single.log 2>&1 && tail -12 gpurun_out/r06_tail_single.log
+    ;;
   q1kc)  # round 6: k = 1024 decoder without the S-layer offset spill; counters of the k >= 1024 kernels
     timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_wide.py -k "not k8192 and not k4096" > gpurun_out/r06_q1kc_wide.log 2>&1
     rc=$?; echo "wide tests rc=$rc"; tail -3 gpurun_out/r06_q1kc_wide.log; [ $rc -eq 0 ] || exit $rc
