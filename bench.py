@@ -271,6 +271,8 @@ def gf16_kernel_names(k: int):
     enc = f"leo16w_encode_kernel<{e_ng}, {eg[e_ng]}>"
     if k == 1024:  # round 6: the quarter-lane kernels (encoder 8 waves, decoder 16)
         return "leo16_encode_q_kernel<1024, false>", "leo16_decode_q_kernel<1024>"
+    if k == 2048:  # round 6: the quarter-lane encoder (16 waves), the wide decoder
+        enc = "leo16_encode_q_kernel<2048, false>"
     return enc, f"leo16w_decode_kernel<{d_ng}, {dg[d_ng]}>"
 
 

@@ -348,7 +348,7 @@ __device__ __forceinline__ int opaque_s(int x) {
 // Positions < 2m = 1024 cover every encoder skew index (IFFT m-1+iend+2d <
 // 2m, FFT iend-1 < m) and every k = 512 decoder one (iend - 1 < n).
 // __constant__ so that the wave-uniform table reads become scalar loads.
-constexpr int kTabPos = 2048;  // skew positions of the register kernels (n <= 2048)
+constexpr int kTabPos = 4096;  // skew positions of the register kernels (decoders n <= 2048, encoders 2m <= 4096)
 
 // 3/3/2 split (round 5): each byte of y in groups of 3, 3 and 2 bits, so a
 // symbol takes 6 lookups per output byte instead of 8.  A 3-bit group indexes
@@ -364,7 +364,7 @@ constexpr int kTabPos = 2048;  // skew positions of the register kernels (n <= 2
 //   [10..13] group 3 (bits 8-10), [14..17] group 4 (bits 11-13), [18, 19] group 5 (bits 14-15)
 // entry e of a group at byte e of its pool: product (e << shift) * c.
 __constant__ uint32_t g_ptab16x[kTabPos * kTab16x];
-__constant__ uint32_t g_ptab16x_merged[3 * kTab16x];
+__constant__ uint32_t g_ptab16x_merged[4 * kTab16x];
 
 __device__ __forceinline__ void mul16x_add_t(uint32_t& xlo, uint32_t& xhi, uint32_t ylo, uint32_t yhi,
                                              const uint32_t* t) {
@@ -1367,16 +1367,18 @@ __device__ __forceinline__ void layer_te_q(WQ& w) {
 
 // M = 1024 (k = 1024, round 6): 8 waves (512 threads), T as the k = 512
 // decoder's (LR = 2: e = ql + 4 (j & 3) + 16 q + 128 (j >> 2)), layers on bits
-// 7, 8 and the merged bit 9; 64 KiB of LDS, two workgroups per CU.
+// 7, 8 and the merged bit 9; 64 KiB of LDS, two workgroups per CU.  M = 2048:
+// 16 waves, T as the k = 1024 decoder's (LR = 1), bits 7-9 and the merged 10,
+// 128 KiB of LDS, one workgroup per CU.
 template <int M, bool REV>
 __global__ __launch_bounds__(M / 2) __attribute__((amdgpu_waves_per_eu(4, 4))) void leo16_encode_q_kernel(
     EncodeArgs a) {
   constexpr int IO = REV ? 0 : M, FO = REV ? M : 0;
-  constexpr int NQ = M / 128, LR = M == 1024 ? 2 : 3, RPR = M == 1024 ? 2 : 4;
+  constexpr int NQ = M / 128, LR = M == 2048 ? 1 : M == 1024 ? 2 : 3, RPR = M == 2048 ? 1 : M == 1024 ? 2 : 4;
   // two transpose rounds (xpose_bt_db; M = 512: 16 KiB each, 1024: 32 KiB); the
   // S-layer images (NQ x 7.5 KiB: bit 0 at q x 5 KiB, bit 1 at IMG1 + q x 2.5
   // KiB) in the same space before the first transpose and after the last
-  __shared__ __attribute__((aligned(16))) uint32_t lds[M == 1024 ? 16384 : 8192];
+  __shared__ __attribute__((aligned(16))) uint32_t lds[M == 2048 ? 32768 : M == 1024 ? 16384 : 8192];
   constexpr int IMG1 = NQ * 5 * 1024;
   const long blk = blockIdx.x;
   const int piece = (int)(blk % a.nchunk);  // nchunk = 128-B pieces of the shard
@@ -1391,23 +1393,27 @@ __global__ __launch_bounds__(M / 2) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   const bool active = col < (uint32_t)a.shard_bytes;
   q_pos_tables<IO, IMG1>(lds, q, lane);
   const uint32_t cl = active ? col : 0u;  // inactive lanes read valid memory, store nothing
+  // M = 2048: the wave's first element in the buffer base (a column vector of a
+  // k = 2048 EDS spans 4 GiB, past the 32-bit buffer offsets)
+  constexpr int QW = M == 2048 ? 0 : 128;  // element offset of the wave left in the offsets
+  const long wb = M == 2048 ? 128L * q : 0L;
   WQ w;
   {
-    const auto in_rsrc = make_rsrc(a.in + sq * a.in_sq_stride + vec * a.in_vec_stride);
+    const auto in_rsrc = make_rsrc(a.in + sq * a.in_sq_stride + vec * a.in_vec_stride + wb * a.in_shard_stride);
     const uint32_t vin = cl + (uint32_t)ql * 32u * (uint32_t)a.in_shard_stride;  // quarter ql: shard + 32 ql
     const int q_ld = opaque_s(q);
 #pragma unroll
     for (int j = 0; j < 32; j++) {
-      const uint32_t so = (uint32_t)(128 * q_ld + q_elem_s(j, 0)) * (uint32_t)a.in_shard_stride;
+      const uint32_t so = (uint32_t)(QW * q_ld + q_elem_s(j, 0)) * (uint32_t)a.in_shard_stride;
       w.lo[j] = __builtin_amdgcn_raw_buffer_load_b32(in_rsrc, vin, so, 0);
       w.hi[j] = __builtin_amdgcn_raw_buffer_load_b32(in_rsrc, vin + 32u, so, 0);
     }
     if (a.copy && active) {  // Q0 placement
-      const auto cp = make_rsrc(a.copy + sq * a.copy_sq_stride + vec * a.copy_vec_stride);
+      const auto cp = make_rsrc(a.copy + sq * a.copy_sq_stride + vec * a.copy_vec_stride + wb * a.copy_shard_stride);
       const uint32_t vcp = col + (uint32_t)ql * 32u * (uint32_t)a.copy_shard_stride;
 #pragma unroll
       for (int j = 0; j < 32; j++) {
-        const uint32_t so = (uint32_t)(128 * q_ld + q_elem_s(j, 0)) * (uint32_t)a.copy_shard_stride;
+        const uint32_t so = (uint32_t)(QW * q_ld + q_elem_s(j, 0)) * (uint32_t)a.copy_shard_stride;
         __builtin_amdgcn_raw_buffer_store_b32(w.lo[j], cp, vcp, so, 0);
         __builtin_amdgcn_raw_buffer_store_b32(w.hi[j], cp, vcp + 32u, so, 0);
       }
@@ -1434,16 +1440,18 @@ __global__ __launch_bounds__(M / 2) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   __syncthreads();  // every wave's reads of its S-layer images are done
   xpose_bt_db<LR, RPR, 0>(w, lds, q, lane);  // rounds A B A B
   layer_te_q<true, 7, IO, LR>(w);
-  if constexpr (M == 1024) layer_te_q<true, 8, IO, LR>(w);
+  if constexpr (M >= 1024) layer_te_q<true, 8, IO, LR>(w);
+  if constexpr (M >= 2048) layer_te_q<true, 9, IO, LR>(w);
   // last IFFT layer (top bit, skew IO + M/2 - 1) merged with the first FFT
   // layer (top bit, skew FO + M/2 - 1): registers j, j + 16
 #pragma unroll
   for (int j = 0; j < 16; j++) {
-    ifft_fft2_16(w, j, j + 16, MERGED_TAB(M == 1024 ? 2 : 1));
+    ifft_fft2_16(w, j, j + 16, MERGED_TAB(M == 2048 ? 3 : M == 1024 ? 2 : 1));
     pin_pair(w, j, j + 16);
   }
   // ---- FFT (fftDIT, skew index FO + iend - 1) ----
-  if constexpr (M == 1024) layer_te_q<false, 8, FO, LR>(w);
+  if constexpr (M >= 2048) layer_te_q<false, 9, FO, LR>(w);
+  if constexpr (M >= 1024) layer_te_q<false, 8, FO, LR>(w);
   layer_te_q<false, 7, FO, LR>(w);
   xpose_bt_db<LR, RPR, 0>(w, lds, q, lane);  // A B A B
   __syncthreads();  // every wave's reads of B are done: the images come back over it
@@ -1459,14 +1467,14 @@ __global__ __launch_bounds__(M / 2) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   layer_s_q<false, 0>(w, ql, lds + q * 64 * kTab16x);
   if (!active) return;
   // ---- store: compare (prerepairSanityCheck), Repair fill, or plain ----
-  const auto out_rsrc = make_rsrc(a.out + sq * a.out_sq_stride + vec * a.out_vec_stride);
+  const auto out_rsrc = make_rsrc(a.out + sq * a.out_sq_stride + vec * a.out_vec_stride + wb * a.out_shard_stride);
   const uint32_t vout = col + (uint32_t)ql * 32u * (uint32_t)a.out_shard_stride;
   const int q_st = opaque_s(q);
   if (a.mismatch) {
     uint32_t diff = 0;
 #pragma unroll
     for (int j = 0; j < 32; j++) {
-      const uint32_t so = (uint32_t)(128 * q_st + q_elem_s(j, 0)) * (uint32_t)a.out_shard_stride;
+      const uint32_t so = (uint32_t)(QW * q_st + q_elem_s(j, 0)) * (uint32_t)a.out_shard_stride;
       diff |= w.lo[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, vout, so, 0);
       diff |= w.hi[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, vout + 32u, so, 0);
     }
@@ -1480,7 +1488,7 @@ __global__ __launch_bounds__(M / 2) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     uint32_t diff = 0;
 #pragma unroll
     for (int j = 0; j < 32; j++) {
-      const uint32_t so = (uint32_t)(128 * q_st + q_elem_s(j, 0)) * (uint32_t)a.out_shard_stride;
+      const uint32_t so = (uint32_t)(QW * q_st + q_elem_s(j, 0)) * (uint32_t)a.out_shard_stride;
       if ((gw >> q_elem_s(j, 0)) & 1) {
         diff |= w.lo[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, vout, so, 0);
         diff |= w.hi[j] ^ __builtin_amdgcn_raw_buffer_load_b32(out_rsrc, vout + 32u, so, 0);
@@ -1494,7 +1502,7 @@ __global__ __launch_bounds__(M / 2) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   }
 #pragma unroll
   for (int j = 0; j < 32; j++) {
-    const uint32_t so = (uint32_t)(128 * q_st + q_elem_s(j, 0)) * (uint32_t)a.out_shard_stride;
+    const uint32_t so = (uint32_t)(QW * q_st + q_elem_s(j, 0)) * (uint32_t)a.out_shard_stride;
     __builtin_amdgcn_raw_buffer_store_b32(w.lo[j], out_rsrc, vout, so, 0);
     __builtin_amdgcn_raw_buffer_store_b32(w.hi[j], out_rsrc, vout + 32u, so, 0);
   }
@@ -1686,7 +1694,7 @@ hipError_t ensure_tables() {
   {
     // merged encoder tables: the element exp(skew[p]) ^ exp(skew[q]) (skew kMod16 = element 0)
     auto elem = [&](int pos) -> unsigned { return t.skew[pos] == kMod16 ? 0u : (unsigned)t.exp[t.skew[pos]]; };
-    const int pairs[3][2] = {{383, 127}, {767, 255}, {1535, 511}};  // m = 256, 512, 1024
+    const int pairs[4][2] = {{383, 127}, {767, 255}, {1535, 511}, {3071, 1023}};  // m = 256 .. 2048
     // 3/3/2-split tables (mul16x_add_t): per skew position and for the two merged elements
     auto tab332 = [&](unsigned c, uint32_t* out) {  // c = field element (0: zero table)
       for (int i = 0; i < kTab16x; i++) out[i] = 0;
@@ -1710,8 +1718,8 @@ hipError_t ensure_tables() {
     for (int pos = 0; pos < kTabPos; pos++)
       if (t.skew[pos] != kMod16) tab332((unsigned)t.exp[t.skew[pos]], px.data() + (size_t)pos * kTab16x);
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_ptab16x), px.data(), px.size() * 4)) != hipSuccess) return e;
-    std::vector<uint32_t> mx(3 * kTab16x, 0u);
-    for (int m = 0; m < 3; m++) tab332(elem(pairs[m][0]) ^ elem(pairs[m][1]), mx.data() + (size_t)m * kTab16x);
+    std::vector<uint32_t> mx(4 * kTab16x, 0u);
+    for (int m = 0; m < 4; m++) tab332(elem(pairs[m][0]) ^ elem(pairs[m][1]), mx.data() + (size_t)m * kTab16x);
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_ptab16x_merged), mx.data(), mx.size() * 4)) != hipSuccess) return e;
     uint16_t lb[16];
     for (int b = 0; b < 16; b++) lb[b] = (uint16_t)t.log[1u << b];
@@ -1746,8 +1754,8 @@ static bool use_wide(int k) { return k > 512 || wide_forced(); }
 // k = 256 / 512 encoders: the half-lane kernels, one workgroup per 256-B piece
 // of a vector's shards (a last partial piece: inactive lanes store nothing)
 hipError_t launch_leo16_encode(int k, const EncodeArgs& a, hipStream_t s) {
-  if (k == 1024 && a.shard_bytes % 64 == 0 && !wide_forced()) {
-    // k = 1024: the quarter-lane encoder, 8 waves, two workgroups per CU, 128-B pieces
+  if ((k == 1024 || k == 2048) && a.shard_bytes % 64 == 0 && !wide_forced()) {
+    // k = 1024 / 2048: the quarter-lane encoder, 8 / 16 waves (two workgroups / one per CU), 128-B pieces
     if (a.reverse && !a.out_present) return hipErrorInvalidValue;
     hipError_t e = ensure_tables();
     if (e != hipSuccess) return e;
@@ -1755,8 +1763,14 @@ hipError_t launch_leo16_encode(int k, const EncodeArgs& a, hipStream_t s) {
     b.nchunk = (a.shard_bytes + 127) / 128;
     const long qb = b.nsq * b.nvec * b.nchunk;
     if (qb <= 0) return hipSuccess;
-    if (a.reverse) hipLaunchKernelGGL((leo16_encode_q_kernel<1024, true>), dim3((unsigned)qb), dim3(512), 0, s, b);
-    else hipLaunchKernelGGL((leo16_encode_q_kernel<1024, false>), dim3((unsigned)qb), dim3(512), 0, s, b);
+    if (k == 2048) {
+      if (a.reverse) hipLaunchKernelGGL((leo16_encode_q_kernel<2048, true>), dim3((unsigned)qb), dim3(1024), 0, s, b);
+      else hipLaunchKernelGGL((leo16_encode_q_kernel<2048, false>), dim3((unsigned)qb), dim3(1024), 0, s, b);
+    } else if (a.reverse) {
+      hipLaunchKernelGGL((leo16_encode_q_kernel<1024, true>), dim3((unsigned)qb), dim3(512), 0, s, b);
+    } else {
+      hipLaunchKernelGGL((leo16_encode_q_kernel<1024, false>), dim3((unsigned)qb), dim3(512), 0, s, b);
+    }
     return hipGetLastError();
   }
   if (use_wide(k)) return launch_leo16w_encode(k, a, s);

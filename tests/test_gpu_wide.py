@@ -34,18 +34,18 @@ def ctx():
 def test_wide_encode_matches_oracle(ctx, k):
     # one slice width per element count: n = k elements -> 32 / 32 / 8 / 4 symbols
     rng = np.random.default_rng(k)
-    shard = 64 if k > 2048 else 128
+    shard = 64 if k > 2048 else 192  # (k = 1024 / 2048: the quarter-lane encoders, a partial 128-B piece)
     data = rng.integers(0, 256, (2, k, shard), dtype=np.uint8)
     par = da.LeoRSCodec(ctx).encode_batch(data)
     for v in range(2):
         assert (par[v] == oracle.encode(data[v])).all()
 
 
-@pytest.mark.parametrize("k", [1024, 2048, 4096, 8192])
-def test_wide_decode_matches_oracle(ctx, k):
-    # decode transforms n = 2k = 2048 .. 16384 elements (the last at 128 KiB of LDS)
+@pytest.mark.parametrize("k,shard", [(1024, 64), (1024, 384), (2048, 64), (4096, 64), (8192, 64)])
+def test_wide_decode_matches_oracle(ctx, k, shard):
+    # decode transforms n = 2k = 2048 .. 16384 elements (the last at 128 KiB of LDS);
+    # k = 1024 with 128-B pieces: the quarter-lane decoder (round 6), else the LDS-slice one
     rng = np.random.default_rng(k + 1)
-    shard = 64
     data = rng.integers(0, 256, (k, shard), dtype=np.uint8)
     full = np.concatenate([data, oracle.encode(data)])
     codec = da.LeoRSCodec(ctx)

@@ -480,3 +480,51 @@ def test_quarterlane_encoder_m1024_equals_leopard_loops(rev):
         q, j, ql = _inv_s(e)
         got.append(R[q][j][ql])
     assert got == ref
+
+
+# --- the k = 2048 encoder (leo16_encode_q_kernel<2048>): m = 2048 over 16
+# waves, T as the k = 1024 decoder's (LR = 1), layers on bits 7-9 and the merged bit 10
+def layer_t1k_off(R, b, off, inv):
+    rd, d = 2 << (b - 7), 1 << b
+    for q, reg in enumerate(R):
+        for jb in range(0, 32, 2 * rd):
+            pos = off + 128 * (jb >> 1) + d - 1
+            for j in range(jb, jb + rd):
+                for ql in range(4):
+                    assert off + (e_t1k(q, j, ql) & ~(2 * d - 1)) + d - 1 == pos
+                    w = [reg[j][ql], reg[j + rd][ql]]
+                    bfly(w, 0, 1, pos, inv)
+                    reg[j][ql], reg[j + rd][ql] = w
+
+
+@pytest.mark.parametrize("rev", [False, True])
+def test_quarterlane_encoder_m2048_equals_leopard_loops(rev):
+    rng = np.random.default_rng(41 + rev)
+    m = 2048
+    io, fo = (0, m) if rev else (m, 0)
+    x = [int(v) for v in rng.integers(0, 65536, m)]
+    ref = list(x)
+    ref_ifft(ref, io)
+    ref_fft(ref, fo)
+    R = [[[x[e_s(q, j, ql)] for ql in range(4)] for j in range(32)] for q in range(NQ1K)]
+    layer_s_off(R, 0, io, True)
+    layer_s_off(R, 1, io, True)
+    swap_sb(R)
+    for b in range(2, 7):
+        layer_b_off(R, b, io, True)
+    R = xpose_bt_1k(R)
+    for b in (7, 8, 9, 10):
+        layer_t1k_off(R, b, io, True)
+    for b in (10, 9, 8, 7):  # (bit 10 merged with the IFFT's in the kernel: registers j, j + 16)
+        layer_t1k_off(R, b, fo, False)
+    R = xpose_bt_1k(R)
+    for b in range(6, 1, -1):
+        layer_b_off(R, b, fo, False)
+    swap_sb(R)
+    layer_s_off(R, 1, fo, False)
+    layer_s_off(R, 0, fo, False)
+    got = []
+    for e in range(m):
+        q, j, ql = _inv_s(e)
+        got.append(R[q][j][ql])
+    assert got == ref

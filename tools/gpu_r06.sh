@@ -11,6 +11,15 @@ case "$1" in
     timeout -k 10 600 python -u bench.py > gpurun_out/r06_clean_bench.log 2>&1 || { echo "bench failed"; tail -5 gpurun_out/r06_clean_bench.log; exit 1; }
     tail -c 600 gpurun_out/r06_clean_bench.log
     ;;
+  q2ke)  # round 6: quarter-lane k = 2048 encoder (16 waves, one workgroup per CU) vs the wide one
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_wide.py -k "not k8192" > gpurun_out/r06_q2ke_wide.log 2>&1
+    rc=$?; echo "wide tests rc=$rc"; tail -3 gpurun_out/r06_q2ke_wide.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_gf16.py tests/test_gpu_split.py > gpurun_out/r06_q2ke_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r06_q2ke_tests.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode split --split-k 2048 --steps 4 --warmup 1" new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 1 "bench:--mode repair --k 2048 --batch 1 --steps 2 --warmup 1 --pattern q3" new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 1 "bench:--mode repair --k 2048 --batch 1 --steps 2 --warmup 1" new= base=lib:celestia-app_amd/libdagpu_base.so
+    ;;
   tail)  # round 6: fused NMT tree tail (few squares in flight) vs one launch per level
     timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_split.py tests/test_gpu_repair_fill.py tests/test_gpu_square.py tests/test_gpu_proof.py > gpurun_out/r06_tail_tests.log 2>&1
     rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r06_tail_tests.log; [ $rc -eq 0 ] || exit $rc
