@@ -924,6 +924,10 @@ DecodeArgs axis_decode_args(uint32_t k, size_t n, uint8_t* eds, uint8_t* present
   }
   d.err_key = r.err_share[axis][0];
   d.err_head = r.err_share[axis][1];
+#ifdef DAGPU_TEST_HOOKS
+  static const bool collide = getenv("DAGPU_TEST_KEY_COLLIDE") != nullptr;  // read once
+  d.key_collide = collide ? 1 : 0;
+#endif
   d.nsq = (long)n;
   d.nvec = w;
   d.nchunk = 1;

@@ -117,6 +117,9 @@ struct DecodeArgs {
   // workspace; NULL = one computation per vector.
   int32_t* err_key;
   int32_t* err_head;
+  // Test builds only (DAGPU_TEST_HOOKS; the product library never sets it):
+  // every key equal, so the candidate-head checks decide every vector's head.
+  int key_collide;
   // Locators only (Repair, after the fill/deferral plan): compute the error
   // locators of the vectors whose flags[] are already set, leaving flags and
   // counts alone; a flagged vector whose head is not flagged computes the

@@ -1907,7 +1907,7 @@ __device__ __forceinline__ void errloc_key_rows_block(const DecodeArgs& a, long 
     const uint64_t m = __builtin_amdgcn_ballot_w64(i < n && pv[i] != 0);
     key ^= key_mix(m, g);
   }
-  if (lane == 0) a.err_key[gv] = (int32_t)key;
+  if (lane == 0) a.err_key[gv] = a.key_collide ? 0x5A5A5A5A : (int32_t)key;
 }
 
 __device__ __forceinline__ void errloc_key_cols_block(const DecodeArgs& a, long bid, uint32_t* acc) {
@@ -1930,7 +1930,7 @@ __device__ __forceinline__ void errloc_key_cols_block(const DecodeArgs& a, long 
     if (key) atomicXor(&acc[lane], key);
   }
   __syncthreads();
-  if (wave == 0 && v < a.nvec) a.err_key[sq * a.nvec + v] = (int32_t)acc[lane];
+  if (wave == 0 && v < a.nvec) a.err_key[sq * a.nvec + v] = a.key_collide ? 0x5A5A5A5A : (int32_t)acc[lane];
 }
 
 static long errloc_key_blocks(const DecodeArgs& a) {

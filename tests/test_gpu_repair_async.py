@@ -263,3 +263,55 @@ def test_join_on_another_stream_keeps_tensors_until_it(ctx):
         torch.cuda.synchronize()
         assert torch.equal(ds.eds, ref) and (status.cpu().numpy() == 0).all()
         del junk
+
+
+_KEY_COLLIDE_SCRIPT = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np, torch
+from celestia_da import da, synth
+from celestia_da.device import DeviceSquares
+ctx = da.Context(0)
+rng = np.random.default_rng(77)
+for k, n in ((8, 3), (128, 4), (256, 2), (512, 1), (1024, 1)):
+    w = 2 * k
+    ds = DeviceSquares(k, n, ctx=ctx)
+    ds.load_ods(synth.blob_squares(k, 40 + k, 0, n))
+    ds.extend()
+    torch.cuda.synchronize()
+    ref = ds.eds.clone()
+    # every row and column its own erasure pattern (70 % of the cells given):
+    # a candidate head accepted without the flag check would decode with
+    # another vector's locators
+    pres = (rng.random((n, w, w)) < 0.7).astype(np.uint8)
+    pres_t = torch.from_numpy(pres.reshape(n, -1)).cuda()
+    ds.eds.copy_((ds.eds.view(n, w * w, 512) * pres_t.view(n, w * w, 1)).view(n, -1))
+    status = torch.full((n,), 99, dtype=torch.int32, device="cuda")
+    ds.repair(pres_t.clone(), status, ds.repair_workspace())
+    torch.cuda.synchronize()
+    print("K", k, bool(torch.equal(ds.eds, ref)), status.cpu().numpy().tolist())
+    del ds
+    torch.cuda.empty_cache()
+ctx.close()
+"""
+
+
+@pytest.mark.parametrize("lib", ["libdagpu_test.so", "libdagpu.so"])
+def test_locator_key_collisions_fall_back_to_own_heads(lib):
+    """Every locator key equal (the test build's DAGPU_TEST_KEY_COLLIDE): each
+    vector's candidate head is its square's first vector, and the flag-by-flag
+    check inside the locator kernels (GF(2^8), GF(2^16) fold, k = 1024) must
+    send every vector with another erasure pattern to its own locators -- the
+    Repairs of squares whose every axis has its own pattern stay bit-exact.
+    The product library ignores the variable."""
+    import os
+    import subprocess
+    import sys
+
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "celestia-app_amd")
+    env = dict(os.environ, DAGPU_LIB=os.path.join(pkg, lib), DAGPU_TEST_KEY_COLLIDE="1")
+    r = subprocess.run([sys.executable, "-c", _KEY_COLLIDE_SCRIPT, pkg], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    for k, n in ((8, 3), (128, 4), (256, 2), (512, 1), (1024, 1)):
+        assert f"K {k} True {[0] * n}" in r.stdout, r.stdout
