@@ -834,7 +834,7 @@ struct RepairWs {
   int32_t* err_share[2][2];  // [axis][same, head]
   int32_t* sel;         // exact-order repair: level of each axis' attempt, [2][w]
   int32_t* bits;
-  int32_t* counters;    // [0] decodable rows, [1] decodable cols, [2] deferred, [3] / [4] fill / reverse fill pairs
+  int32_t* counters;    // kCtrSlots round counters (kernels.hpp kCtr*)
   // fill route / deferral (repair.hip PlanArgs)
   int32_t* fill;        // [sq][idx] of the round's axis
   int32_t* pair_list;   // k = 128 fill pairs, n * w entries
@@ -916,11 +916,13 @@ DecodeArgs axis_decode_args(uint32_t k, size_t n, uint8_t* eds, uint8_t* present
   if (axis == 0) {
     d.vec_stride = w * (long)kSS; d.shard_stride = kSS;
     d.p_vec_stride = w; d.p_shard_stride = 1;
-    d.err = r.err_rows; d.flags = r.flags_rows; d.ndecodable = r.counters + 0;
+    d.err = r.err_rows; d.flags = r.flags_rows; d.ndecodable = r.counters + kCtrRowsDec;
+    d.nfill = r.counters + kCtrFillRows;
   } else {
     d.vec_stride = kSS; d.shard_stride = w * (long)kSS;
     d.p_vec_stride = 1; d.p_shard_stride = w;
-    d.err = r.err_cols; d.flags = r.flags_cols; d.ndecodable = r.counters + 1;
+    d.err = r.err_cols; d.flags = r.flags_cols; d.ndecodable = r.counters + kCtrColsDec;
+    d.nfill = r.counters + kCtrFillCols;
   }
   d.err_key = r.err_share[axis][0];
   d.err_head = r.err_share[axis][1];
@@ -1177,7 +1179,7 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
   HIP_TRY(ctx, hipMemsetAsync(r.parity_bad, 0, n * 2 * w * sizeof(int32_t), s));
   HIP_TRY(ctx, hipMemsetAsync(r.counters, 0, kCtrSlots * sizeof(int32_t), s));  // kernels.hpp kCtr*
   int64_t rounds_run = 0, deferred_run = 0;
-  HIP_TRY(ctx, launch_axis_complete(d_present, (int)k, (long)n, r.complete_before, s, r.counters + 5));
+  HIP_TRY(ctx, launch_axis_complete(d_present, (int)k, (long)n, r.complete_before, s, r.counters + kCtrComplete));
   // prerepairSanityCheck: complete axes must satisfy parity == Encode(data).
   // Queued after the first round's counter read, and only when some axis is
   // complete (a complete axis is never written by the crossword, so the order
@@ -1242,7 +1244,7 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
     int last_ax = -1;
     if (pass > 0) {  // (the repair's first memset covers pass 0)
       HIP_TRY(ctx, hipMemsetAsync(r.counters, 0, (kCtrPairsRev + 1) * sizeof(int32_t), s));
-      HIP_TRY(ctx, hipMemsetAsync(r.counters + kCtrDeferSquares, 0, 2 * sizeof(int32_t), s));
+      HIP_TRY(ctx, hipMemsetAsync(r.counters + kCtrDeferSquares, 0, 2 * sizeof(int32_t), s));  // and DeferredPrev
     }
     for (int round = 0; round < max_rounds; round++) {
       DecodeArgs dr = axis_decode_args(k, n, d_eds, d_present, 0, r);
@@ -1269,22 +1271,22 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
         if (!stats_out) g.lock();
         int64_t* st = stats_out ? stats_out : ctx->rep_stats;
         st[0] = rounds_run;
-        st[1] = cnt[8];
-        st[2] = cnt[9];
-        st[3] = cnt[10];
-        st[4] = deferred_run + cnt[2];
+        st[1] = cnt[kCtrPlan];
+        st[2] = cnt[kCtrPlan + 1];
+        st[3] = cnt[kCtrPlan + 2];
+        st[4] = deferred_run + cnt[kCtrDeferred];
       }
-      if (pass == 0 && round == 0 && cnt[5] > 0) {
+      if (pass == 0 && round == 0 && cnt[kCtrComplete] > 0) {
         const int prc = prerepair();
         if (prc) return prc;
       }
-      deferred_total += cnt[2];
-      deferred_run += cnt[2];
-      if (cnt[0] == 0 && cnt[1] == 0) break;
+      deferred_total += cnt[kCtrDeferred];
+      deferred_run += cnt[kCtrDeferred];
+      if (cnt[kCtrRowsDec] == 0 && cnt[kCtrColsDec] == 0) break;
       rounds_run++;
-      int ax = cnt[0] >= cnt[1] ? 0 : 1;
+      int ax = cnt[kCtrRowsDec] >= cnt[kCtrColsDec] ? 0 : 1;
       // after a deferral the other axis is the one with complete data halves
-      if (cnt[2] > 0 && last_ax >= 0 && cnt[1 - last_ax] > 0) ax = 1 - last_ax;
+      if (cnt[kCtrDeferred] > 0 && last_ax >= 0 && cnt[kCtrRowsDec + 1 - last_ax] > 0) ax = 1 - last_ax;
       last_ax = ax;
       DecodeArgs& d = ax == 0 ? dr : dc;
       if (shortcut) {
@@ -1310,19 +1312,21 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
         pa.flags = d.flags;
         pa.fill = r.fill;
         pa.pair_list = listed ? r.pair_list : nullptr;
-        pa.pair_count = r.counters + 3;
+        pa.pair_count = r.counters + kCtrPairs;
         pa.pair_list_rev = listed ? r.pair_list_rev : nullptr;
-        pa.pair_count_rev = r.counters + 4;
+        pa.pair_count_rev = r.counters + kCtrPairsRev;
         pa.known = r.known;
         pa.deferred = r.deferred;
         pa.nodefer = r.nodefer;
-        pa.ndeferred = r.counters + 2;
-        pa.nplan = r.counters + 8;
+        pa.ndeferred = r.counters + kCtrDeferred;
+        pa.nplan = r.counters + kCtrPlan;
         pa.k = (int)k;
         pa.nsq = (long)n;
         pa.axis = ax;
         HIP_TRY(ctx, launch_repair_plan(pa, s));
-        {
+        // no fill candidates on this axis (the count launch's tally of the
+        // plan's f / r vectors): the two fill launches would find nothing
+        if (cnt[ax == 0 ? kCtrFillRows : kCtrFillCols] > 0) {
           ProfScope p(ctx, 6, s);
           // reverse fills: parity half in, data half out (its presence k shards before)
           EncodeArgs er = e;
@@ -1332,10 +1336,10 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
           er.reverse = 1;
           if (listed) {
             e.pair_list = r.pair_list;
-            e.pair_count = r.counters + 3;
+            e.pair_count = r.counters + kCtrPairs;
             HIP_TRY(ctx, launch_leo8_fill_sliced(e, (long)n * w_ / 2, s));
             er.pair_list = r.pair_list_rev;
-            er.pair_count = r.counters + 4;
+            er.pair_count = r.counters + kCtrPairsRev;
             HIP_TRY(ctx, launch_leo8_fill_sliced(er, (long)n * w_ / 2, s));
           } else {
             e.vec_flags = er.vec_flags = r.fill;
@@ -1359,9 +1363,10 @@ int repair_device(dagpu_ctx* ctx, uint32_t k, size_t n, uint8_t* d_eds, uint8_t*
     }
     if (!shortcut || deferred_total == 0) break;
     // deferred vectors whose codeword property is not implied: compare-mode encodes
-    HIP_TRY(ctx, launch_repair_defer_check(r.deferred, r.known, (int)k, (long)n, r.check, s, r.counters + 6));
+    HIP_TRY(ctx, launch_repair_defer_check(r.deferred, r.known, (int)k, (long)n, r.check, s,
+                                           r.counters + kCtrDeferSquares));
     int32_t left = 0;  // squares whose deferred axes are not proven codewords
-    HIP_TRY(ctx, read_small(&left, r.counters + 6, sizeof left, mb, s));
+    HIP_TRY(ctx, read_small(&left, r.counters + kCtrDeferSquares, sizeof left, mb, s));
     if (left == 0) break;
     for (int axis = 0; axis < 2; axis++) {
       EncodeArgs e{};

@@ -109,6 +109,7 @@ struct DecodeArgs {
   int32_t* too_few;    // optional: set to 1 if any vector has < k shards
   int32_t* progress;   // optional: += number of vectors rebuilt (mark pass)
   int32_t* ndecodable; // optional: += number of decodable vectors (errlocs pass)
+  int32_t* nfill;      // optional (vec_count): += decodable vectors with a complete data or parity half
   // Optional error-locator sharing: the locators depend only on the erasure
   // pattern, and many vectors of a repair pass share it (every row of a square
   // kept by the same column set).  err_key[v] = 32-bit hash of v's pattern;
@@ -272,15 +273,16 @@ hipError_t launch_repair_defer_check(int32_t* deferred, const int32_t* known, in
 // would leave them.
 hipError_t launch_vec_count(const DecodeArgs& a, hipStream_t s);
 // Repair round counters (int32 slots of the 64-slot counters array):
-// decodable rows / columns of the round (vec_count), deferrals of the round's
-// plan, its fill pair counts, complete axes before the repair, squares left for
-// the deferral check, the previous round's deferrals (moved there by the next
-// round's count launch, so the host reads it with the round's counts), the
-// plan's totals (3 slots), the count launch's last-block ticket.  The host
-// reads slots [0, kCtrRead).
-constexpr int kCtrRowsDec = 0, kCtrColsDec = 1, kCtrDeferred = 2, kCtrPairs = 3, kCtrPairsRev = 4,
-              kCtrComplete = 5, kCtrDeferSquares = 6, kCtrDeferredPrev = 7, kCtrPlan = 8, kCtrRead = 11,
-              kCtrTicket = 12, kCtrSlots = 64;
+// decodable rows / columns of the round and, of those, the fill candidates
+// (a complete data or parity half) per axis (vec_count; the round's last
+// launch clears these four), deferrals of the round's plan, its fill pair
+// counts, complete axes before the repair, squares left for the deferral
+// check, the previous round's deferrals (moved there by the next round's count
+// launch, so the host reads it with the round's counts), the plan's totals (3
+// slots), the count launch's last-block ticket.  The host reads [0, kCtrRead).
+constexpr int kCtrRowsDec = 0, kCtrColsDec = 1, kCtrFillRows = 2, kCtrFillCols = 3, kCtrDeferred = 4,
+              kCtrPairs = 5, kCtrPairsRev = 6, kCtrComplete = 7, kCtrDeferSquares = 8, kCtrDeferredPrev = 9,
+              kCtrPlan = 10, kCtrRead = 13, kCtrTicket = 14, kCtrSlots = 64;
 struct RoundCounters {
   int32_t* ctr;   // device counters (kCtrSlots)
   int32_t* host;  // optional: page-locked host copy of slots [0, kCtrRead), written by the last block,
@@ -288,7 +290,7 @@ struct RoundCounters {
   int32_t seq;
 };
 // Both axes' vec_count of a Repair round in one launch plus the counter
-// bookkeeping above.  Slots kCtrRowsDec / kCtrColsDec must be 0 on entry
+// bookkeeping above.  Slots kCtrRowsDec .. kCtrFillCols must be 0 on entry
 // (the previous round's launch_rs_mark_round clears them).
 hipError_t launch_vec_count_round(const DecodeArgs& a0, const DecodeArgs& a1, const RoundCounters& rc,
                                   hipStream_t s);
@@ -298,8 +300,8 @@ hipError_t launch_rs_mark_present(const DecodeArgs& a, const int32_t* flags, hip
                                   int32_t* known = nullptr);
 // The end of a Repair round in one launch: presence += vectors flagged in
 // a.flags (decoded) or fill (optional, filled); known[v] = 0 where both are
-// set; zero2[0..1] (optional) := 0 for the next round's counts.
-hipError_t launch_rs_mark_round(const DecodeArgs& a, const int32_t* fill, int32_t* known, int32_t* zero2,
+// set; zero4[0..3] (optional) := 0 for the next round's counts.
+hipError_t launch_rs_mark_round(const DecodeArgs& a, const int32_t* fill, int32_t* known, int32_t* zero4,
                                 hipStream_t s);
 // (optional) pre_fail[sq] = 1 where the pre-repair check failed
 hipError_t launch_finalize_repair(const int32_t* bits, const int32_t* complete_before, const int32_t* root_bad,

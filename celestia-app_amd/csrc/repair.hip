@@ -274,6 +274,8 @@ constexpr int kPlanThreads = 256;
 // lane load; otherwise (column axis) one lane per vector, the 2k flags split
 // over the 16 waves of the block and summed in LDS.  (One lane per vector
 // throughout took 0.1 ms per launch at k = 512, 2 squares: 2,048 lanes in all.)
+// blk_cnt[0] += decodable, blk_cnt[1] += decodable with a complete data or
+// parity half (the Repair plan's fill candidates, repair_plan_kernel's f / r)
 __device__ __forceinline__ void vec_count_finish(const DecodeArgs& a, long v, int sys, int tot, int* blk_cnt) {
   const int k = a.k, n = 2 * k;
   const bool decode = tot >= k && tot < n && vec_selected(a, v);
@@ -281,6 +283,13 @@ __device__ __forceinline__ void vec_count_finish(const DecodeArgs& a, long v, in
   if (a.vec_counts) a.vec_counts[v] = sys | (tot << 16);
   if (tot < k && a.too_few) atomicOr(a.too_few, 1);
   if (decode) atomicAdd(blk_cnt, 1);
+  if (decode && (sys == k || tot - sys == k)) atomicAdd(blk_cnt + 1, 1);
+}
+
+__device__ __forceinline__ void vec_count_flush(const DecodeArgs& a, const int* blk_cnt) {
+  if (threadIdx.x != 0) return;
+  if (blk_cnt[0] && a.ndecodable) atomicAdd(a.ndecodable, blk_cnt[0]);
+  if (blk_cnt[1] && a.nfill) atomicAdd(a.nfill, blk_cnt[1]);
 }
 
 // Rows of the presence map: 16 lanes per row (4 rows per wave) when the row's
@@ -288,7 +297,7 @@ __device__ __forceinline__ void vec_count_finish(const DecodeArgs& a, long v, in
 // otherwise (a wave per row spent most of its time launching and reducing:
 // 35 us for 256 k = 128 squares).
 __device__ __forceinline__ void vec_count_rows_block(const DecodeArgs& a, long bid, int* blk_cnt) {
-  if (threadIdx.x == 0) *blk_cnt = 0;
+  if (threadIdx.x == 0) blk_cnt[0] = blk_cnt[1] = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int k = a.k, n = 2 * k;
@@ -334,7 +343,7 @@ __device__ __forceinline__ void vec_count_rows_block(const DecodeArgs& a, long b
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0 && *blk_cnt && a.ndecodable) atomicAdd(a.ndecodable, *blk_cnt);
+  vec_count_flush(a, blk_cnt);
 }
 
 __device__ __forceinline__ void vec_count_cols_block(const DecodeArgs& a, long bid, int* blk_cnt, int* acc_sys,
@@ -344,7 +353,7 @@ __device__ __forceinline__ void vec_count_cols_block(const DecodeArgs& a, long b
   const long sq = bid / nb;
   const long vec = (bid - sq * nb) * 64 + lane;
   if (threadIdx.x < 64) acc_sys[threadIdx.x] = acc_tot[threadIdx.x] = 0;
-  if (threadIdx.x == 0) *blk_cnt = 0;
+  if (threadIdx.x == 0) blk_cnt[0] = blk_cnt[1] = 0;
   __syncthreads();
   const int k = a.k, n = 2 * k;
   if (vec < a.nvec) {
@@ -362,7 +371,7 @@ __device__ __forceinline__ void vec_count_cols_block(const DecodeArgs& a, long b
   __syncthreads();
   if (wave == 0 && vec < a.nvec) vec_count_finish(a, sq * a.nvec + vec, acc_sys[lane], acc_tot[lane], blk_cnt);
   __syncthreads();
-  if (threadIdx.x == 0 && *blk_cnt && a.ndecodable) atomicAdd(a.ndecodable, *blk_cnt);
+  vec_count_flush(a, blk_cnt);
 }
 
 // the 4-rows-per-wave layout of vec_count_rows_block (same condition as the block's)
@@ -383,9 +392,9 @@ __device__ __forceinline__ void vec_count_block(const DecodeArgs& a, long bid, i
 }
 
 __global__ __launch_bounds__(1024) void vec_count_kernel(DecodeArgs a) {
-  __shared__ int blk_cnt;
+  __shared__ int blk_cnt[2];
   __shared__ int acc_sys[64], acc_tot[64];
-  vec_count_block(a, blockIdx.x, &blk_cnt, acc_sys, acc_tot);
+  vec_count_block(a, blockIdx.x, blk_cnt, acc_sys, acc_tot);
 }
 
 hipError_t launch_vec_count(const DecodeArgs& a, hipStream_t s) {
@@ -402,7 +411,7 @@ hipError_t launch_vec_count(const DecodeArgs& a, hipStream_t s) {
 // host mailbox, so the host's read needs no copy of its own.
 __global__ __launch_bounds__(1024) void vec_count_round_kernel(DecodeArgs a0, DecodeArgs a1, long nb0,
                                                                RoundCounters rc) {
-  __shared__ int blk_cnt;
+  __shared__ int blk_cnt[2];
   __shared__ int acc_sys[64], acc_tot[64];
   __shared__ int last_s;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -410,8 +419,8 @@ __global__ __launch_bounds__(1024) void vec_count_round_kernel(DecodeArgs a0, De
     atomicExch(rc.ctr + kCtrPairs, 0);
     atomicExch(rc.ctr + kCtrPairsRev, 0);
   }
-  if ((long)blockIdx.x < nb0) vec_count_block(a0, blockIdx.x, &blk_cnt, acc_sys, acc_tot);
-  else vec_count_block(a1, blockIdx.x - nb0, &blk_cnt, acc_sys, acc_tot);
+  if ((long)blockIdx.x < nb0) vec_count_block(a0, blockIdx.x, blk_cnt, acc_sys, acc_tot);
+  else vec_count_block(a1, blockIdx.x - nb0, blk_cnt, acc_sys, acc_tot);
   if (!rc.host) return;  // uniform
   if (threadIdx.x == 0) {
     // This thread's counter atomics are performed (their completion waited
@@ -580,14 +589,14 @@ __global__ __launch_bounds__(256) void mark_flagged_kernel(DecodeArgs a, const i
 // a column axis ORs in the bytes of flagged columns; threads gid < nsq * w
 // also do the known[] update of vector gid.  A vector is flagged in flags or
 // (optional) flags2; the known[] update follows flags2 when it is given.
-// zero2 (optional): two counters cleared for the next Repair round.
+// zero4 (optional): four counters cleared for the next Repair round.
 __global__ __launch_bounds__(256) void mark_flagged_map_kernel(DecodeArgs a, const int32_t* flags,
                                                                const int32_t* flags2, int32_t* known, int rows,
-                                                               int32_t* zero2) {
+                                                               int32_t* zero4) {
   const int w = 2 * a.k, w4 = w / 4;
   const long gid = (long)blockIdx.x * 256 + threadIdx.x;
   const long nv = a.nsq * w;
-  if (zero2 && gid < 2) zero2[gid] = 0;
+  if (zero4 && gid < 4) zero4[gid] = 0;
   const int32_t* kf = flags2 ? flags2 : flags;
   if (known && gid < nv && kf[gid] && a.flags[gid]) known[gid] = 0;
   if (gid >= nv * w4) return;
@@ -637,7 +646,7 @@ hipError_t launch_rs_mark_present(const DecodeArgs& a, const int32_t* flags, hip
   return hipGetLastError();
 }
 
-hipError_t launch_rs_mark_round(const DecodeArgs& a, const int32_t* fill, int32_t* known, int32_t* zero2,
+hipError_t launch_rs_mark_round(const DecodeArgs& a, const int32_t* fill, int32_t* known, int32_t* zero4,
                                 hipStream_t s) {
   const long nv = a.nsq * a.nvec;
   bool rows = false;
@@ -645,12 +654,12 @@ hipError_t launch_rs_mark_round(const DecodeArgs& a, const int32_t* fill, int32_
     const long w = 2L * a.k;
     const long threads = a.nsq * w * (w / 4);
     hipLaunchKernelGGL(mark_flagged_map_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, a, a.flags,
-                       fill, known, rows ? 1 : 0, zero2);
+                       fill, known, rows ? 1 : 0, zero4);
     return hipGetLastError();
   }
   hipError_t e = launch_rs_mark_present(a, a.flags, s, nullptr);
   if (e == hipSuccess && fill) e = launch_rs_mark_present(a, fill, s, known);
-  if (e == hipSuccess && zero2) e = hipMemsetAsync(zero2, 0, 2 * sizeof(int32_t), s);
+  if (e == hipSuccess && zero4) e = hipMemsetAsync(zero4, 0, 4 * sizeof(int32_t), s);
   return e;
 }
 

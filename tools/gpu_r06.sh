@@ -11,6 +11,16 @@ case "$1" in
     timeout -k 10 600 python -u bench.py > gpurun_out/r06_clean_bench.log 2>&1 || { echo "bench failed"; tail -5 gpurun_out/r06_clean_bench.log; exit 1; }
     tail -c 600 gpurun_out/r06_clean_bench.log
     ;;
+  fillskip)  # round 6: fill-candidate counts from the count launch; fill launches skipped on axes without candidates
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py tests/test_gpu_repair_async.py tests/test_gpu_parity.py tests/test_gpu_bench_checks.py > gpurun_out/r06_fillskip_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r06_fillskip_tests.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 600 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_wide.py -k "not k8192 and not k4096" > gpurun_out/r06_fillskip_wide.log 2>&1
+    rc=$?; echo "wide tests rc=$rc"; tail -3 gpurun_out/r06_fillskip_wide.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 3 repair512 new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 2 repair128 new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 2 repair512q3 new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 256 --batch 8 --steps 10 --warmup 2" new= base=lib:celestia-app_amd/libdagpu_base.so
+    ;;
   q2ke)  # round 6: quarter-lane k = 2048 encoder (16 waves, one workgroup per CU) vs the wide one
     timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_wide.py -k "not k8192" > gpurun_out/r06_q2ke_wide.log 2>&1
     rc=$?; echo "wide tests rc=$rc"; tail -3 gpurun_out/r06_q2ke_wide.log; [ $rc -eq 0 ] || exit $rc
