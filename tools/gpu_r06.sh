@@ -1,6 +1,8 @@
-# Round-6 GPU steps.  Steps comparing against another build expect it in
-# celestia-app_amd/libdagpu_ab_<label>.so (deleted again after the call; .so
-# files are not in git).  Results: the profiles/*_r06*.log named in DESIGN.md.
+# Round-6 GPU steps.  Steps comparing against another build expect it built
+# beforehand on the CPU with tools/build_variant.sh (e.g. `base HEAD` ->
+# celestia-app_amd/libdagpu_base.so, or a -D variant); delete it after the call
+# (.so files are not in git).  Results: the profiles/*_r06*.log named in DESIGN.md.
+# (The `tail` step's switch DAGPU_NMT_TAIL was removed with the kernel it chose.)
 #   bash tools/gpu_r06.sh <step>
 set -o pipefail
 mkdir -p gpurun_out
