@@ -36,6 +36,7 @@ ERR_SQUARE = -13
 EXPORTS = (
     "dagpu_version",
     "dagpu_max_square_width",
+    "dagpu_max_codec_width",
     "dagpu_init",
     "dagpu_destroy",
     "dagpu_last_error",
@@ -146,6 +147,7 @@ def lib() -> ctypes.CDLL:
             L = _Tolerant(L)
         L.dagpu_version.restype = ctypes.c_int
         L.dagpu_max_square_width.restype = ctypes.c_uint32
+        L.dagpu_max_codec_width.restype = ctypes.c_uint32
         L.dagpu_init.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
         L.dagpu_destroy.argtypes = [vp]
         L.dagpu_destroy.restype = None

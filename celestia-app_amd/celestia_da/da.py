@@ -415,10 +415,11 @@ class LeoRSCodec:
         return "Leopard"
 
     def max_chunks(self) -> int:
-        """rsmt2d Codec.MaxChunks: ODS chunks of the widest square this library
-        serves (dagpu_max_square_width()^2; upstream Leopard reports 32768^2,
-        beyond one GPU's HBM -- include/dagpu.h DAGPU_MAX_SQUARE_WIDTH)."""
-        w = int(_abi.lib().dagpu_max_square_width())
+        """rsmt2d Codec.MaxChunks: the square of the widest codec vector
+        (dagpu_max_codec_width()^2 = 32768^2, Leopard GF(2^16)'s 65536 shards,
+        as upstream LeoRSCodec reports).  Squares stop earlier: one GPU holds an
+        EDS up to dagpu_max_square_width() (include/dagpu.h)."""
+        w = int(_abi.lib().dagpu_max_codec_width())
         return w * w
 
     def encode(self, data: Sequence[bytes]) -> List[bytes]:

@@ -362,6 +362,11 @@ uint32_t dagpu_max_square_width(void) {
   return (uint32_t)kMaxK;
 }
 
+uint32_t dagpu_max_codec_width(void) {
+  static_assert(DAGPU_MAX_CODEC_WIDTH == kMaxCodecK, "header and kernels disagree on the widest codec vector");
+  return (uint32_t)kMaxCodecK;
+}
+
 int dagpu_init(int device, dagpu_ctx** out) {
   if (!out) return DAGPU_ERR_ARG;
   *out = nullptr;
@@ -737,7 +742,7 @@ int dagpu_encode(dagpu_ctx* ctx, uint32_t k, size_t nvec, size_t shard_size,
     return set_err(ctx, DAGPU_ERR_SHARE_SIZE, "shard size must be a multiple of 64");
   std::lock_guard<std::mutex> g(ctx->mu);
   (void)hipSetDevice(ctx->device);
-  int rc = check_k(ctx, k);
+  int rc = check_codec_k(ctx, k);
   if (rc) return rc;
   if (nvec == 0) return DAGPU_OK;
   const size_t bytes = (size_t)k * shard_size * nvec;
@@ -772,7 +777,7 @@ int dagpu_decode(dagpu_ctx* ctx, uint32_t k, size_t nvec, size_t shard_size, uin
     return set_err(ctx, DAGPU_ERR_SHARE_SIZE, "shard size must be a multiple of 64");
   std::lock_guard<std::mutex> g(ctx->mu);
   (void)hipSetDevice(ctx->device);
-  int rc = check_k(ctx, k);
+  int rc = check_codec_k(ctx, k);
   if (rc) return rc;
   if (nvec == 0) return DAGPU_OK;
   const size_t n = 2 * (size_t)k;

@@ -15,6 +15,13 @@ constexpr int kDigest = 32;
 // HBM, k = 16384 (512 GiB) does not.  GF(2^16) above k = 128; register-resident
 // kernels at k = 256 / 512, LDS-slice kernels (rs_gf16_wide.hip) above.
 constexpr int kMaxK = 8192;
+// Widest codec vector (rsmt2d.Codec Encode / Decode, dagpu_encode / dagpu_decode):
+// Leopard GF(2^16)'s whole field, k data + k parity = 65536 shards (klauspost
+// leopardFF16 rejects more; rsmt2d LeoRSCodec.MaxChunks = 32768 * 32768).  A
+// vector is k x shard bytes, so these widths fit one GPU even where the square
+// of the same width does not; the wide kernels serve k = 16384 / 32768 with
+// 2- / 1-symbol LDS slices (rs_gf16_wide.hip).
+constexpr int kMaxCodecK = 32768;
 
 // Bytes of error-locator workspace per decoded vector.
 // Error-locator workspace per vector: GF(2^8) 256 B; GF(2^16) the n = 2k uint16

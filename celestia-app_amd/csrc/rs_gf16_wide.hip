@@ -1,5 +1,6 @@
 // rs_gf16_wide.hip -- Leopard GF(2^16) encode / reconstruct for wide squares,
-// k = 1024 .. kMaxK (2k = 2048 .. 16384 shards per vector).
+// k = 1024 .. kMaxK (2k = 2048 .. 16384 shards per vector), and for codec
+// vectors up to kMaxCodecK (2k = 65536 shards, Leopard's whole field).
 //
 // Replaces klauspost/reedsolomon v1.11.8 leopardFF16 encode / reconstruct
 // (leopard.go), which rsmt2d v0.11.0 LeoRSCodec uses for every width above
@@ -16,12 +17,15 @@
 // vector in LDS -- S symbols of every element (S = 32 / 16 / 8 / 4, chosen so
 // the slice stays <= 128 KiB) as a low-byte plane and a high-byte plane of
 // dwords (4 symbols per dword, element-major, one pad dword per element
-// against bank conflicts).  Each butterfly stage is one pass of radix-4 units
+// against bank conflicts).  Codec vectors past the widest square (n = 32768 /
+// 65536 elements) keep 2 / 1 symbols per element, low and high bytes packed in
+// one dword / one 16-bit word (PK = 2 / 1); registers hold them as the same
+// lo / hi dwords with zero upper bytes, which every multiply keeps zero.  Each butterfly stage is one pass of radix-4 units
 // (4 elements x G dword groups per lane, both layers of the radix-4 step in
 // registers, one barrier per stage).  A multiply by a skew constant is the
 // 16-dword product table of that skew position (the products of every 2-bit
 // group of a symbol, low and high bytes, for v_perm; 1 MiB for all positions
-// < 2 kMaxK), loaded once per unit and applied to its G groups.  The decoder's
+// < 2 kMaxCodecK), loaded once per unit and applied to its G groups.  The decoder's
 // per-element errLocs multiplies use one product table per element (exp gathers;
 // log/exp gathers per symbol at 4 symbols per element).
 #include <hip/hip_runtime.h>
@@ -47,14 +51,14 @@ constexpr uint32_t kMod = 65535u;
 // profiles/gf16_wide_ab_r06.log).
 constexpr int kWideThreads = 512;
 template <int NG>
-constexpr int dec_threads() { return NG <= 4 ? 1024 : 512; }
-constexpr int kPtabPos = 2 * kMaxK;  // skew positions used by any transform <= 2 kMaxK
+constexpr int dec_threads() { return NG <= 4 ? 1024 : 512; }  // (packed slices: NG = 1)
+constexpr int kPtabPos = 2 * kMaxCodecK;  // skew positions used by any transform <= 2 kMaxCodecK
 
 struct WideTabs {
   const uint16_t* log;
   const uint16_t* exp;
   const uint32_t* ptab;   // kPtabPos x kTabW dwords
-  const uint16_t* wfold;  // folded Walsh weights, n = 2048 .. 2 kMaxK, back to back
+  const uint16_t* wfold;  // folded Walsh weights, n = 2048 .. 2 kMaxCodecK, back to back
 };
 
 __device__ __forceinline__ uint32_t xor3w(uint32_t a, uint32_t b, uint32_t c) {
@@ -82,13 +86,18 @@ __device__ __forceinline__ void pmul_add(uint32_t& xlo, uint32_t& xhi, uint32_t 
   xhi = xor3w(xor3w(xor3w(xhi, h0, h1), h2, h3), h4, h5);
 }
 
-// The only zero skews (log 0) sit at positions 2^m - 1 (Leopard skips their
-// multiply): the block at offset 0 of every layer, all of the top layer.
-// Leopard's initFFTSkew zeroes FFTSkew[2^m - 1] only for m <= kBits - 2 = 14
-// (position 32767 has a nonzero skew), so the bit test holds only while every
-// position a transform uses stays below 2^14.
-static_assert(kPtabPos <= (1 << 14), "zero_skew: FFTSkew[2^m - 1] is log 0 only for m <= 14");
-__device__ __forceinline__ bool zero_skew(int pos) { return ((pos + 1) & pos) == 0; }
+// The only zero skews (log 0) below 2^14 sit at positions 2^m - 1 (Leopard
+// skips their multiply): the block at offset 0 of every layer, all of the top
+// layer.  Leopard's initFFTSkew zeroes FFTSkew[2^m - 1] only for m <= kBits - 2
+// = 14 (position 32767 has a nonzero skew), so the bit test is used only below
+// 2^14; a position above (ZG: transforms that reach past 2^14 positions, the
+// codec vectors past k = 8192) always multiplies, by its table, which is all
+// zero where the skew is log 0 (tables() below), so a zero skew there still
+// adds nothing.  Square transforms (m, n <= 16384) stay below 2^14.
+template <bool ZG>
+__device__ __forceinline__ bool zero_skew(int pos) {
+  return (!ZG || pos < (1 << 14)) && ((pos + 1) & pos) == 0;
+}
 __device__ __forceinline__ void load_tab(const WideTabs& T, int pos, uint32_t (&t)[kTabW]) {
   const uint4* p = (const uint4*)(T.ptab + (long)pos * kTabW);
 #pragma unroll
@@ -223,36 +232,97 @@ __device__ __forceinline__ void mul_elem(const WideTabs& T, uint32_t (&lo)[NG], 
 
 // LDS planes: lo[e * NGP + g], hi[...] (NG = S / 4 dword groups, NGP = NG + 1
 // for odd element strides, so lanes on different elements spread over banks;
-// NG = 2 is used only at n = 8192, where a pad dword would not fit 160 KiB)
-template <int NG>
+// NG = 2 is used only at n = 8192, where a pad dword would not fit 160 KiB).
+// PK = 2 / 1 (NG = 1): one packed word per element, lo[e] = lo16 | hi16 << 16
+// (2 symbols) or ((uint16_t*)lo)[e] = lo8 | hi8 << 8 (1 symbol); hi unused.
+template <int NG_, int PK_ = 0>
 struct Planes {
+  static constexpr int NG = NG_, PK = PK_;
+  static_assert(PK == 0 || NG == 1, "packed slices hold one group");
   static constexpr int NGP = NG <= 2 ? NG : NG + 1;
+  static constexpr int SYM = PK ? PK : 4 * NG;  // symbols per element in the slice
   uint32_t* lo;
   uint32_t* hi;
   __device__ __forceinline__ int at(int e, int g) const { return e * NGP + g; }
+  __device__ __forceinline__ void get(int e, int g, uint32_t& l, uint32_t& h) const {
+    if constexpr (PK == 0) {
+      l = lo[at(e, g)];
+      h = hi[at(e, g)];
+    } else if constexpr (PK == 2) {
+      const uint32_t d = lo[e];
+      l = d & 0xFFFFu;
+      h = d >> 16;
+    } else {
+      const uint32_t d = ((const uint16_t*)lo)[e];
+      l = d & 0xFFu;
+      h = d >> 8;
+    }
+  }
+  __device__ __forceinline__ void put(int e, int g, uint32_t l, uint32_t h) const {
+    if constexpr (PK == 0) {
+      lo[at(e, g)] = l;
+      hi[at(e, g)] = h;
+    } else if constexpr (PK == 2) {
+      lo[e] = l | (h << 16);
+    } else {
+      ((uint16_t*)lo)[e] = (uint16_t)(l | (h << 8));
+    }
+  }
+  // LDS bytes of an n-element slice
+  static constexpr size_t bytes(int n) { return PK ? (size_t)n * PK * 2 : (size_t)2 * n * NGP * 4; }
 };
 
+// Global memory side of a slice group: p is the group's low-byte dword (4
+// symbols at b[i], high bytes at b[i + 32]), or for packed slices its 2 / 1
+// low bytes.
+template <int PK>
+__device__ __forceinline__ void gload(const uint8_t* p, uint32_t& lo, uint32_t& hi) {
+  if constexpr (PK == 0) {
+    lo = ((const uint32_t*)p)[0];
+    hi = ((const uint32_t*)p)[8];
+  } else if constexpr (PK == 2) {
+    lo = ((const uint16_t*)p)[0];
+    hi = ((const uint16_t*)p)[16];
+  } else {
+    lo = p[0];
+    hi = p[32];
+  }
+}
+template <int PK>
+__device__ __forceinline__ void gstore(uint8_t* p, uint32_t lo, uint32_t hi) {
+  if constexpr (PK == 0) {
+    ((uint32_t*)p)[0] = lo;
+    ((uint32_t*)p)[8] = hi;
+  } else if constexpr (PK == 2) {
+    ((uint16_t*)p)[0] = (uint16_t)lo;
+    ((uint16_t*)p)[16] = (uint16_t)hi;
+  } else {
+    p[0] = (uint8_t)lo;
+    p[32] = (uint8_t)hi;
+  }
+}
+template <int PK>
+__device__ __forceinline__ bool gdiffers(const uint8_t* p, uint32_t lo, uint32_t hi) {
+  uint32_t l, h;
+  gload<PK>(p, l, h);
+  return l != lo || h != hi;
+}
+
 // One radix-4 (or radix-2) unit: elements e[0..R), dword groups g0 .. g0+G-1.
-template <int NG, int G, int R>
+template <class PL, int G, int R>
 struct Unit {
   uint32_t lo[R][G], hi[R][G];
-  __device__ __forceinline__ void load(const Planes<NG>& P, const int (&e)[R], int g0) {
+  __device__ __forceinline__ void load(const PL& P, const int (&e)[R], int g0) {
 #pragma unroll
     for (int r = 0; r < R; r++)
 #pragma unroll
-      for (int g = 0; g < G; g++) {
-        lo[r][g] = P.lo[P.at(e[r], g0 + g)];
-        hi[r][g] = P.hi[P.at(e[r], g0 + g)];
-      }
+      for (int g = 0; g < G; g++) P.get(e[r], g0 + g, lo[r][g], hi[r][g]);
   }
-  __device__ __forceinline__ void store(const Planes<NG>& P, const int (&e)[R], int g0) const {
+  __device__ __forceinline__ void store(const PL& P, const int (&e)[R], int g0) const {
 #pragma unroll
     for (int r = 0; r < R; r++)
 #pragma unroll
-      for (int g = 0; g < G; g++) {
-        P.lo[P.at(e[r], g0 + g)] = lo[r][g];
-        P.hi[P.at(e[r], g0 + g)] = hi[r][g];
-      }
+      for (int g = 0; g < G; g++) P.put(e[r], g0 + g, lo[r][g], hi[r][g]);
   }
   // ifftDIT2: y ^= x; x ^= y * skew (zero: the skew is log 0, no multiply)
   __device__ __forceinline__ void ifft2(int i, int j, const uint32_t (&t)[kTabW], bool zero) {
@@ -293,9 +363,9 @@ __device__ __forceinline__ void load_tab_u(const WideTabs& T, int pos, uint32_t 
 // One radix-4 IFFT step (dist, dist4 = 4 dist) over all units.  UNI: the 64
 // units of a wave lie in one block of 4 dist elements (dist * CH >= 64), so
 // their three skew positions are wave-uniform and the tables come by scalar loads.
-template <int NG, int G, bool UNI, int TH>
-__device__ __forceinline__ void ifft_step(const Planes<NG>& P, const WideTabs& T, int n, int base, int dist) {
-  constexpr int CH = NG / G;
+template <class PL, int G, bool UNI, int TH, bool ZG>
+__device__ __forceinline__ void ifft_step(const PL& P, const WideTabs& T, int n, int base, int dist) {
+  constexpr int CH = PL::NG / G;
   const int dist4 = dist << 2;
   const int units = (n / 4) * CH;
   uint32_t t[kTabW];
@@ -303,19 +373,19 @@ __device__ __forceinline__ void ifft_step(const Planes<NG>& P, const WideTabs& T
     const int quad = u / CH, g0 = (u - quad * CH) * G;
     const int r = (quad / dist) * dist4, i = r + (quad % dist), iend = r + dist;
     const int e[4] = {i, i + dist, i + 2 * dist, i + 3 * dist};
-    Unit<NG, G, 4> x;
+    Unit<PL, G, 4> x;
     x.load(P, e, g0);
     auto tab = [&](int pos) {
       if constexpr (UNI) load_tab_u(T, pos, t);
       else load_tab(T, pos, t);
     };
-    bool z = zero_skew(base + iend);
+    bool z = zero_skew<ZG>(base + iend);
     if (!z) tab(base + iend);
     x.ifft2(0, 1, t, z);
-    z = zero_skew(base + iend + 2 * dist);
+    z = zero_skew<ZG>(base + iend + 2 * dist);
     if (!z) tab(base + iend + 2 * dist);
     x.ifft2(2, 3, t, z);
-    z = zero_skew(base + iend + dist);
+    z = zero_skew<ZG>(base + iend + dist);
     if (!z) tab(base + iend + dist);
     x.ifft2(0, 2, t, z);
     x.ifft2(1, 3, t, z);
@@ -326,25 +396,25 @@ __device__ __forceinline__ void ifft_step(const Planes<NG>& P, const WideTabs& T
 
 // ifftDITEncoder / ifftDITDecoder over n elements (mtrunc = n), skew index
 // base + iend (encoder: base = IO - 1; decoder: -1)
-template <int NG, int G, int TH>
-__device__ void wide_ifft(const Planes<NG>& P, const WideTabs& T, int n, int base) {
-  constexpr int CH = NG / G;
+template <class PL, int G, int TH, bool ZG>
+__device__ void wide_ifft(const PL& P, const WideTabs& T, int n, int base) {
+  constexpr int CH = PL::NG / G;
   int dist = 1, dist4 = 4;
   while (dist4 <= n) {
-    if (dist * CH >= 64) ifft_step<NG, G, true, TH>(P, T, n, base, dist);
-    else ifft_step<NG, G, false, TH>(P, T, n, base, dist);
+    if (dist * CH >= 64) ifft_step<PL, G, true, TH, ZG>(P, T, n, base, dist);
+    else ifft_step<PL, G, false, TH, ZG>(P, T, n, base, dist);
     dist = dist4;
     dist4 <<= 2;
   }
   if (dist < n) {  // one radix-2 layer left (log2 n odd): one position for all
     const int units = (n / 2) * CH;
     uint32_t t[kTabW];
-    const bool z = zero_skew(base + dist);
+    const bool z = zero_skew<ZG>(base + dist);
     if (!z) load_tab_u(T, base + dist, t);
     for (int u = threadIdx.x; u < units; u += TH) {
       const int p = u / CH, g0 = (u - p * CH) * G;
       const int e[2] = {p, p + dist};
-      Unit<NG, G, 2> x;
+      Unit<PL, G, 2> x;
       x.load(P, e, g0);
       x.ifft2(0, 1, t, z);
       x.store(P, e, g0);
@@ -354,9 +424,9 @@ __device__ void wide_ifft(const Planes<NG>& P, const WideTabs& T, int n, int bas
 }
 
 // One radix-4 FFT step (fftDIT, skew index fo + iend - 1); UNI as ifft_step.
-template <int NG, int G, bool UNI, int TH>
-__device__ __forceinline__ void fft_step(const Planes<NG>& P, const WideTabs& T, int n, int fo, int dist) {
-  constexpr int CH = NG / G;
+template <class PL, int G, bool UNI, int TH, bool ZG>
+__device__ __forceinline__ void fft_step(const PL& P, const WideTabs& T, int n, int fo, int dist) {
+  constexpr int CH = PL::NG / G;
   const int dist4 = dist << 2;
   const int units = (n / 4) * CH;
   uint32_t t[kTabW];
@@ -364,20 +434,20 @@ __device__ __forceinline__ void fft_step(const Planes<NG>& P, const WideTabs& T,
     const int quad = u / CH, g0 = (u - quad * CH) * G;
     const int r = (quad / dist) * dist4, i = r + (quad % dist), iend = r + dist;
     const int e[4] = {i, i + dist, i + 2 * dist, i + 3 * dist};
-    Unit<NG, G, 4> x;
+    Unit<PL, G, 4> x;
     x.load(P, e, g0);
     auto tab = [&](int pos) {
       if constexpr (UNI) load_tab_u(T, pos, t);
       else load_tab(T, pos, t);
     };
-    bool z = zero_skew(fo + iend + dist - 1);
+    bool z = zero_skew<ZG>(fo + iend + dist - 1);
     if (!z) tab(fo + iend + dist - 1);
     x.fft2(0, 2, t, z);
     x.fft2(1, 3, t, z);
-    z = zero_skew(fo + iend - 1);
+    z = zero_skew<ZG>(fo + iend - 1);
     if (!z) tab(fo + iend - 1);
     x.fft2(0, 1, t, z);
-    z = zero_skew(fo + iend + 2 * dist - 1);
+    z = zero_skew<ZG>(fo + iend + 2 * dist - 1);
     if (!z) tab(fo + iend + 2 * dist - 1);
     x.fft2(2, 3, t, z);
     x.store(P, e, g0);
@@ -386,13 +456,13 @@ __device__ __forceinline__ void fft_step(const Planes<NG>& P, const WideTabs& T,
 }
 
 // fftDIT over n elements (mtrunc = n), skew index fo + iend - 1
-template <int NG, int G, int TH>
-__device__ void wide_fft(const Planes<NG>& P, const WideTabs& T, int n, int fo) {
-  constexpr int CH = NG / G;
+template <class PL, int G, int TH, bool ZG>
+__device__ void wide_fft(const PL& P, const WideTabs& T, int n, int fo) {
+  constexpr int CH = PL::NG / G;
   int dist4 = n, dist = n >> 2;
   while (dist != 0) {
-    if (dist * CH >= 64) fft_step<NG, G, true, TH>(P, T, n, fo, dist);
-    else fft_step<NG, G, false, TH>(P, T, n, fo, dist);
+    if (dist * CH >= 64) fft_step<PL, G, true, TH, ZG>(P, T, n, fo, dist);
+    else fft_step<PL, G, false, TH, ZG>(P, T, n, fo, dist);
     dist4 = dist;
     dist >>= 2;
   }
@@ -402,9 +472,9 @@ __device__ void wide_fft(const Planes<NG>& P, const WideTabs& T, int n, int fo) 
     for (int u = threadIdx.x; u < units; u += TH) {
       const int p = u / CH, g0 = (u - p * CH) * G;
       const int e[2] = {2 * p, 2 * p + 1};
-      const bool z = zero_skew(fo + 2 * p);
+      const bool z = zero_skew<ZG>(fo + 2 * p);
       if (!z) load_tab(T, fo + 2 * p, t);
-      Unit<NG, G, 2> x;
+      Unit<PL, G, 2> x;
       x.load(P, e, g0);
       x.fft2(0, 1, t, z);
       x.store(P, e, g0);
@@ -414,16 +484,16 @@ __device__ void wide_fft(const Planes<NG>& P, const WideTabs& T, int n, int fo) 
 }
 
 // Column slice of a workgroup: blockIdx -> (vector v, 64-B block, slice of
-// S = 4 NG symbols).  Consecutive logical blocks (the slices and blocks of one
+// S symbols: 4 NG, or PK for packed slices).  Consecutive logical blocks (the slices and blocks of one
 // vector, which share cache lines) are kept on one XCD: hardware dispatch
 // deals workgroups round-robin over the 8 XCDs.
 struct SliceCoord {
   long v, blk;
   int sl;
 };
-template <int NG>
+template <int S>
 __device__ __forceinline__ SliceCoord slice_of(long nblk) {
-  constexpr int nsl = 8 / NG;
+  constexpr int nsl = 32 / S;
   long b = blockIdx.x;
   const long G = gridDim.x;
   if ((G & 7) == 0) b = (b & 7) * (G >> 3) + (b >> 3);
@@ -440,42 +510,40 @@ __device__ __forceinline__ SliceCoord slice_of(long nblk) {
 // other encoders: Q0 placement copy, compare mode (mismatch), Repair fill
 // (out_present / redo), reverse fill (IFFT at skew offset 0, FFT at m).
 // ---------------------------------------------------------------------------
-template <int NG, int G>
+template <int NG, int G, int PK = 0>
 __global__ __launch_bounds__(kWideThreads) void leo16w_encode_kernel(EncodeArgs a, WideTabs T, int k) {
+  using PL = Planes<NG, PK>;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  Planes<NG> P{lds, lds + k * Planes<NG>::NGP};
-  const SliceCoord c = slice_of<NG>(a.shard_bytes / 64);
+  PL P{lds, lds + k * PL::NGP};
+  const SliceCoord c = slice_of<PL::SYM>(a.shard_bytes / 64);
   const long sq = c.v / a.nvec, vec = c.v % a.nvec;
   if (vec_skipped(a, c.v)) return;  // uniform
-  const long col = c.blk * 64 + (long)c.sl * 4 * NG;  // byte of lo dword 0 of this slice
+  const long col = c.blk * 64 + (long)c.sl * PL::SYM;  // byte of lo dword 0 of this slice
   const uint8_t* in = a.in + sq * a.in_sq_stride + vec * a.in_vec_stride + col;
   uint8_t* cp = a.copy ? a.copy + sq * a.copy_sq_stride + vec * a.copy_vec_stride + col : nullptr;
   for (int t = threadIdx.x; t < k * NG; t += kWideThreads) {
     const int e = t / NG, g = t - e * NG;
-    const uint32_t* src = (const uint32_t*)(in + (long)e * a.in_shard_stride) + g;
-    const uint32_t lo = src[0], hi = src[8];
-    P.lo[P.at(e, g)] = lo;
-    P.hi[P.at(e, g)] = hi;
-    if (cp) {
-      uint32_t* dst = (uint32_t*)(cp + (long)e * a.copy_shard_stride) + g;
-      dst[0] = lo;
-      dst[8] = hi;
-    }
+    uint32_t lo, hi;
+    gload<PK>(in + (long)e * a.in_shard_stride + 4 * g, lo, hi);
+    P.put(e, g, lo, hi);
+    if (cp) gstore<PK>(cp + (long)e * a.copy_shard_stride + 4 * g, lo, hi);
   }
   __syncthreads();
-  wide_ifft<NG, G, kWideThreads>(P, T, k, a.reverse ? -1 : k - 1);
-  wide_fft<NG, G, kWideThreads>(P, T, k, a.reverse ? k : 0);
+  // positions up to 2k - 2: past 2^14 only for k >= 16384 (NG = 1 or packed)
+  constexpr bool ZG = NG == 1;
+  wide_ifft<PL, G, kWideThreads, ZG>(P, T, k, a.reverse ? -1 : k - 1);
+  wide_fft<PL, G, kWideThreads, ZG>(P, T, k, a.reverse ? k : 0);
   uint8_t* out = a.out + sq * a.out_sq_stride + vec * a.out_vec_stride + col;
   bool diff = false;
   for (int t = threadIdx.x; t < k * NG; t += kWideThreads) {
     const int e = t / NG, g = t - e * NG;
-    const uint32_t lo = P.lo[P.at(e, g)], hi = P.hi[P.at(e, g)];
-    uint32_t* dst = (uint32_t*)(out + (long)e * a.out_shard_stride) + g;
+    uint32_t lo, hi;
+    P.get(e, g, lo, hi);
+    uint8_t* dst = out + (long)e * a.out_shard_stride + 4 * g;
     if (a.mismatch || (a.out_present && fill_given(a, sq, vec, e))) {
-      diff |= (dst[0] != lo) || (dst[8] != hi);
+      diff |= gdiffers<PK>(dst, lo, hi);
     } else {
-      dst[0] = lo;
-      dst[8] = hi;
+      gstore<PK>(dst, lo, hi);
     }
   }
   if (a.mismatch && diff) {
@@ -488,7 +556,9 @@ __global__ __launch_bounds__(kWideThreads) void leo16w_encode_kernel(EncodeArgs 
 // ---------------------------------------------------------------------------
 // Error locators (leopard.go reconstruct, first part) from n-point transforms:
 // FWHT_n(FWHT_n(e) * wfold), wfold[r] = sum_q logWalsh[q n + r] mod 65535
-// (see rs_gf16.hip leo16_errlocs_fold_kernel; n = 2k up to 2 kMaxK here).
+// (see rs_gf16.hip leo16_errlocs_fold_kernel; n = 2k up to 2 kMaxCodecK here:
+// ET = uint32_t LDS words up to n = 32768, uint16_t at 65536 -- every value is
+// a residue mod 65535, so 16 bits hold it -- both 128 KiB).
 // ---------------------------------------------------------------------------
 constexpr int kFoldThreads = 512;
 
@@ -501,14 +571,15 @@ __device__ __forceinline__ uint32_t sub_mod(uint32_t a, uint32_t b) {
   return (d + (d >> 16)) & 0xFFFFu;
 }
 
-__device__ void fwht_rt(uint32_t* e, int n) {
+template <typename ET>
+__device__ void fwht_rt(ET* e, int n) {
   int dist = 1;
   if ((__builtin_ctz(n) & 1) != 0) {  // odd log2: one radix-2 stage first
     for (int g = threadIdx.x; g < n / 2; g += kFoldThreads) {
       const int i = 2 * g;
       const uint32_t t0 = e[i], t1 = e[i + 1];
-      e[i] = add_mod(t0, t1);
-      e[i + 1] = sub_mod(t0, t1);
+      e[i] = (ET)add_mod(t0, t1);
+      e[i + 1] = (ET)sub_mod(t0, t1);
     }
     __syncthreads();
     dist = 2;
@@ -521,17 +592,22 @@ __device__ void fwht_rt(uint32_t* e, int n) {
       const uint32_t t0 = e[i], t1 = e[i + dist], t2 = e[i + 2 * dist], t3 = e[i + 3 * dist];
       const uint32_t a0 = add_mod(t0, t1), a1 = sub_mod(t0, t1);
       const uint32_t a2 = add_mod(t2, t3), a3 = sub_mod(t2, t3);
-      e[i] = add_mod(a0, a2);
-      e[i + 2 * dist] = sub_mod(a0, a2);
-      e[i + dist] = add_mod(a1, a3);
-      e[i + 3 * dist] = sub_mod(a1, a3);
+      e[i] = (ET)add_mod(a0, a2);
+      e[i + 2 * dist] = (ET)sub_mod(a0, a2);
+      e[i + dist] = (ET)add_mod(a1, a3);
+      e[i + 3 * dist] = (ET)sub_mod(a1, a3);
     }
     __syncthreads();
   }
 }
 
+template <typename ET>
 __global__ __launch_bounds__(kFoldThreads) void leo16w_errlocs_kernel(DecodeArgs a, WideTabs T, long wf_off) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t e[];
+  extern __shared__ __attribute__((aligned(16))) uint32_t e_lds[];
+  ET* e = (ET*)e_lds;
+  // bit r of miss: element threadIdx.x + r * kFoldThreads is missing (n <= 64 *
+  // kFoldThreads; the 16-bit build, n = 65536, reads the presence bytes again)
+  constexpr bool kMissBits = sizeof(ET) == 4;
   __shared__ int cnt_s;
   const long v = blockIdx.x;
   const long sq = v / a.nvec, vec = v % a.nvec;
@@ -543,12 +619,15 @@ __global__ __launch_bounds__(kFoldThreads) void leo16w_errlocs_kernel(DecodeArgs
   if (threadIdx.x == 0) cnt_s = 0;
   __syncthreads();
   int cnt = 0;
-  uint32_t miss = 0;  // bit r: element threadIdx.x + r * kFoldThreads is missing (n <= 32 * kFoldThreads)
+  uint64_t miss = 0;
+  auto missing = [&](int i) -> uint32_t {
+    return i < k ? (pres[(long)(k + i) * a.p_shard_stride] ? 0u : 1u)   // parity k+i -> work i
+                 : (pres[(long)(i - k) * a.p_shard_stride] ? 0u : 1u);  // data i-k -> work i
+  };
   for (int i = threadIdx.x, r = 0; i < n; i += kFoldThreads, r++) {
-    const uint32_t x = i < k ? (pres[(long)(k + i) * a.p_shard_stride] ? 0u : 1u)   // parity k+i -> work i
-                             : (pres[(long)(i - k) * a.p_shard_stride] ? 0u : 1u);  // data i-k -> work i
-    e[i] = x;
-    miss |= x << r;
+    const uint32_t x = missing(i);
+    e[i] = (ET)x;
+    if constexpr (kMissBits) miss |= (uint64_t)x << r;
     cnt += (x == 0);
   }
   atomicAdd(&cnt_s, cnt);
@@ -567,7 +646,7 @@ __global__ __launch_bounds__(kFoldThreads) void leo16w_errlocs_kernel(DecodeArgs
   if (!err_computes(a, v, hv)) return;  // shares an earlier vector's locators
   fwht_rt(e, n);
   const uint16_t* wf = T.wfold + wf_off;
-  for (int i = threadIdx.x; i < n; i += kFoldThreads) e[i] = (e[i] * (uint32_t)wf[i]) % kMod;
+  for (int i = threadIdx.x; i < n; i += kFoldThreads) e[i] = (ET)(((uint32_t)e[i] * (uint32_t)wf[i]) % kMod);
   __syncthreads();
   fwht_rt(e, n);
   uint16_t* out = (uint16_t*)(a.err + hv * (long)rs_err_bytes(k));
@@ -580,8 +659,9 @@ __global__ __launch_bounds__(kFoldThreads) void leo16w_errlocs_kernel(DecodeArgs
   if (rs_err_elem_bytes(a.k) == 32) {  // (k = 1024: leo16_errlocs_fold_kernel<2048> writes 80-B tables)
     uint4* pbo = (uint4*)(a.err + hv * (long)rs_err_bytes(k) + rs_err_tab_off(k));
     for (int i = threadIdx.x, r = 0; i < n; i += kFoldThreads, r++) {
-      const uint32_t lm0 = e[i] & 0xFFFFu;
-      const uint32_t lm = ((miss >> r) & 1) ? kMod - lm0 : lm0;
+      const uint32_t lm0 = (uint32_t)e[i] & 0xFFFFu;
+      const bool gone = kMissBits ? ((miss >> r) & 1) != 0 : missing(i) != 0;
+      const uint32_t lm = gone ? kMod - lm0 : lm0;
       uint32_t p[8];
 #pragma unroll
       for (int b = 0; b < 16; b += 2) {
@@ -605,18 +685,19 @@ __global__ __launch_bounds__(kFoldThreads) void leo16w_errlocs_kernel(DecodeArgs
 // elements above e, so element chunks are processed in ascending order, each
 // reading before a barrier and writing after it.
 // ---------------------------------------------------------------------------
-template <int NG, int G>
+template <int NG, int G, int PK = 0>
 __global__ __launch_bounds__(dec_threads<NG>()) void leo16w_decode_kernel(DecodeArgs a, WideTabs T) {
+  using PL = Planes<NG, PK>;
   constexpr int TH = dec_threads<NG>();
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   constexpr int CH = NG / G;
   const int k = a.k, n = 2 * k;
-  Planes<NG> P{lds, lds + n * Planes<NG>::NGP};
-  const SliceCoord c = slice_of<NG>(a.shard_bytes / 64);
+  PL P{lds, lds + n * PL::NGP};
+  const SliceCoord c = slice_of<PL::SYM>(a.shard_bytes / 64);
   const long v = c.v;
   if (a.flags[v] == 0) return;  // uniform
   const long sq = v / a.nvec, vec = v % a.nvec;
-  const long col = c.blk * 64 + (long)c.sl * 4 * NG;
+  const long col = c.blk * 64 + (long)c.sl * PL::SYM;
   uint8_t* base = a.data + sq * a.sq_stride + vec * a.vec_stride + col;
   const uint8_t* pres = a.present + sq * a.p_sq_stride + vec * a.p_vec_stride;
   const uint16_t* err = (const uint16_t*)(a.err + err_vec(a, v) * (long)rs_err_bytes(k));
@@ -628,30 +709,22 @@ __global__ __launch_bounds__(dec_threads<NG>()) void leo16w_decode_kernel(Decode
   for (int i = threadIdx.x; i < n; i += TH) {
     const long shard = i < k ? k + i : i - k;
     if (pres[shard * a.p_shard_stride]) {
-      const uint32_t* src = (const uint32_t*)(base + shard * a.shard_stride);
+      const uint8_t* src = base + shard * a.shard_stride;
       uint32_t lo[NG], hi[NG];
 #pragma unroll
-      for (int g = 0; g < NG; g++) {
-        lo[g] = src[g];
-        hi[g] = src[8 + g];
-      }
+      for (int g = 0; g < NG; g++) gload<PK>(src + 4 * g, lo[g], hi[g]);
       if (pbase) mul_elem_pb<NG>(pbase + (long)i * 32, lo, hi);
       else mul_elem<NG>(T, lo, hi, err[i]);
 #pragma unroll
-      for (int g = 0; g < NG; g++) {
-        P.lo[P.at(i, g)] = lo[g];
-        P.hi[P.at(i, g)] = hi[g];
-      }
+      for (int g = 0; g < NG; g++) P.put(i, g, lo[g], hi[g]);
     } else {
 #pragma unroll
-      for (int g = 0; g < NG; g++) {
-        P.lo[P.at(i, g)] = 0u;
-        P.hi[P.at(i, g)] = 0u;
-      }
+      for (int g = 0; g < NG; g++) P.put(i, g, 0u, 0u);
     }
   }
   __syncthreads();
-  wide_ifft<NG, G, TH>(P, T, n, -1);
+  constexpr bool ZG = PK != 0;  // positions below n - 1: past 2^14 only for n >= 32768 (packed)
+  wide_ifft<PL, G, TH, ZG>(P, T, n, -1);
   {  // formal derivative, ascending chunks of X elements
     constexpr int X = TH / CH;
     for (int x0 = 0; x0 < n; x0 += X) {
@@ -661,48 +734,38 @@ __global__ __launch_bounds__(dec_threads<NG>()) void leo16w_decode_kernel(Decode
       const bool act = x < n;
       if (act) {
 #pragma unroll
-        for (int g = 0; g < G; g++) {
-          dl[g] = P.lo[P.at(x, g0 + g)];
-          dh[g] = P.hi[P.at(x, g0 + g)];
-        }
+        for (int g = 0; g < G; g++) P.get(x, g0 + g, dl[g], dh[g]);
         for (int b = 1; b < n; b <<= 1) {
           if (x & b) continue;
 #pragma unroll
           for (int g = 0; g < G; g++) {
-            dl[g] ^= P.lo[P.at(x + b, g0 + g)];
-            dh[g] ^= P.hi[P.at(x + b, g0 + g)];
+            uint32_t l, h;
+            P.get(x + b, g0 + g, l, h);
+            dl[g] ^= l;
+            dh[g] ^= h;
           }
         }
       }
       __syncthreads();
       if (act) {
 #pragma unroll
-        for (int g = 0; g < G; g++) {
-          P.lo[P.at(x, g0 + g)] = dl[g];
-          P.hi[P.at(x, g0 + g)] = dh[g];
-        }
+        for (int g = 0; g < G; g++) P.put(x, g0 + g, dl[g], dh[g]);
       }
       __syncthreads();
     }
   }
-  wide_fft<NG, G, TH>(P, T, n, 0);
+  wide_fft<PL, G, TH, ZG>(P, T, n, 0);
   for (int i = threadIdx.x; i < n; i += TH) {
     const long shard = i < k ? k + i : i - k;
     if (pres[shard * a.p_shard_stride]) continue;
     uint32_t lo[NG], hi[NG];
 #pragma unroll
-    for (int g = 0; g < NG; g++) {
-      lo[g] = P.lo[P.at(i, g)];
-      hi[g] = P.hi[P.at(i, g)];
-    }
+    for (int g = 0; g < NG; g++) P.get(i, g, lo[g], hi[g]);
     if (pbase) mul_elem_pb<NG>(pbase + (long)i * 32, lo, hi);  // (the stored factor is the postmultiply's)
     else mul_elem<NG>(T, lo, hi, kMod - err[i]);
-    uint32_t* dst = (uint32_t*)(base + shard * a.shard_stride);
+    uint8_t* dst = base + shard * a.shard_stride;
 #pragma unroll
-    for (int g = 0; g < NG; g++) {
-      dst[g] = lo[g];
-      dst[8 + g] = hi[g];
-    }
+    for (int g = 0; g < NG; g++) gstore<PK>(dst + 4 * g, lo[g], hi[g]);
   }
 }
 
@@ -758,8 +821,8 @@ hipError_t tables(WideTabs& out) {
         o[hi_dw] |= ((prod >> 8) & 0xFFu) << (8 * (e2 & 3));
       }
   }
-  std::vector<uint16_t> wf((size_t)wfold_offset(2 * 2 * kMaxK), 0);
-  for (int n = 2048; n <= 2 * kMaxK; n <<= 1) {
+  std::vector<uint16_t> wf((size_t)wfold_offset(2 * 2 * kMaxCodecK), 0);
+  for (int n = 2048; n <= 2 * kMaxCodecK; n <<= 1) {
     const long off = wfold_offset(n);
     for (int r = 0; r < n; r++) {
       uint64_t acc = 0;
@@ -786,10 +849,13 @@ hipError_t tables(WideTabs& out) {
 // Slice width per element count: S = 4 NG symbols, LDS = 2 planes x n x NGP
 // dwords <= 160 KiB.  Round 6: the widest slice that fits (n <= 2048: 32
 // symbols, 144 KiB; 4096: 16, 160 KiB; 8192: 8 without the pad dword, 128 KiB;
-// 16384: 4, 128 KiB), so that every skew table a unit loads, every
-// per-element errLocs table and every 64-B block's load serve more symbols
-// (round 5: 8 / 4 symbols at n = 4096 / 8192; profiles/gf16_wide_ab_r06.log).
-int slice_ng(int n) { return n <= 2048 ? 8 : n <= 4096 ? 4 : n <= 8192 ? 2 : 1; }
+// 16384: 4, 128 KiB; codec vectors 32768: 2 packed, 128 KiB; 65536: 1 packed,
+// 128 KiB), so that every skew table a unit loads, every per-element errLocs
+// table and every 64-B block's load serve more symbols (round 5: 8 / 4 symbols
+// at n = 4096 / 8192; profiles/gf16_wide_ab_r06.log).
+int slice_sym(int n) {
+  return n <= 2048 ? 32 : n <= 4096 ? 16 : n <= 8192 ? 8 : n <= 16384 ? 4 : n <= 32768 ? 2 : 1;
+}
 
 size_t lds_bytes(int n, int ng) {
   const int ngp = ng <= 2 ? ng : ng + 1;  // Planes<NG>::NGP
@@ -803,26 +869,29 @@ hipError_t lds_attr(K kernel, size_t bytes) {
                        : hipSuccess;
 }
 
-template <int NG, int G>
+template <int NG, int G, int PK = 0>
 hipError_t launch_enc(const EncodeArgs& a, const WideTabs& T, int k, hipStream_t s) {
-  const size_t lds = lds_bytes(k, NG);
-  hipError_t e = lds_attr(leo16w_encode_kernel<NG, G>, lds);
+  using PL = Planes<NG, PK>;
+  const size_t lds = PL::bytes(k);
+  hipError_t e = lds_attr(leo16w_encode_kernel<NG, G, PK>, lds);
   if (e != hipSuccess) return e;
-  const long blocks = a.nsq * a.nvec * (a.shard_bytes / 64) * (8 / NG);
+  const long blocks = a.nsq * a.nvec * (a.shard_bytes / 64) * (32 / PL::SYM);
   if (blocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL((leo16w_encode_kernel<NG, G>), dim3((unsigned)blocks), dim3(kWideThreads), lds, s, a, T, k);
+  hipLaunchKernelGGL((leo16w_encode_kernel<NG, G, PK>), dim3((unsigned)blocks), dim3(kWideThreads), lds, s, a, T, k);
   return hipGetLastError();
 }
 
-template <int NG, int G>
+template <int NG, int G, int PK = 0>
 hipError_t launch_dec(const DecodeArgs& a, const WideTabs& T, hipStream_t s) {
+  using PL = Planes<NG, PK>;
   const int n = 2 * a.k;
-  const size_t lds = lds_bytes(n, NG);
-  hipError_t e = lds_attr(leo16w_decode_kernel<NG, G>, lds);
+  const size_t lds = PL::bytes(n);
+  hipError_t e = lds_attr(leo16w_decode_kernel<NG, G, PK>, lds);
   if (e != hipSuccess) return e;
-  const long blocks = a.nsq * a.nvec * (a.shard_bytes / 64) * (8 / NG);
+  const long blocks = a.nsq * a.nvec * (a.shard_bytes / 64) * (32 / PL::SYM);
   if (blocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL((leo16w_decode_kernel<NG, G>), dim3((unsigned)blocks), dim3(dec_threads<NG>()), lds, s, a, T);
+  hipLaunchKernelGGL((leo16w_decode_kernel<NG, G, PK>), dim3((unsigned)blocks), dim3(dec_threads<NG>()), lds, s, a,
+                     T);
   return hipGetLastError();
 }
 
@@ -832,7 +901,7 @@ hipError_t launch_dec(const DecodeArgs& a, const WideTabs& T, hipStream_t s) {
 // the k = 1024 split square went 5.0 -> 7.2 ms; profiles/gf16_wide_ab_r06.log)
 constexpr int WG8 = 8, WG8E = 4;
 
-bool wide_k_ok(int k) { return k >= 256 && k <= kMaxK && (k & (k - 1)) == 0; }
+bool wide_k_ok(int k) { return k >= 256 && k <= kMaxCodecK && (k & (k - 1)) == 0; }
 
 }  // namespace
 
@@ -845,11 +914,15 @@ hipError_t leo16w_prepare() {
   if (e == hipSuccess) e = lds_attr(leo16w_encode_kernel<4, 4>, lds_bytes(4096, 4));
   if (e == hipSuccess) e = lds_attr(leo16w_encode_kernel<2, 2>, lds_bytes(8192, 2));
   if (e == hipSuccess) e = lds_attr(leo16w_encode_kernel<1, 1>, big);
+  if (e == hipSuccess) e = lds_attr(leo16w_encode_kernel<1, 1, 2>, Planes<1, 2>::bytes(kMaxCodecK));
   if (e == hipSuccess) e = lds_attr(leo16w_decode_kernel<8, WG8>, lds_bytes(2048, 8));
   if (e == hipSuccess) e = lds_attr(leo16w_decode_kernel<4, 4>, lds_bytes(4096, 4));
   if (e == hipSuccess) e = lds_attr(leo16w_decode_kernel<2, 2>, lds_bytes(8192, 2));
   if (e == hipSuccess) e = lds_attr(leo16w_decode_kernel<1, 1>, big);
-  if (e == hipSuccess) e = lds_attr(leo16w_errlocs_kernel, (size_t)4 * 2 * kMaxK);
+  if (e == hipSuccess) e = lds_attr(leo16w_decode_kernel<1, 1, 2>, Planes<1, 2>::bytes(2 * kMaxCodecK / 2));
+  if (e == hipSuccess) e = lds_attr(leo16w_decode_kernel<1, 1, 1>, Planes<1, 1>::bytes(2 * kMaxCodecK));
+  if (e == hipSuccess) e = lds_attr(leo16w_errlocs_kernel<uint32_t>, (size_t)4 * kMaxCodecK);
+  if (e == hipSuccess) e = lds_attr(leo16w_errlocs_kernel<uint16_t>, (size_t)2 * 2 * kMaxCodecK);
   return e;
 }
 
@@ -859,11 +932,12 @@ hipError_t launch_leo16w_encode(int k, const EncodeArgs& a, hipStream_t s) {
   WideTabs T;
   hipError_t e = tables(T);
   if (e != hipSuccess) return e;
-  switch (slice_ng(k)) {
-    case 8: return launch_enc<8, WG8E>(a, T, k, s);
-    case 4: return launch_enc<4, 4>(a, T, k, s);
-    case 2: return launch_enc<2, 2>(a, T, k, s);
-    default: return launch_enc<1, 1>(a, T, k, s);
+  switch (slice_sym(k)) {
+    case 32: return launch_enc<8, WG8E>(a, T, k, s);
+    case 16: return launch_enc<4, 4>(a, T, k, s);
+    case 8: return launch_enc<2, 2>(a, T, k, s);
+    case 4: return launch_enc<1, 1>(a, T, k, s);
+    default: return launch_enc<1, 1, 2>(a, T, k, s);  // m = 32768 (k + k = 65536 shards)
   }
 }
 
@@ -875,9 +949,17 @@ hipError_t launch_leo16w_errlocs(const DecodeArgs& a, hipStream_t s) {
   const long nv = a.nsq * a.nvec;
   if (nv <= 0) return hipSuccess;
   const int n = 2 * a.k;
+  if (n > 32768) {  // n = 65536: 16-bit words (128 KiB)
+    const size_t lds = (size_t)n * 2;
+    if ((e = lds_attr(leo16w_errlocs_kernel<uint16_t>, lds)) != hipSuccess) return e;
+    hipLaunchKernelGGL(leo16w_errlocs_kernel<uint16_t>, dim3((unsigned)nv), dim3(kFoldThreads), lds, s, a, T,
+                       wfold_offset(n));
+    return hipGetLastError();
+  }
   const size_t lds = (size_t)n * 4;
-  if ((e = lds_attr(leo16w_errlocs_kernel, lds)) != hipSuccess) return e;
-  hipLaunchKernelGGL(leo16w_errlocs_kernel, dim3((unsigned)nv), dim3(kFoldThreads), lds, s, a, T, wfold_offset(n));
+  if ((e = lds_attr(leo16w_errlocs_kernel<uint32_t>, lds)) != hipSuccess) return e;
+  hipLaunchKernelGGL(leo16w_errlocs_kernel<uint32_t>, dim3((unsigned)nv), dim3(kFoldThreads), lds, s, a, T,
+                     wfold_offset(n));
   return hipGetLastError();
 }
 
@@ -888,11 +970,13 @@ hipError_t launch_leo16w_decode_only(const DecodeArgs& a, hipStream_t s, bool ma
   if (e != hipSuccess) return e;
   const long nv = a.nsq * a.nvec;
   if (nv <= 0) return hipSuccess;
-  switch (slice_ng(2 * a.k)) {
-    case 8: e = launch_dec<8, WG8>(a, T, s); break;
-    case 4: e = launch_dec<4, 4>(a, T, s); break;
-    case 2: e = launch_dec<2, 2>(a, T, s); break;
-    default: e = launch_dec<1, 1>(a, T, s); break;
+  switch (slice_sym(2 * a.k)) {
+    case 32: e = launch_dec<8, WG8>(a, T, s); break;
+    case 16: e = launch_dec<4, 4>(a, T, s); break;
+    case 8: e = launch_dec<2, 2>(a, T, s); break;
+    case 4: e = launch_dec<1, 1>(a, T, s); break;
+    case 2: e = launch_dec<1, 1, 2>(a, T, s); break;  // codec k = 16384
+    default: e = launch_dec<1, 1, 1>(a, T, s); break;  // codec k = 32768
   }
   if (e != hipSuccess) return e;
   if (mark_present) {

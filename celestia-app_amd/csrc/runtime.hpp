@@ -265,3 +265,13 @@ inline int check_k(dagpu_ctx* ctx, uint64_t k) {
   }
   return DAGPU_OK;
 }
+
+// codec width (dagpu_encode / dagpu_decode): one vector, not a square
+inline int check_codec_k(dagpu_ctx* ctx, uint64_t k) {
+  if (!is_pow2(k)) return set_err(ctx, DAGPU_ERR_ARG, "codec width must be a power of two");
+  if (k > (uint64_t)kMaxCodecK) {
+    return set_err(ctx, DAGPU_ERR_UNSUPPORTED,
+                   "codec width k > " + std::to_string(kMaxCodecK) + " is not supported (Leopard: 65536 shards)");
+  }
+  return DAGPU_OK;
+}

@@ -67,10 +67,18 @@ int dagpu_version(void);
  * checks only that the share count is a power of two, and rsmt2d's LeoRSCodec
  * reports MaxChunks() = 32768 * 32768 (Leopard GF(2^16): 65536 shards); the EDS
  * of k = 8192 is 128 GiB, which fits one MI355X's 288 GB of HBM, and k = 16384
- * (512 GiB) does not, so every entry point returns DAGPU_ERR_UNSUPPORTED above
- * it.  A cgo LeoRSCodec.MaxChunks() over this library returns the square of it. */
+ * (512 GiB) does not, so every square entry point returns DAGPU_ERR_UNSUPPORTED
+ * above it. */
 #define DAGPU_MAX_SQUARE_WIDTH 8192
 uint32_t dagpu_max_square_width(void);
+
+/* Widest codec vector (k data shards) dagpu_encode / dagpu_decode serve:
+ * Leopard GF(2^16)'s limit, k + k = 65536 shards (klauspost/reedsolomon
+ * leopardFF16 New: dataShards + parityShards <= 65536).  A cgo
+ * LeoRSCodec.MaxChunks() over this library returns the square of it, as
+ * rsmt2d's own (32768 * 32768).  DAGPU_ERR_UNSUPPORTED above it. */
+#define DAGPU_MAX_CODEC_WIDTH 32768
+uint32_t dagpu_max_codec_width(void);
 
 /* Open a context on HIP device `device` (one context per GPU per process). */
 int dagpu_init(int device, dagpu_ctx** out);

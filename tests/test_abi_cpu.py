@@ -102,8 +102,10 @@ def test_max_square_width_and_codec_limits():
     text = open(HEADER).read()
     m = re.search(r"#define DAGPU_MAX_SQUARE_WIDTH (\d+)", text)
     assert m and int(m.group(1)) == L.dagpu_max_square_width() == 8192
+    m = re.search(r"#define DAGPU_MAX_CODEC_WIDTH (\d+)", text)
+    assert m and int(m.group(1)) == L.dagpu_max_codec_width() == 32768  # Leopard: 65536 shards
     codec = da.LeoRSCodec()
-    assert codec.max_chunks() == 8192 * 8192
+    assert codec.max_chunks() == 32768 * 32768  # rsmt2d LeoRSCodec.MaxChunks
     assert codec.name() == "Leopard"
 
 

@@ -1,4 +1,5 @@
-"""Squares and codec vectors wider than k = 512 (k = 1024 ... 8192): the
+"""Squares and codec vectors wider than k = 512 (k = 1024 ... 8192; codec
+vectors up to k = 32768): the
 LDS-slice GF(2^16) kernels of csrc/rs_gf16_wide.hip, the chunked DAH kernel
 and the width-generic Repair helpers.
 
@@ -64,12 +65,52 @@ def test_wide_decode_too_few_and_limits(ctx):
     k = 1024
     with pytest.raises(da.ErrTooFewShards):
         da.LeoRSCodec(ctx).decode([bytes(64)] * (k - 1) + [None] * (k + 1))
-    # beyond the widest square this library serves: an explicit error, not a fault
-    big = 2 * _abi.lib().dagpu_max_square_width()
+    # beyond Leopard's 65536 shards: an explicit error, not a fault
+    big = 2 * _abi.lib().dagpu_max_codec_width()
     d = np.zeros(big * 64, np.uint8)
     p = np.zeros_like(d)
     rc = ctx._L.dagpu_encode(ctx.handle, big, 1, 64, _abi.addr(d), _abi.addr(p))
     assert rc == _abi.ERR_UNSUPPORTED
+    assert ctx.last_error().startswith("codec width k > 32768")
+    pres = np.ones(2 * big, np.uint8)
+    rc = ctx._L.dagpu_decode(ctx.handle, big, 1, 64, _abi.addr(np.zeros(2 * big * 64, np.uint8)), _abi.addr(pres))
+    assert rc == _abi.ERR_UNSUPPORTED
+
+
+@pytest.mark.parametrize("k,shard,nvec", [(16384, 64, 2), (16384, 192, 1), (32768, 64, 1)])
+def test_codec_beyond_square_widths_matches_oracle(ctx, k, shard, nvec):
+    """rsmt2d.Codec widths no single-GPU square reaches (include/dagpu.h
+    DAGPU_MAX_CODEC_WIDTH; Leopard GF(2^16) serves k + k <= 65536 shards):
+    k = 16384 encodes on 4-symbol slices and decodes n = 32768 on 2-symbol
+    packed slices, k = 32768 encodes on 2-symbol and decodes n = 65536 on
+    1-symbol packed slices (16-bit locator words).  Bit-exact against the
+    oracle's GF(2^16) restatement (parity unpinned: no reference vector at
+    these widths); erasures: random k and k + 3 kept, data only, parity only."""
+    rng = np.random.default_rng(k + shard)
+    data = rng.integers(0, 256, (nvec, k, shard), dtype=np.uint8)
+    codec = da.LeoRSCodec(ctx)
+    par = codec.encode_batch(data)
+    full = []
+    for v in range(nvec):
+        ref = oracle.encode(data[v])
+        assert (par[v] == ref).all(), v
+        full.append(np.concatenate([data[v], ref]))
+    pats = [np.isin(np.arange(2 * k), rng.choice(2 * k, k + extra, replace=False)) for extra in (0, 3)]
+    pats += [np.arange(2 * k) < k, np.arange(2 * k) >= k]
+    for j, present in enumerate(pats):
+        present = present.astype(np.uint8)
+        damaged = full[0] * present[:, None]
+        if j == 0:
+            assert (oracle.decode(damaged, present) == full[0]).all()
+        got = codec.decode([damaged[i].tobytes() if present[i] else None for i in range(2 * k)])
+        assert b"".join(got) == full[0].tobytes(), j
+    if nvec > 1:
+        # two vectors with different patterns in one call (own locators each)
+        shards = np.stack(full)
+        pres = np.stack([pats[0], pats[1]]).astype(np.uint8)
+        buf = np.ascontiguousarray(shards * pres[:, :, None])
+        ctx.check(ctx._L.dagpu_decode(ctx.handle, k, nvec, shard, _abi.addr(buf), _abi.addr(pres)))
+        assert (buf == shards).all()
 
 
 @pytest.mark.parametrize("k", [256, 512])
