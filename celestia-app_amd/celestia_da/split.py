@@ -52,6 +52,9 @@ class SplitPart:
         L = ctx._L
         ws = L.dagpu_split_workspace_size(k, parts)
         if ws == 0:
+            if k == 2 * L.dagpu_max_square_width() and parts < 8:  # include/dagpu.h DAGPU_MAX_SPLIT_WIDTH
+                raise DAError(_abi.ERR_UNSUPPORTED,
+                              f"split square k = {k} needs >= 8 parts (its EDS is 512 GiB)")
             raise DAError(_abi.ERR_ARG, f"invalid split k={k} parts={parts}")
         u8 = dict(dtype=torch.uint8, device=device)
         self.ws = torch.empty(ws, **u8)

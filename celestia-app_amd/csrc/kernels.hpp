@@ -22,6 +22,12 @@ constexpr int kMaxK = 8192;
 // of the same width does not; the wide kernels serve k = 16384 / 32768 with
 // 2- / 1-symbol LDS slices (rs_gf16_wide.hip).
 constexpr int kMaxCodecK = 32768;
+// Widest split square (split.cpp, one oversized square over P GPUs): k = 16384,
+// whose 512 GiB EDS one GPU cannot hold, over P >= kMinWideSplitParts ranks
+// (P = 8: per rank a 64 GiB column slab, 32 GiB of row staging and send
+// block, ~38 GiB of forest records -- under 288 GB; P = 4 would not fit).
+constexpr int kMaxSplitK = 2 * kMaxK;
+constexpr int kMinWideSplitParts = 8;
 
 // Bytes of error-locator workspace per decoded vector.
 // Error-locator workspace per vector: GF(2^8) 256 B; GF(2^16) the n = 2k uint16

@@ -486,7 +486,7 @@ static bool dah_split_enabled() {  // DAGPU_DAH_SPLIT=0: one workgroup per squar
 
 hipError_t launch_dah(const SquareArgs& a, hipStream_t s) {
   const int n = 4 * a.k;
-  if (a.k > kMaxK) return hipErrorInvalidValue;
+  if (a.k > kMaxSplitK) return hipErrorInvalidValue;  // (k = 16384: split squares' finish step)
   if (a.digests && n >= 1024 && a.nsq < 64 && dah_split_enabled()) {
     // the digest buffer (w^2 * 32 B per square) holds the n / 64 subtree roots
     const int per = n / kDahSub;

@@ -261,7 +261,10 @@ inline int check_k(dagpu_ctx* ctx, uint64_t k) {
   if (!is_pow2(k)) return set_err(ctx, DAGPU_ERR_ARG, "square width must be a power of two");
   if (k > (uint64_t)kMaxK) {
     return set_err(ctx, DAGPU_ERR_UNSUPPORTED,
-                   "square width k > " + std::to_string(kMaxK) + " is not supported");
+                   "square width k > " + std::to_string(kMaxK) + " is not supported on one GPU" +
+                       (k <= (uint64_t)kMaxSplitK ? " (k = " + std::to_string(kMaxSplitK) +
+                                                        ": the split square over >= 8 GPUs, dagpu_split_*)"
+                                                  : ""));
   }
   return DAGPU_OK;
 }

@@ -32,9 +32,20 @@ namespace {
 
 size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
 
+// k <= kMaxK as every square entry point; k = kMaxSplitK only over at least
+// kMinWideSplitParts ranks (its EDS fits 8 GPUs, not fewer)
+bool wide_split(uint32_t k) { return k > (uint32_t)kMaxK && k <= (uint32_t)kMaxSplitK && is_pow2(k); }
+
 int check_split(dagpu_ctx* ctx, uint32_t k, uint32_t parts, uint32_t part) {
-  int rc = check_k(ctx, k);
-  if (rc) return rc;
+  if (wide_split(k)) {
+    if (parts < (uint32_t)kMinWideSplitParts)
+      return set_err(ctx, DAGPU_ERR_UNSUPPORTED,
+                     "split square k = " + std::to_string(k) + " needs >= " + std::to_string(kMinWideSplitParts) +
+                         " parts (its EDS is 512 GiB)");
+  } else {
+    int rc = check_k(ctx, k);
+    if (rc) return rc;
+  }
   if (!is_pow2(parts) || parts > k) return set_err(ctx, DAGPU_ERR_ARG, "parts must be a power of two <= k");
   if (part >= parts) return set_err(ctx, DAGPU_ERR_ARG, "part out of range");
   return DAGPU_OK;
@@ -94,6 +105,7 @@ extern "C" {
 
 size_t dagpu_split_workspace_size(uint32_t k, uint32_t parts) {
   if (k == 0 || parts == 0 || !is_pow2(k) || !is_pow2(parts) || parts > k) return 0;
+  if (k > (uint32_t)kMaxK && (!wide_split(k) || parts < (uint32_t)kMinWideSplitParts)) return 0;
   return split_ws_bytes(k, parts, nullptr, nullptr) + 256;
 }
 

@@ -62,8 +62,9 @@ typedef struct dagpu_ctx dagpu_ctx;
 /* Library version (major*10000 + minor*100 + patch). */
 int dagpu_version(void);
 
-/* Widest square (and codec width k = data shards per vector) this build
- * serves: DAGPU_MAX_SQUARE_WIDTH.  pkg/da ExtendShares (data_availability_header.go:65-75)
+/* Widest square one GPU serves: DAGPU_MAX_SQUARE_WIDTH (the split square
+ * goes to DAGPU_MAX_SPLIT_WIDTH over >= 8 GPUs, codec vectors to
+ * DAGPU_MAX_CODEC_WIDTH).  pkg/da ExtendShares (data_availability_header.go:65-75)
  * checks only that the share count is a power of two, and rsmt2d's LeoRSCodec
  * reports MaxChunks() = 32768 * 32768 (Leopard GF(2^16): 65536 shards); the EDS
  * of k = 8192 is 128 GiB, which fits one MI355X's 288 GB of HBM, and k = 16384
@@ -370,7 +371,12 @@ int dagpu_blob_commitments(dagpu_ctx* ctx, size_t nblobs, const uint8_t* namespa
  * synchronise it before reading the results.  With P = 1 the one
  * send block is rows 0..k-1 of the slab: pass the slab itself as d_send and
  * skip step 2 (the encoder then writes [Q0 | Q1] in place).
- * d_workspace: dagpu_split_workspace_size(k, P) bytes (0 = invalid k / P). */
+ * d_workspace: dagpu_split_workspace_size(k, P) bytes (0 = invalid k / P).
+ * Widths: every k up to DAGPU_MAX_SQUARE_WIDTH, and k = DAGPU_MAX_SPLIT_WIDTH
+ * (16384: a 512 GiB EDS, beyond one GPU) over P >= 8 parts -- per rank a 64 GiB
+ * column slab plus ~70 GiB of staging and forest records at P = 8;
+ * DAGPU_ERR_UNSUPPORTED (workspace size 0) for fewer parts or wider squares. */
+#define DAGPU_MAX_SPLIT_WIDTH 16384
 size_t dagpu_split_workspace_size(uint32_t k, uint32_t parts);
 int dagpu_split_rows_device(dagpu_ctx* ctx, uint32_t k, uint32_t parts, uint32_t part,
                             const uint8_t* d_ods_rows, uint8_t* d_send, int32_t* d_status,

@@ -132,3 +132,20 @@ def test_no_device_wait_on_later_queued_signals():
             if re.search(r"hipStreamWait(Value|Write)|hipStreamWriteValue|hipStreamBatchMemOp", code):
                 bad.append(f"{name}:{no}: {line.strip()}")
     assert not bad, bad
+
+
+def test_split_widths_host_side():
+    # k = 16384 (a 512 GiB EDS) only as a split square over >= 8 parts
+    # (include/dagpu.h DAGPU_MAX_SPLIT_WIDTH); host-only sizing, no GPU call
+    L = _abi.lib()
+    text = open(HEADER).read()
+    m = re.search(r"#define DAGPU_MAX_SPLIT_WIDTH (\d+)", text)
+    assert m and int(m.group(1)) == 2 * L.dagpu_max_square_width() == 16384
+    assert L.dagpu_split_workspace_size(8192, 1) > 0
+    assert L.dagpu_split_workspace_size(16384, 4) == 0
+    ws8 = L.dagpu_split_workspace_size(16384, 8)
+    # per rank at P = 8: row staging 32 GiB + leaf / column / row forest records
+    # ~38 GiB; with the 64 GiB slab and 32 GiB send block it stays under 288 GB
+    assert 64 << 30 < ws8 < 80 << 30, ws8
+    assert L.dagpu_split_workspace_size(16384, 64) > 0
+    assert L.dagpu_split_workspace_size(32768, 64) == 0
