@@ -417,21 +417,31 @@ __global__ __launch_bounds__(256) void node_gather_kernel(const uint8_t* nodes, 
 
 // Packed 90-B nodes (minNs | maxNs | digest) -> 96-B records (each field
 // zero padded to 32 B), one lane per node.
-__global__ __launch_bounds__(256) void node_to_rec_kernel(const uint8_t* nodes, long n, uint8_t* recs) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
+// One thread per output dword (24 per record): the byte-loop form (one thread
+// per record, 96 byte loads and stores that the compiler kept in order since the
+// buffers may alias) took 24 us for the 1,024 row roots of a k = 512 split square.
+__global__ __launch_bounds__(256) void node_to_rec_kernel(const uint8_t* __restrict__ nodes, long n,
+                                                          uint8_t* __restrict__ recs) {
+  const long t = (long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n * (kRecNmt / 4)) return;
+  const long i = t / (kRecNmt / 4);
+  const int j = (int)(t - i * (kRecNmt / 4));  // dword j of the record: field j / 8, bytes 4 (j % 8) ..
   const uint8_t* nd = nodes + i * kNodeSize;
-  uint8_t* r = recs + i * kRecNmt;
-  for (int b = 0; b < 32; b++) {
-    r[b] = b < 29 ? nd[b] : 0;
-    r[32 + b] = b < 29 ? nd[29 + b] : 0;
-    r[64 + b] = nd[58 + b];
+  const int f = j >> 3, off = 4 * (j & 7);
+  const uint8_t* src = nd + 29 * f;  // minNs, maxNs, then the digest at 58
+  uint32_t v = 0;
+#pragma unroll
+  for (int b = 0; b < 4; b++) {
+    const int o = off + b;
+    if (f == 2 || o < 29) v |= (uint32_t)src[o] << (8 * b);
   }
+  ((uint32_t*)(recs + i * kRecNmt))[j] = v;
 }
 
 hipError_t launch_node_to_rec(const uint8_t* nodes, long n, uint8_t* recs, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(node_to_rec_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, nodes, n, recs);
+  const long threads = n * (kRecNmt / 4);
+  hipLaunchKernelGGL(node_to_rec_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, nodes, n, recs);
   return hipGetLastError();
 }
 

@@ -1,0 +1,18 @@
+# Round 6, last session: GPU steps after the wide-codec / k = 16384 split work.
+# A/B steps expect celestia-app_amd/libdagpu_base.so built beforehand on the CPU
+# (tools/build_variant.sh base <rev>); delete it after the call.
+#   bash tools/gpu_r06b.sh <step>
+set -o pipefail
+mkdir -p gpurun_out
+case "$1" in
+  ab)  # node_to_rec per dword (split k = 512), wide-kernel templates (k = 2048 Repair / split), codec timings
+    timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_split.py tests/test_gpu_split16k.py > gpurun_out/r06b_ab_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/r06b_ab_tests.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 3 "bench:--mode split --split-k 512 --steps 40 --warmup 3" new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 1 "bench:--mode repair --k 2048 --batch 1 --steps 2 --warmup 1" new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 1 "bench:--mode split --split-k 2048 --steps 4 --warmup 1" new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    timeout -k 10 300 python -u tools/codec_wide.py 3 > gpurun_out/r06b_codec_wide.log 2>&1 && cat gpurun_out/r06b_codec_wide.log && \
+    cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_codec -o codec -- python3 -u tools/codec_wide.py 2 > gpurun_out/r06b_codec_prof.log 2>&1
+    ;;
+esac
