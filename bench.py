@@ -522,8 +522,14 @@ def main():
         out["other_configs"] = {
             "configs[2]_mixed_4096": run_mixed(ctx, 3, 1),
             # 10 timed steps (round 6; 3 before): round-over-round changes of a few
-            # per cent must be resolvable (verdict r05)
-            "configs[3]_repair_k128": run_repair(ctx, 128, 256, 10, 2),
+            # per cent must be resolvable (verdict r05).  The 256 squares as 4
+            # started repairs (dagpu_repair_start / _join, each slice's crossword on
+            # its own stream, so one slice's host turnarounds and last tree levels
+            # overlap another's kernels): 17.19-17.44 k vs 17.01-17.14 k squares/s
+            # as one batch, same box (profiles/repair_slices_ab_r06.log; 8 slices:
+            # 16.97-17.12 k, 16: 16.26-16.34 k); the one-batch call stays beside it.
+            "configs[3]_repair_k128": run_repair(ctx, 128, 256, 10, 2, slices=4),
+            "configs[3]_repair_k128_one_batch": run_repair(ctx, 128, 256, 10, 2),
             "repair_k512_gf16": run_repair(ctx, 512, 2, 10, 2),
             # the other maximal erasure pattern (Q3 only kept): the reverse fill's case
             "repair_k128_q3": run_repair(ctx, 128, 256, 10, 2, pattern="q3"),

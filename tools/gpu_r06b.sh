@@ -16,3 +16,12 @@ case "$1" in
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_codec -o codec -- python3 -u tools/codec_wide.py 2 > gpurun_out/r06b_codec_prof.log 2>&1
     ;;
 esac
+case "$1" in
+  slices)  # started-repair slices for the Repair lines (C4 k = 128 x 256, k = 512 x 2)
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 128 --batch 256 --steps 10 --warmup 2" s1= s2=args:--repair-slices\ 2 s4=args:--repair-slices\ 4 && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 512 --batch 2 --steps 10 --warmup 2" s1= s2=args:--repair-slices\ 2
+    ;;
+  slices8)  # more slices for C4
+    bash tools/gpu_ab.sh --rounds 3 "bench:--mode repair --k 128 --batch 256 --steps 10 --warmup 2" s1= s4=args:--repair-slices\ 4 s8=args:--repair-slices\ 8 s16=args:--repair-slices\ 16
+    ;;
+esac
