@@ -685,10 +685,9 @@ __global__ __launch_bounds__(kFoldThreads) void leo16w_errlocs_kernel(DecodeArgs
 // elements above e, so element chunks are processed in ascending order, each
 // reading before a barrier and writing after it.
 // ---------------------------------------------------------------------------
-template <int NG, int G, int PK = 0>
-__global__ __launch_bounds__(dec_threads<NG>()) void leo16w_decode_kernel(DecodeArgs a, WideTabs T) {
+template <int NG, int G, int PK = 0, int TH = dec_threads<NG>()>
+__global__ __launch_bounds__(TH) void leo16w_decode_kernel(DecodeArgs a, WideTabs T) {
   using PL = Planes<NG, PK>;
-  constexpr int TH = dec_threads<NG>();
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   constexpr int CH = NG / G;
   const int k = a.k, n = 2 * k;
@@ -881,17 +880,16 @@ hipError_t launch_enc(const EncodeArgs& a, const WideTabs& T, int k, hipStream_t
   return hipGetLastError();
 }
 
-template <int NG, int G, int PK = 0>
+template <int NG, int G, int PK = 0, int TH = dec_threads<NG>()>
 hipError_t launch_dec(const DecodeArgs& a, const WideTabs& T, hipStream_t s) {
   using PL = Planes<NG, PK>;
   const int n = 2 * a.k;
   const size_t lds = PL::bytes(n);
-  hipError_t e = lds_attr(leo16w_decode_kernel<NG, G, PK>, lds);
+  hipError_t e = lds_attr(leo16w_decode_kernel<NG, G, PK, TH>, lds);
   if (e != hipSuccess) return e;
   const long blocks = a.nsq * a.nvec * (a.shard_bytes / 64) * (32 / PL::SYM);
   if (blocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL((leo16w_decode_kernel<NG, G, PK>), dim3((unsigned)blocks), dim3(dec_threads<NG>()), lds, s, a,
-                     T);
+  hipLaunchKernelGGL((leo16w_decode_kernel<NG, G, PK, TH>), dim3((unsigned)blocks), dim3(TH), lds, s, a, T);
   return hipGetLastError();
 }
 

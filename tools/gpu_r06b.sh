@@ -25,3 +25,10 @@ case "$1" in
     bash tools/gpu_ab.sh --rounds 3 "bench:--mode repair --k 128 --batch 256 --steps 10 --warmup 2" s1= s4=args:--repair-slices\ 4 s8=args:--repair-slices\ 8 s16=args:--repair-slices\ 16
     ;;
 esac
+case "$1" in
+  w2)  # k = 2048 decoder: 8-symbol slices at 512 threads (two workgroups per CU) vs 16 at 1,024 (one)
+    DAGPU_LIB=celestia-app_amd/libdagpu_w2.so timeout -k 10 600 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_wide.py -k "k2048 or decode_matches or codec_beyond" > gpurun_out/r06b_w2_tests.log 2>&1
+    rc=$?; echo "w2 tests rc=$rc"; tail -2 gpurun_out/r06b_w2_tests.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 2048 --batch 1 --steps 3 --warmup 1" new= w2=lib:celestia-app_amd/libdagpu_w2.so
+    ;;
+esac
