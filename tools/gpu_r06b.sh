@@ -32,3 +32,12 @@ case "$1" in
     bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 2048 --batch 1 --steps 3 --warmup 1" new= w2=lib:celestia-app_amd/libdagpu_w2.so
     ;;
 esac
+case "$1" in
+  init)  # fused Repair start-up (one init launch, known[] from the completeness kernels) + roots queued ahead of the deferred-axis read
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py tests/test_gpu_repair_async.py tests/test_gpu_parity.py tests/test_gpu_gf16.py > gpurun_out/r06b_init_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r06b_init_tests.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 3 repair512 new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 128 --batch 256 --steps 10 --warmup 2" new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 2 repair512q3 new= base=lib:celestia-app_amd/libdagpu_base.so
+    ;;
+esac
