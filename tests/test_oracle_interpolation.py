@@ -67,3 +67,39 @@ def test_leopard_encode_is_interpolation(k, bits):
     data[0, :5] = 0  # zero symbols take the no-log path
     par = oracle.encode(data)
     assert (_symbols(par, bits) == _interpolate(_symbols(data, bits), bits)).all()
+
+
+def _gmul(a: int, b: int, poly: int, bits: int) -> int:
+    r = 0
+    while b:
+        if b & 1:
+            r ^= a
+        b >>= 1
+        a <<= 1
+        if a >> bits:
+            a ^= poly
+    return r
+
+
+@pytest.mark.parametrize("bits,poly,basis", [
+    (8, 0x11D, [1, 214, 152, 146, 86, 200, 88, 230]),
+    (16, 0x1002D, [0x0001, 0xACCA, 0x3C0E, 0x163E, 0xC582, 0xED2E, 0x914C, 0x4012,
+                   0x6C98, 0x10D8, 0x6A72, 0xB900, 0xFDB8, 0xFB34, 0xFF38, 0x991E]),
+])
+def test_field_parameters_are_consistent(bits, poly, basis):
+    """The recalled field parameters (the tables of
+    oracle/da_oracle.c and csrc/gf16_host.hpp) have the properties Leopard's
+    construction needs: a primitive polynomial (x has order 2^bits - 1) and a
+    Cantor basis (beta_0 = 1, beta_i^2 + beta_i = beta_{i-1}).  GF(2^8)'s are
+    pinned by the reference goldens; for GF(2^16) this is consistency, not a pin
+    (each beta_i has two candidate roots)."""
+    x, order = 1, 0
+    while True:
+        x = _gmul(x, 2, poly, bits)
+        order += 1
+        if x == 1:
+            break
+    assert order == (1 << bits) - 1
+    assert basis[0] == 1
+    for i in range(1, bits):
+        assert _gmul(basis[i], basis[i], poly, bits) ^ basis[i] == basis[i - 1], i
