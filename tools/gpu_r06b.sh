@@ -27,6 +27,7 @@ case "$1" in
 esac
 case "$1" in
   w2)  # k = 2048 decoder: 8-symbol slices at 512 threads (two workgroups per CU) vs 16 at 1,024 (one)
+        # (historical: the DAGPU_WIDE4096_NG2 switch was removed after this A/B lost; profiles/wide2048_ng2_ab_r06.log)
     DAGPU_LIB=celestia-app_amd/libdagpu_w2.so timeout -k 10 600 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_wide.py -k "k2048 or decode_matches or codec_beyond" > gpurun_out/r06b_w2_tests.log 2>&1
     rc=$?; echo "w2 tests rc=$rc"; tail -2 gpurun_out/r06b_w2_tests.log; [ $rc -eq 0 ] || exit $rc
     bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 2048 --batch 1 --steps 3 --warmup 1" new= w2=lib:celestia-app_amd/libdagpu_w2.so
@@ -34,6 +35,7 @@ case "$1" in
 esac
 case "$1" in
   init)  # fused Repair start-up (one init launch, known[] from the completeness kernels) + roots queued ahead of the deferred-axis read
+        # (historical: the change was reverted after this A/B, within noise; profiles/repair_init_ab_r06.log)
     timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py tests/test_gpu_repair_async.py tests/test_gpu_parity.py tests/test_gpu_gf16.py > gpurun_out/r06b_init_tests.log 2>&1
     rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r06b_init_tests.log; [ $rc -eq 0 ] || exit $rc
     bash tools/gpu_ab.sh --rounds 3 repair512 new= base=lib:celestia-app_amd/libdagpu_base.so && \
