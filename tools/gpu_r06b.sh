@@ -43,3 +43,8 @@ case "$1" in
     bash tools/gpu_ab.sh --rounds 2 repair512q3 new= base=lib:celestia-app_amd/libdagpu_base.so
     ;;
 esac
+case "$1" in
+  slices_n)  # C4: started-repair slice counts around 4
+    bash tools/gpu_ab.sh --rounds 3 "bench:--mode repair --k 128 --batch 256 --steps 10 --warmup 2" s1= s3=args:--repair-slices\ 3 s4=args:--repair-slices\ 4 s5=args:--repair-slices\ 5 s6=args:--repair-slices\ 6
+    ;;
+esac
