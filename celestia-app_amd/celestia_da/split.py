@@ -204,3 +204,44 @@ def _extend_split_distributed(dist, part, ods_rows, group, stream):
     status = max_status(dist, part.status, group)
     _check_status(status)
     return rr, col_all, dah
+
+
+# ---- width routing (ExtendShares above one GPU's widest square) -------------
+
+MIN_WIDE_PARTS = 8  # include/dagpu.h DAGPU_MAX_SPLIT_WIDTH: k = 16384 over >= 8 parts
+
+
+def route(k: int, world: int) -> str:
+    """Where `da.ExtendShares` of width k runs on a job of `world` GPUs
+    (pkg/da/data_availability_header.go:65-75 puts no upper bound on k):
+    "single" -- each rank extends whole squares (k <= dagpu_max_square_width());
+    "split"  -- the square is split over all ranks (k = 16384 needs >= 8).
+    Raises DAError(ERR_UNSUPPORTED) where neither path serves k."""
+    if k < 1 or k & (k - 1):
+        raise DAError(_abi.ERR_ARG, f"square width must be a power of two: got {k}")
+    L = _abi.lib()
+    if k <= L.dagpu_max_square_width():
+        return "single"
+    if k == 2 * L.dagpu_max_square_width() and world >= MIN_WIDE_PARTS and world & (world - 1) == 0:
+        return "split"
+    raise DAError(_abi.ERR_UNSUPPORTED,
+                  f"square width k = {k} needs the split path over >= {MIN_WIDE_PARTS} GPUs (a power of two); "
+                  f"this job has {world}" if k == 2 * L.dagpu_max_square_width()
+                  else f"square width k = {k} is not supported (widest: {2 * L.dagpu_max_square_width()})")
+
+
+def extend_wide_distributed(dist, k: int, ods_rows: torch.Tensor, ctx: Context, group=None,
+                            stream=None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """ExtendShares + NewDataAvailabilityHeader of one square wider than a
+    single GPU serves: this rank's k / world Q0 rows in, the square's row roots,
+    column roots and DAH out (identical on every rank).  The part's buffers
+    live for the call only (a 64 GiB slab per rank at k = 16384, P = 8)."""
+    world = dist.get_world_size(group) if dist is not None else 1
+    rank = dist.get_rank(group) if dist is not None else 0
+    if route(k, world) != "split":
+        raise DAError(_abi.ERR_ARG, f"k = {k} fits one GPU: use the single-GPU entry points")
+    part = SplitPart(k, world, rank, ctx, ods_rows.device)
+    try:
+        return extend_split_distributed(dist, part, ods_rows, group, stream)
+    finally:
+        del part

@@ -149,3 +149,15 @@ def test_split_widths_host_side():
     assert 64 << 30 < ws8 < 80 << 30, ws8
     assert L.dagpu_split_workspace_size(16384, 64) > 0
     assert L.dagpu_split_workspace_size(32768, 64) == 0
+
+
+def test_split_route_host_side():
+    from celestia_da import split
+    assert split.route(128, 1) == "single" and split.route(8192, 8) == "single"
+    assert split.route(16384, 8) == "split" and split.route(16384, 64) == "split"
+    for k, world in ((16384, 4), (16384, 1), (16384, 12), (32768, 64)):
+        with pytest.raises(da.DAError) as e:
+            split.route(k, world)
+        assert e.value.code == _abi.ERR_UNSUPPORTED, (k, world)
+    with pytest.raises(da.DAError):
+        split.route(100, 8)
