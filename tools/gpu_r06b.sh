@@ -48,3 +48,16 @@ case "$1" in
     bash tools/gpu_ab.sh --rounds 3 "bench:--mode repair --k 128 --batch 256 --steps 10 --warmup 2" s1= s3=args:--repair-slices\ 3 s4=args:--repair-slices\ 4 s5=args:--repair-slices\ 5 s6=args:--repair-slices\ 6
     ;;
 esac
+case "$1" in
+  roots2)  # Repair verification: the second half's roots on a side stream behind the first half's leaves
+        # (historical: reverted after this A/B; profiles/repair_roots2_ab_r06.log)
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_repair_fill.py tests/test_gpu_repair_byz.py tests/test_gpu_repair_async.py tests/test_gpu_gf16.py tests/test_gpu_parity.py > gpurun_out/r06b_roots2_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r06b_roots2_tests.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 600 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_wide.py -k "repair or k4096" > gpurun_out/r06b_roots2_wide.log 2>&1
+    rc=$?; echo "wide rc=$rc"; tail -2 gpurun_out/r06b_roots2_wide.log; [ $rc -eq 0 ] || exit $rc
+    bash tools/gpu_ab.sh --rounds 3 "bench:--mode repair --k 512 --batch 2 --steps 10 --warmup 2" new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 512 --batch 2 --steps 10 --warmup 2 --pattern q3" new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 2 "bench:--mode repair --k 256 --batch 8 --steps 10 --warmup 2" new= base=lib:celestia-app_amd/libdagpu_base.so && \
+    bash tools/gpu_ab.sh --rounds 1 "bench:--mode repair --k 1024 --batch 2 --steps 3 --warmup 1" new= base=lib:celestia-app_amd/libdagpu_base.so
+    ;;
+esac
