@@ -536,9 +536,12 @@ def main():
             "repair_k512_gf16_q3": run_repair(ctx, 512, 2, 10, 2, pattern="q3"),
             # configs[4] stress square through the split path at P = 1 (the N > 1 line
             # carries the same square split over every rank as split_stress)
-            # 20 steps: at 5 the first step's launch latency was ~7 % of a 1.4-ms square
-            "configs[4]_split_k256": bench_split(None, 0, 1, local, ctx, 256, 20, 3),
-            "configs[4]_split_k512": bench_split(None, 0, 1, local, ctx, 512, 20, 3),
+            # 40 steps (round 6; 20 before, 5 before that): each step ends in the
+            # status read-back, so the next step's first launch latency is in every
+            # step; more steps only steady the mean (split k = 512 1.199 ms at 20,
+            # 1.177-1.187 at 40, profiles/split_n2r_ab_r06.log)
+            "configs[4]_split_k256": bench_split(None, 0, 1, local, ctx, 256, 40, 3),
+            "configs[4]_split_k512": bench_split(None, 0, 1, local, ctx, 512, 40, 3),
         }
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.cpu_threads or host_threads())
