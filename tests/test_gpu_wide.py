@@ -250,9 +250,10 @@ def test_dah_chunked_kernel_k1024(ctx, monkeypatch):
     torch.cuda.empty_cache()
 
 
-def _wide_square_checks(ds, ods, k, rng, n_rows=2, n_cols=2):
+def _wide_square_checks(ds, ods, k, rng, n_rows=2, n_cols=2, n_roots=0):
     """Sampled rows and columns of every quadrant against the oracle's encoder,
-    sampled roots against the oracle's wrapper tree, the DAH from all roots."""
+    sampled roots against the oracle's wrapper tree (the four corner axes plus
+    n_roots random ones), the DAH from all roots."""
     w = 2 * k
     e = ds.eds.view(w, w, 512)
     q0 = ods.reshape(k, k, 512)
@@ -265,9 +266,22 @@ def _wide_square_checks(ds, ods, k, rng, n_rows=2, n_cols=2):
     rr = ds.row_roots[0].cpu().numpy()
     cr = ds.col_roots[0].cpu().numpy()
     assert bytes(ds.dah[0].cpu().numpy()) == oracle.dah_hash(rr, cr)
-    for ax, idx in ((0, 1), (0, w - 2), (1, 0), (1, w - 1)):
+    axes = [(0, 1), (0, w - 2), (1, 0), (1, w - 1)]
+    axes += [(int(rng.integers(2)), int(rng.integers(w))) for _ in range(n_roots)]
+    for ax, idx in axes:
         vec = (e[idx] if ax == 0 else e[:, idx]).cpu().numpy()
         assert (rr if ax == 0 else cr)[idx].tobytes() == _axis_root(vec, idx, k), (ax, idx)
+
+
+def _q3_identity(ctx, ds, k, rows=512):
+    """Every row of Q3 equals its Q2 row encoded through the codec (the column
+    pass built Q3 from the columns of Q1): the whole quadrant, in row slabs."""
+    w = 2 * k
+    e = ds.eds.view(w, w, 512)
+    codec = da.LeoRSCodec(ctx)
+    for r0 in range(k, w, rows):
+        q2 = np.ascontiguousarray(e[r0:r0 + rows, :k].cpu().numpy())
+        assert (codec.encode_batch(q2) == e[r0:r0 + rows, k:].cpu().numpy()).all(), r0
 
 
 def _max_erasure_repair(ctx, ds, k, rng, ref=None):
@@ -295,8 +309,8 @@ def _max_erasure_repair(ctx, ds, k, rng, ref=None):
 
 def test_wide_k4096_square(ctx):
     """k = 4096 (32 GiB EDS, device-resident, ODS in place): sampled vectors of
-    every quadrant and sampled roots against the oracle, the DAH from all 16,384
-    roots, then a maximal-erasure Repair (a random 4096 x 4096 sub-grid kept)
+    every quadrant and 16 sampled roots against the oracle, the Q3 identity over
+    all 4,096 rows of Q3, the DAH from all 16,384 roots, then a maximal-erasure Repair (a random 4096 x 4096 sub-grid kept)
     that restores every EDS byte and re-verifies every root."""
     k = 4096
     ds = DeviceSquares(k, 1, ctx=ctx, in_place=True)
@@ -306,7 +320,8 @@ def test_wide_k4096_square(ctx):
     torch.cuda.synchronize()
     assert int(ds.status[0]) == 0
     rng = np.random.default_rng(4096)
-    _wide_square_checks(ds, ods, k, rng)
+    _wide_square_checks(ds, ods, k, rng, n_rows=4, n_cols=4, n_roots=12)
+    _q3_identity(ctx, ds, k)  # verdict r05: more than sampled vectors at this width
     ref = ds.eds.clone()
     ds.workspace = None  # the repair brings its own
     torch.cuda.empty_cache()
@@ -317,8 +332,8 @@ def test_wide_k4096_square(ctx):
 
 def test_wide_k8192_square(ctx):
     """k = 8192, the widest square one MI355X serves (128 GiB EDS): sampled
-    vectors of every quadrant and sampled roots against the oracle, the DAH
-    from all 32,768 roots; then a maximal-erasure Repair in place whose status
+    vectors of every quadrant and sampled roots against the oracle, the Q3
+    identity over all 8,192 rows of Q3, the DAH from all 32,768 roots; then a maximal-erasure Repair in place whose status
     proves every root re-verified, and sampled rows against the ODS / oracle."""
     k = 8192
     w = 2 * k
@@ -330,8 +345,10 @@ def test_wide_k8192_square(ctx):
     print("k=8192: extended", flush=True)
     assert int(ds.status[0]) == 0
     rng = np.random.default_rng(8192)
-    _wide_square_checks(ds, ods, k, rng, n_rows=1, n_cols=2)
+    _wide_square_checks(ds, ods, k, rng, n_rows=1, n_cols=2, n_roots=4)
     print("k=8192: sampled vectors, roots and DAH checked", flush=True)
+    _q3_identity(ctx, ds, k, rows=256)
+    print("k=8192: Q3 identity over all rows checked", flush=True)
     ds.workspace = None
     torch.cuda.empty_cache()
     _max_erasure_repair(ctx, ds, k, rng)
