@@ -196,15 +196,13 @@ def test_wide_k2048_properties(ctx):
     for c in rng.choice(w, 2, replace=False):  # Q2 / Q3 columns = Encode([Q0|Q1] columns)
         col = e[:, c].cpu().numpy()
         assert (col[k:] == oracle.encode(np.ascontiguousarray(col[:k]))).all()
-    # Q3 identity: rows of Q2 encode to the rows of Q3 (the column pass built Q3)
-    rows = rng.choice(np.arange(k, w), 8, replace=False)
-    q2 = np.ascontiguousarray(e[rows, :k].cpu().numpy())
-    assert (da.LeoRSCodec(ctx).encode_batch(q2) == e[rows, k:].cpu().numpy()).all()
+    # Q3 identity: rows of Q2 encode to the rows of Q3 (the column pass built Q3), every row
+    _q3_identity(ctx, ds, k)
     # roots: sampled axes against the oracle, DAH from all roots
     rr = ds.row_roots[0].cpu().numpy()
     cr = ds.col_roots[0].cpu().numpy()
     assert bytes(ds.dah[0].cpu().numpy()) == oracle.dah_hash(rr, cr)
-    for ax, idx in ((0, 0), (0, w - 1), (1, 1), (1, k + 3)):
+    for ax, idx in [(0, 0), (0, w - 1), (1, 1), (1, k + 3)] + [(int(rng.integers(2)), int(rng.integers(w))) for _ in range(8)]:
         vec = (e[idx] if ax == 0 else e[:, idx]).cpu().numpy()
         got = (rr if ax == 0 else cr)[idx].tobytes()
         assert got == _axis_root(vec, idx, k), (ax, idx)
